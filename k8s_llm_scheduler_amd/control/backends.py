@@ -1,0 +1,94 @@
+"""Decision backends: what answers the chat request the reference sends to HuggingFace
+(``scheduler.py:425-433``).
+
+* :class:`ScriptedBackend`  -- the FakeEngine of SURVEY.md section 4 (T2): scripted texts,
+  exceptions, hangs, per-call callables.  Used by tests and by the fault-injection hook.
+* :class:`LocalEngineBackend` -- the in-process Llama decision engine on MI355X
+  (``engine.LLMEngine``): chat template + tokenize, continuous-batched prefill/decode,
+  detokenize.  Enforces ``llm.timeout`` as a per-call deadline.
+* ``None`` (no backend) -- "LLM disabled": the decision service falls back immediately
+  (BASELINE config 1, CPU-only plumbing).
+"""
+
+from __future__ import annotations
+
+import threading
+import time
+from typing import Callable, List, Optional, Sequence, Union
+
+from .decision import GenerationRequest
+
+Script = Union[str, BaseException, Callable[[GenerationRequest], str], "Hang"]
+
+
+class Hang:
+    """Script entry that blocks for ``seconds`` (then raises TimeoutError) - an engine hang."""
+
+    def __init__(self, seconds: float):
+        self.seconds = seconds
+
+
+class ScriptedBackend:
+    name = "scripted"
+
+    def __init__(self, script: Sequence[Script] = (), default: Optional[Script] = None):
+        self._script: List[Script] = list(script)
+        self.default = default
+        self.calls: List[List[GenerationRequest]] = []
+        self._lock = threading.Lock()
+
+    def push(self, *entries: Script) -> None:
+        with self._lock:
+            self._script.extend(entries)
+
+    def _next(self) -> Optional[Script]:
+        with self._lock:
+            return self._script.pop(0) if self._script else self.default
+
+    def complete(self, requests: Sequence[GenerationRequest]) -> List[str]:
+        self.calls.append(list(requests))
+        out: List[str] = []
+        for r in requests:
+            entry = self._next()
+            if entry is None:
+                raise RuntimeError("scripted backend exhausted")
+            if isinstance(entry, BaseException):
+                raise entry
+            if isinstance(entry, Hang):
+                limit = r.deadline_s if r.deadline_s is not None else entry.seconds
+                time.sleep(min(entry.seconds, limit))
+                raise TimeoutError(f"engine did not answer within {limit}s")
+            out.append(entry(r) if callable(entry) else str(entry))
+        return out
+
+
+def first_node_answer(req: GenerationRequest) -> str:
+    """A well-formed answer naming the first node listed in the prompt (LLM-success path)."""
+    marker = "VALID NODE NAMES: "
+    line = req.user[req.user.index(marker) + len(marker):].split("\n", 1)[0]
+    node = line.split(", ")[0]
+    return ('{"selected_node": "%s", "confidence": 0.85, "reasoning": "Lowest utilisation"}' % node)
+
+
+class LocalEngineBackend:
+    """Adapter from chat requests to the in-process engine (engine.LLMEngine)."""
+
+    name = "local"
+
+    def __init__(self, engine, ignore_eos: Optional[bool] = None):
+        self.engine = engine
+        self.ignore_eos = ignore_eos
+
+    def complete(self, requests: Sequence[GenerationRequest]) -> List[str]:
+        from ..engine.sampling import SamplingParams
+
+        deadline = None
+        if requests and requests[0].deadline_s:
+            deadline = time.monotonic() + float(requests[0].deadline_s)
+        prompts, params = [], []
+        for r in requests:
+            prompts.append(self.engine.render_chat(r.system, r.user))
+            params.append(SamplingParams(max_tokens=r.max_tokens, temperature=r.temperature, top_p=r.top_p,
+                                         ignore_eos=bool(self.ignore_eos)))
+        outs = self.engine.generate(prompts, params, deadline=deadline)
+        return [o.text for o in outs]
