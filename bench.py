@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Headline benchmark: scheduling decisions/s + p50 decision latency, Llama-3.3-70B, TP = N.
+
+BASELINE.json metric: "scheduling decisions/sec + p50 decision latency, Llama-3.3-70B local TP=8".
+One *step* is one complete scheduling decision of the reference's per-pod pipeline
+(scheduler.py:690-729) minus the apiserver round trips: pod spec -> prompt (exact reference
+template, 3-node kind cluster as in ai-test-pods.yaml) -> decision service (cache disabled,
+breaker, retries) -> Llama-3 chat template + tokenize -> prefill (paged KV, prefix cache) ->
+decode of a FIXED number of tokens (default 64 ~ one JSON answer; EOS ignored because the
+weights are random) -> detokenize -> JSON extraction -> validation/fallback.
+
+Weights: Llama-3.3-70B architecture, deterministic random init, bf16 (no checkpoint offline).
+Data: synthetic cluster snapshots and pods.  Parallelism: one process per GPU (torchrun),
+tensor parallel over RCCL; decisions are made by all ranks together, so the job value is the
+decision rate itself.  Scaling is "strong" (fixed work per decision, more GPUs).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--preset llama-3.3-70b] [--gen-tokens 64]
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import random
+import statistics
+import sys
+import time
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+BASELINE_DECISIONS_PER_S = 0.3   # implied by test_e2e.py:68-75 (3 pods within 10 s); BASELINE.md
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--preset", default="llama-3.3-70b")
+    ap.add_argument("--nodes", type=int, default=3, help="cluster size in the prompt (reference: 3-node kind)")
+    ap.add_argument("--gen-tokens", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=1, help="pods decided per step (1 = reference single-pod loop)")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from k8s_llm_scheduler_amd.control import DecisionService, LocalEngineBackend
+    from k8s_llm_scheduler_amd.control.breaker import CircuitBreaker
+    from k8s_llm_scheduler_amd.control.prompt import PromptEngine
+    from k8s_llm_scheduler_amd.engine import build_engine
+    from k8s_llm_scheduler_amd.engine.synthetic import random_nodes, random_pod, reference_cluster
+    from k8s_llm_scheduler_amd.parallel import init_from_env
+
+    logging.basicConfig(level=logging.WARNING, format="%(asctime)s %(levelname)s %(message)s")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    tp = init_from_env("cuda")
+    rank = tp.rank
+
+    t_init = time.perf_counter()
+    bs = 16
+    per_seq = 2048 + args.gen_tokens + bs
+    eng = build_engine(args.preset, tp=tp, max_batch=max(1, args.batch), block_size=bs,
+                       num_blocks=max(args.batch, 2) * (per_seq // bs + 2) + 64,
+                       max_model_len=args.max_model_len, cuda_graphs=not args.no_graphs,
+                       prefix_caching=not args.no_prefix_cache, capture=False, decode_chunk=8)
+    if eng.use_graphs:
+        eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= max(1, args.batch)] or [1])
+    torch.cuda.synchronize()
+    init_s = time.perf_counter() - t_init
+
+    backend = LocalEngineBackend(eng, ignore_eos=True)
+    svc = DecisionService(backend, max_retries=3, max_tokens=args.gen_tokens, temperature=0.3, top_p=1.0,
+                          timeout=None, cache=None, breaker=CircuitBreaker())
+    pe = PromptEngine()
+    rng = random.Random(1234)
+    base_nodes, base_pods = reference_cluster(args.nodes)
+
+    def make_items():
+        items = []
+        for _ in range(args.batch):
+            nodes = base_nodes if args.nodes == 3 else random_nodes(rng, args.nodes)
+            # vary utilisation a little so no two snapshots are identical (cache is off anyway)
+            for n in nodes:
+                n.pod_count = rng.randint(2, 12)
+                n.cpu_usage_percent = n.memory_usage_percent = n.pod_count / n.max_pods * 50
+            pod = rng.choice(base_pods) if rng.random() < 0.5 else random_pod(rng)
+            items.append((pe.construct_scheduling_prompt(pod, nodes), pod, list(nodes)))
+        return items
+
+    prompt_tokens = len(eng.render_chat(svc.system_message, make_items()[0][0]))
+
+    def barrier():
+        if tp.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        svc.decide_many(make_items())
+    eng.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in eng.stats.items()})
+    lat = []
+    barrier()
+    t0 = time.perf_counter()
+    fallbacks = 0
+    for _ in range(args.steps):
+        s0 = time.perf_counter()
+        ds = svc.decide_many(make_items())
+        lat.append(time.perf_counter() - s0)
+        fallbacks += sum(d.fallback_needed for d in ds)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if tp.world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    decisions = args.steps * args.batch
+    value = decisions / elapsed
+    st = eng.stats
+    dec_tok_ms = 1000 * st["decode_time"] / max(1, st["decode_steps"])
+    res = {
+        "metric": "scheduling_decisions_per_sec",
+        "value": round(value, 4),
+        "unit": "decisions/s",
+        "n_gpus": tp.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": round(value / BASELINE_DECISIONS_PER_S, 3),
+        "dtype": "bf16",
+        "data": "synthetic cluster-state prompts, random-init weights",
+        "config": {
+            "model": f"{args.preset} (Llama-3.3-70B-Instruct architecture)" if "70b" in args.preset else args.preset,
+            "global_batch": args.batch,
+            "seq_len": prompt_tokens + args.gen_tokens,
+            "prompt_tokens": prompt_tokens,
+            "gen_tokens": args.gen_tokens,
+            "cluster_nodes": args.nodes,
+            "parallelism": f"tp{tp.world}",
+            "cuda_graphs": eng.use_graphs,
+            "prefix_cache": not args.no_prefix_cache,
+        },
+        "p50_decision_latency_ms": round(1000 * statistics.median(lat), 2),
+        "p99_decision_latency_ms": round(1000 * sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))], 2),
+        "decode_ms_per_step": round(dec_tok_ms, 3),
+        "prefill_ms_per_decision": round(1000 * st["prefill_time"] / max(1, args.steps), 2),
+        "prefill_tokens_per_decision": round(st["prefill_tokens"] / max(1, decisions), 1),
+        "fallback_rate": round(fallbacks / decisions, 3),
+        "init_s": round(init_s, 1),
+        "baseline_note": "BASELINE.md publishes no numbers; vs_baseline uses the implied 0.3 decisions/s of test_e2e.py",
+    }
+    if rank == 0:
+        line = json.dumps(res)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if tp.world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,132 @@
+// pybind11 module `_C`: launchers for the gfx950 kernels + native runtime classes.
+//
+// Tensors cross the boundary as raw device pointers (Python passes tensor.data_ptr()); shape and
+// dtype checks live in the Python wrappers (k8s_llm_scheduler_amd/ops/__init__.py).  Kernels are
+// launched on the CURRENT PyTorch HIP stream (queried through c10), so they are captured by
+// torch.cuda.CUDAGraph (= hipGraph) like any PyTorch op.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstdint>
+#include <string>
+
+#include "runtime/block_allocator.h"
+
+namespace py = pybind11;
+
+extern "C" {
+void* k8s_current_stream();
+int k8s_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows, int H, float eps, hipStream_t s);
+int k8s_rope_kv_write(void* q_out, void* k_cache, void* v_cache, const void* qkv, const float* cos_sin,
+                      const int* positions, const int* slot_mapping, const int* context_lens, const int* block_tables,
+                      int max_blocks, int block_size, int T, int nq, int nkv, int D, hipStream_t s);
+int k8s_paged_decode_attention(void* out, void* part_acc, void* part_ml, const void* q, const void* k_cache,
+                               const void* v_cache, const int* block_tables, const int* context_lens, float scale,
+                               int B, int nq, int nkv, int D, int block_size, int max_blocks, int part, int pmax,
+                               hipStream_t s);
+int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, const void* v_cache, const int* cu_q,
+                                const int* context_lens, const int* block_tables, float scale, int num_seqs,
+                                int max_qlen, int nq, int nkv, int D, int block_size, int max_blocks, hipStream_t s);
+void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int* splits_out);
+int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi, hipStream_t s);
+int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
+               const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist,
+               int hist_stride, int* steps, hipStream_t s);
+int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab, hipStream_t s);
+int k8s_silu_mul(void* out, const void* gu, int T, int I, hipStream_t s);
+int k8s_hash_init(void* out, int rows, int cols, long long gcols, long long row0, long long col0, uint32_t seed,
+                  uint32_t tensor_id, float scale, float shift, hipStream_t s);
+}
+
+namespace {
+
+template <typename T = void>
+inline T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+inline hipStream_t S(int64_t s) {
+  return s < 0 ? reinterpret_cast<hipStream_t>(k8s_current_stream()) : reinterpret_cast<hipStream_t>(s);
+}
+
+inline void check(int rc, const char* what) {
+  if (rc == 0) return;
+  std::string msg = std::string(what) + " failed: ";
+  if (rc < 0) msg += "invalid arguments (code " + std::to_string(rc) + ")";
+  else msg += hipGetErrorString(static_cast<hipError_t>(rc));
+  throw std::runtime_error(msg);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "gfx950 HIP kernels and native runtime of k8s_llm_scheduler_amd";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("rmsnorm", [](uintptr_t out, uintptr_t x, uintptr_t residual, uintptr_t w, int rows, int H, float eps,
+                      int64_t s) { check(k8s_rmsnorm(P(out), P(x), P(residual), P(w), rows, H, eps, S(s)), "rmsnorm"); });
+  m.def("rope_kv_write", [](uintptr_t q_out, uintptr_t kc, uintptr_t vc, uintptr_t qkv, uintptr_t cos_sin,
+                            uintptr_t pos, uintptr_t slots, uintptr_t ctx, uintptr_t bt, int max_blocks, int bs, int T,
+                            int nq, int nkv, int D, int64_t s) {
+    check(k8s_rope_kv_write(P(q_out), P(kc), P(vc), P(qkv), P<float>(cos_sin), P<int>(pos), P<int>(slots),
+                            P<int>(ctx), P<int>(bt), max_blocks, bs, T, nq, nkv, D, S(s)),
+          "rope_kv_write");
+  });
+  m.def("paged_decode_attention", [](uintptr_t out, uintptr_t pacc, uintptr_t pml, uintptr_t q, uintptr_t kc,
+                                     uintptr_t vc, uintptr_t bt, uintptr_t ctx, float scale, int B, int nq, int nkv,
+                                     int D, int bs, int max_blocks, int part, int pmax, int64_t s) {
+    check(k8s_paged_decode_attention(P(out), P(pacc), P(pml), P(q), P(kc), P(vc), P<int>(bt), P<int>(ctx), scale, B,
+                                     nq, nkv, D, bs, max_blocks, part, pmax, S(s)),
+          "paged_decode_attention");
+  });
+  m.def("paged_prefill_attention", [](uintptr_t out, uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t cu_q,
+                                      uintptr_t ctx, uintptr_t bt, float scale, int nseq, int max_qlen, int nq,
+                                      int nkv, int D, int bs, int max_blocks, int64_t s) {
+    check(k8s_paged_prefill_attention(P(out), P(q), P(kc), P(vc), P<int>(cu_q), P<int>(ctx), P<int>(bt), scale, nseq,
+                                      max_qlen, nq, nkv, D, bs, max_blocks, S(s)),
+          "paged_prefill_attention");
+  });
+  m.def("gemv_plan", [](int M, int N, int K, int epi) {
+    int ks, sp;
+    k8s_gemv_plan(M, N, K, epi, &ks, &sp);
+    return py::make_tuple(ks, sp);
+  });
+  m.def("gemv", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, int M, int N, int K, int epi,
+                   int64_t s) { check(k8s_gemv(P(out), P(partial), P(x), P(W), M, N, K, epi, S(s)), "gemv"); });
+  m.def("sample", [](uintptr_t tokens, uintptr_t logits, int B, int Vs, int shards, uintptr_t temp, uintptr_t top_p,
+                     uintptr_t seeds, uintptr_t counter, uintptr_t ctx_inc, uintptr_t hist, int hist_stride,
+                     uintptr_t steps, int64_t s) {
+    check(k8s_sample(P<int>(tokens), P<float>(logits), B, Vs, shards, P<float>(temp), P<float>(top_p),
+                     P<uint32_t>(seeds), P<int>(counter), P<int>(ctx_inc), P<int>(hist), hist_stride, P<int>(steps),
+                     S(s)),
+          "sample");
+  });
+  m.def("embedding", [](uintptr_t out, uintptr_t ids, uintptr_t table, int T, int H, int vocab, int64_t s) {
+    check(k8s_embedding(P(out), P<int>(ids), P(table), T, H, vocab, S(s)), "embedding");
+  });
+  m.def("silu_mul", [](uintptr_t out, uintptr_t gu, int T, int I, int64_t s) {
+    check(k8s_silu_mul(P(out), P(gu), T, I, S(s)), "silu_mul");
+  });
+  m.def("hash_init", [](uintptr_t out, int rows, int cols, long long gcols, long long row0, long long col0,
+                        uint32_t seed, uint32_t tid, float scale, float shift, int64_t s) {
+    check(k8s_hash_init(P(out), rows, cols, gcols, row0, col0, seed, tid, scale, shift, S(s)), "hash_init");
+  });
+
+  using k8sllm::BlockAllocator;
+  py::class_<BlockAllocator::Allocation>(m, "Allocation")
+      .def_readonly("blocks", &BlockAllocator::Allocation::blocks)
+      .def_readonly("cached_tokens", &BlockAllocator::Allocation::cached_tokens);
+  py::class_<BlockAllocator>(m, "BlockAllocator")
+      .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("block_size"), py::arg("prefix_caching") = true)
+      .def("allocate", &BlockAllocator::allocate)
+      .def("can_allocate", &BlockAllocator::can_allocate)
+      .def("commit_prefix", &BlockAllocator::commit_prefix)
+      .def("release", &BlockAllocator::release)
+      .def("reset_prefix_cache", &BlockAllocator::reset_prefix_cache)
+      .def_property_readonly("num_blocks", &BlockAllocator::num_blocks)
+      .def_property_readonly("block_size", &BlockAllocator::block_size)
+      .def_property_readonly("num_free", &BlockAllocator::num_free)
+      .def_property_readonly("num_cached", &BlockAllocator::num_cached)
+      .def_property_readonly("hits", &BlockAllocator::hits)
+      .def_property_readonly("queries", &BlockAllocator::queries)
+      .def("refcount", &BlockAllocator::refcount);
+}

@@ -1,0 +1,207 @@
+// K6: causal prefill flash attention over the PAGED KV cache, MFMA bf16 (gfx950).
+//
+// Reading K/V through the block table (instead of from the chunk's own q/k/v) makes the same
+// kernel serve plain prefill, chunked prefill and prefix-cached prompts: query i of sequence s
+// sits at absolute position ctx_s - qlen_s + i and attends keys [0, pos].
+//
+// Structure (one workgroup = 4 waves = 64 query rows of ONE query head):
+//  * "swapped" QK^T: S^T = K . Q^T with v_mfma_f32_16x16x32_bf16, so each lane ends up holding
+//    16 scores of ONE query row (row = lane & 15): the row max/sum need 2 cross-lane steps and
+//    the probabilities feed the P.V MFMA as its A operand straight from registers (the key
+//    order inside a 32-key step is permuted identically on the V side, see below).
+//  * V tiles (64 keys x 128 d) are staged in LDS with an XOR swizzle and read with the gfx950
+//    transposing read ds_read_b64_tr_b16, which delivers 4 keys of one d column per lane --
+//    exactly the B-operand layout, so V needs no register transpose.
+//  * K fragments are loaded per lane straight from the cache (16-byte rows pieces).
+//  * online softmax in the log2 domain (scale * log2(e) folded into S).
+#include "common.h"
+
+namespace k8sllm {
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ int v_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+template <int D>
+__global__ void __launch_bounds__(256) paged_prefill_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int* __restrict__ cu_q, const int* __restrict__ context_lens,
+    const int* __restrict__ block_tables, float scale_log2, int nq, int nkv, int block_size, int max_blocks) {
+  static_assert(D == 128, "head_dim 128");
+  constexpr int KT = 64;  // keys per tile
+  __shared__ __attribute__((aligned(16))) char vlds[KT * D * 2];
+
+  const int s = blockIdx.z, h = blockIdx.y, tile = blockIdx.x;
+  const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
+  if (tile * 64 >= qlen) return;
+  const int ctx = context_lens[s];
+  const int qstart = ctx - qlen;  // absolute position of query 0
+  const int kvh = h / (nq / nkv);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int* bt = block_tables + (size_t)s * max_blocks;
+
+  // my query row (B operand columns / softmax rows)
+  const int row = tile * 64 + wid * 16 + li;
+  const int row_c = min(row, qlen - 1);  // clamp padding rows to a valid query
+  const int qpos = qstart + row_c;
+  bf16x8 qf[D / 32];
+  {
+    const bf16_t* qp = q + ((size_t)(q0 + row_c) * nq + h) * D;
+#pragma unroll
+    for (int kk = 0; kk < D / 32; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(qp + kk * 32 + g * 8);
+  }
+
+  f32x4 o[D / 16];
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int last_row = min(tile * 64 + 63, qlen - 1);
+  const int kv_end = qstart + last_row + 1;  // keys needed by this workgroup
+  const int ntiles = (kv_end + KT - 1) / KT;
+  const size_t kv_stride = (size_t)nkv * D;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int kbase = t * KT;
+    // ---- stage V tile into LDS (swizzled 16-byte chunks); keys >= ctx are zero-filled
+#pragma unroll
+    for (int c = 0; c < (KT * D / 8) / 256; ++c) {
+      const int idx = tid + 256 * c;
+      const int kr = idx / (D / 8), ch = idx % (D / 8);
+      const int key = kbase + kr;
+      u32x4 val = u32x4{0u, 0u, 0u, 0u};
+      if (key < ctx) {
+        const int slot = bt[key / block_size] * block_size + key % block_size;
+        val = *reinterpret_cast<const u32x4*>(v_cache + slot * kv_stride + kvh * D + ch * 8);
+      }
+      *reinterpret_cast<u32x4*>(vlds + kr * (D * 2) + 16 * (ch ^ v_swz(kr))) = val;
+    }
+
+    // ---- S^T = K . Q^T for 4 key sub-tiles of 16
+    f32x4 sacc[KT / 16];
+#pragma unroll
+    for (int m = 0; m < KT / 16; ++m) {
+      const int key = min(kbase + m * 16 + li, ctx - 1);
+      const int slot = bt[key / block_size] * block_size + key % block_size;
+      const bf16_t* kp = k_cache + slot * kv_stride + kvh * D + g * 8;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < D / 32; ++kk) {
+        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kp + kk * 32);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[kk], acc, 0, 0, 0);
+      }
+      sacc[m] = acc;
+    }
+    // lane holds S[row li][key kbase + 16m + 4g + i]
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int m = 0; m < KT / 16; ++m) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kbase + m * 16 + g * 4 + i;
+        float v = sacc[m][i] * scale_log2;
+        v = (key <= qpos && key < ctx) ? v : -INFINITY;
+        sacc[m][i] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, WAVE));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, WAVE));
+    const float m_new = fmaxf(m_run, tmax);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    float rsum = 0.f;
+#pragma unroll
+    for (int m = 0; m < KT / 16; ++m) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pv = exp2f(sacc[m][i] - m_use);
+        sacc[m][i] = pv;
+        rsum += pv;
+      }
+    }
+    rsum += __shfl_xor(rsum, 16, WAVE);
+    rsum += __shfl_xor(rsum, 32, WAVE);
+    l_run = l_run * alpha + rsum;
+    m_run = m_new;
+
+    // rescale O rows (row 4g+i of O lives in lanes whose li == 4g+i for the stats)
+    float a_i[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a_i[i] = __shfl(alpha, g * 4 + i, WAVE);
+#pragma unroll
+    for (int n = 0; n < D / 16; ++n) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[n][i] *= a_i[i];
+    }
+
+    // P as A operand: k-step st covers keys 32st..32st+31 in the permuted order
+    // slot j<4 -> key 32st + 4g + j ; slot j>=4 -> key 32st + 16 + 4g + (j-4)
+    bf16x8 pa[KT / 32];
+#pragma unroll
+    for (int st = 0; st < KT / 32; ++st) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pa[st][j] = (__bf16)sacc[2 * st][j];
+        pa[st][4 + j] = (__bf16)sacc[2 * st + 1][j];
+      }
+    }
+    __syncthreads();  // V tile visible
+
+    const int qd = li >> 2, pd = li & 3;  // tr-read lane roles: row q, column group p
+#pragma unroll
+    for (int st = 0; st < KT / 32; ++st) {
+      const int r0 = 32 * st + 4 * g + qd;
+      const int r1 = r0 + 16;
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n) {
+        const int col = 16 * n + 4 * pd;
+        const int ch = col >> 3, hb = (col & 7) * 2;
+        const lds_bf16x4* a0 = (const lds_bf16x4*)(vlds + r0 * (D * 2) + 16 * (ch ^ v_swz(r0)) + hb);
+        const lds_bf16x4* a1 = (const lds_bf16x4*)(vlds + r1 * (D * 2) + 16 * (ch ^ v_swz(r1)) + hb);
+        const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+        const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+        bf16x8 vb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { vb[j] = v0[j]; vb[4 + j] = v1[j]; }
+        o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[st], vb, o[n], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // before the next tile overwrites vlds
+  }
+
+  // ---- normalise and store: o[n][i] = O[row 4g+i][d 16n + li]
+  float inv_l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lv = __shfl(l_run, g * 4 + i, WAVE);
+    inv_l[i] = lv > 0.f ? 1.f / lv : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = tile * 64 + wid * 16 + g * 4 + i;
+    if (r < qlen) {
+      bf16_t* op = out + ((size_t)(q0 + r) * nq + h) * D + li;
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n) op[16 * n] = f2bf(o[n][i] * inv_l[i]);
+    }
+  }
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+extern "C" int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, const void* v_cache,
+                                           const int* cu_q, const int* context_lens, const int* block_tables,
+                                           float scale, int num_seqs, int max_qlen, int nq, int nkv, int D,
+                                           int block_size, int max_blocks, hipStream_t stream) {
+  if (num_seqs <= 0 || max_qlen <= 0) return 0;
+  if (D != 128 || nq % nkv != 0) return -1;
+  dim3 grid((max_qlen + 63) / 64, nq, num_seqs);
+  paged_prefill_kernel<128><<<grid, 256, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, (const bf16_t*)k_cache,
+                                                     (const bf16_t*)v_cache, cu_q, context_lens, block_tables,
+                                                     scale * 1.4426950408889634f, nq, nkv, block_size, max_blocks);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,216 @@
+// K3/K8/K9/K11/K12 decode path: skinny GEMM out[M, N] = x[M, K] . W[N, K]^T for M <= 8 rows
+// (decode batch), bf16 weights streamed from HBM exactly once.
+//
+// The weight stream is the whole cost (HBM-bound: 2 bytes per weight, ~1 FLOP/byte at M = 1),
+// so the kernel is built around keeping many 16-byte weight loads in flight per lane:
+//  * one wave owns RPW output rows; a workgroup = 4 waves shares one K-slice of x staged in
+//    LDS (x is re-read by every row, the LDS read is 256 B/clk/CU vs the L1's 64),
+//  * weights are loaded with non-temporal hints (read once: keep them out of L2/MALL),
+//  * bf16 pairs are multiplied with v_dot2_f32_bf16 (fp32 accumulate),
+//  * when N alone gives too few workgroups to fill 256 CUs, K is split (grid.y) and partial
+//    fp32 slabs are combined by a finalize kernel that also applies the epilogue.
+// Epilogues: BF16 store, FP32 store (logits), SWIGLU: W = [gate; up] (2I rows) and the output is
+// silu(gate_j) * up_j (SURVEY.md K10 fused into K9).
+#include "common.h"
+
+namespace k8sllm {
+
+enum Epi { EPI_BF16 = 0, EPI_F32 = 1, EPI_SWIGLU = 2 };
+
+__device__ __forceinline__ float dot2(uint32_t w, uint32_t x, float acc) {
+  // bf16 pairs -> v_dot2c_f32_bf16.  (Passing the 16-byte vectors by reference and bit-casting
+  // their elements miscompiled to a single-dword load under ROCm 7.2 -- keep scalars here.)
+  bf16x2 a, b;
+  __builtin_memcpy(&a, &w, 4);
+  __builtin_memcpy(&b, &x, 4);
+  return __builtin_amdgcn_fdot2_f32_bf16(a, b, acc, false);
+}
+__device__ __forceinline__ float dot8(u32x4 w, u32x4 x, float acc) {
+  acc = dot2(w.x, x.x, acc);
+  acc = dot2(w.y, x.y, acc);
+  acc = dot2(w.z, x.z, acc);
+  return dot2(w.w, x.w, acc);
+}
+
+__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+
+template <int M, int RPW, int EPI>
+__global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float* __restrict__ partial,
+                                                   const bf16_t* __restrict__ x, const bf16_t* __restrict__ W,
+                                                   int N_out, int K, int KS, int half_rows) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  u32x4* xs = reinterpret_cast<u32x4*>(smem);  // [M][KS/8]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int kb = blockIdx.y * KS;
+  const int klen = min(KS, K - kb);
+  const int nch = klen >> 3;  // 16-byte chunks in this slice
+
+  // stage x[:, kb:kb+klen] into LDS
+  for (int i = threadIdx.x; i < M * nch; i += blockDim.x) {
+    const int m = i / nch, c = i - m * nch;
+    xs[m * (KS >> 3) + c] = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + kb + c * 8);
+  }
+  __syncthreads();
+
+  constexpr int NR = (EPI == EPI_SWIGLU) ? 2 * RPW : RPW;  // weight rows per wave
+  const int r0 = (blockIdx.x * 4 + wid) * RPW;               // first output row of this wave
+  if (r0 >= N_out) return;
+  const bf16_t* wrow[NR];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int n = min(r0 + r, N_out - 1);
+    wrow[r] = W + (size_t)n * K + kb;
+    if (EPI == EPI_SWIGLU) wrow[RPW + r] = W + (size_t)(n + half_rows) * K + kb;
+  }
+  float acc[NR][M];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+
+  constexpr int U = (NR >= 4) ? 2 : ((NR >= 2) ? 4 : 8);  // chunks per lane in flight per row
+  int c = lane;
+  for (; c + 64 * (U - 1) < nch; c += 64 * U) {
+    u32x4 wv[U][NR];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+        wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + c + 64 * u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const u32x4 xv = xs[m * (KS >> 3) + c + 64 * u];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[r][m] = dot8(wv[u][r], xv, acc[r][m]);
+      }
+    }
+  }
+  for (; c < nch; c += 64) {
+    u32x4 wv[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) wv[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + c);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const u32x4 xv = xs[m * (KS >> 3) + c];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) acc[r][m] = dot8(wv[r], xv, acc[r][m]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+
+  if (lane != 0) return;
+  const int wrows = (EPI == EPI_SWIGLU) ? 2 * half_rows : N_out;  // weight rows (slab width)
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int n = r0 + r;
+    if (n >= N_out) break;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (partial != nullptr) {
+        float* slab = partial + ((size_t)blockIdx.y * M + m) * wrows;
+        slab[n] = acc[r][m];
+        if (EPI == EPI_SWIGLU) slab[n + half_rows] = acc[RPW + r][m];
+      } else if (EPI == EPI_F32) {
+        reinterpret_cast<float*>(out)[(size_t)m * N_out + n] = acc[r][m];
+      } else if (EPI == EPI_SWIGLU) {
+        reinterpret_cast<bf16_t*>(out)[(size_t)m * N_out + n] = f2bf(silu(acc[r][m]) * acc[RPW + r][m]);
+      } else {
+        reinterpret_cast<bf16_t*>(out)[(size_t)m * N_out + n] = f2bf(acc[r][m]);
+      }
+    }
+  }
+}
+
+template <int EPI>
+__global__ void gemv_finalize_kernel(void* __restrict__ out, const float* __restrict__ partial, int M, int N_out,
+                                     int splits, int half_rows) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * N_out) return;
+  const int m = i / N_out, n = i - m * N_out;
+  const int wrows = (EPI == EPI_SWIGLU) ? 2 * half_rows : N_out;
+  float a = 0.f, b = 0.f;
+  for (int s = 0; s < splits; ++s) {
+    const float* slab = partial + ((size_t)s * M + m) * wrows;
+    a += slab[n];
+    if (EPI == EPI_SWIGLU) b += slab[n + half_rows];
+  }
+  if (EPI == EPI_F32) reinterpret_cast<float*>(out)[i] = a;
+  else if (EPI == EPI_SWIGLU) reinterpret_cast<bf16_t*>(out)[i] = f2bf(silu(a) * b);
+  else reinterpret_cast<bf16_t*>(out)[i] = f2bf(a);
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+// Plan the launch: returns the K-slice length (multiple of 512) and the split count.
+extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int* splits_out) {
+  const int rpw = (M >= 4) ? 2 : 1;
+  const int rows_per_wg = 4 * rpw;
+  const int n_wg = (N_out + rows_per_wg - 1) / rows_per_wg;
+  const int lds_cap_elems = 32768 / (2 * M);  // <= 32 KiB of x per workgroup
+  int splits = 1;
+  const int target = 256;  // split K only when N alone cannot give every CU a workgroup
+  if (n_wg < target) splits = (target + n_wg - 1) / n_wg;
+  int ks = (K + splits - 1) / splits;
+  ks = ((ks + 511) / 512) * 512;
+  if (ks < 512) ks = 512;
+  while (ks > lds_cap_elems) ks -= 512;
+  if (ks > K) ks = ((K + 7) / 8) * 8;
+  splits = (K + ks - 1) / ks;
+  (void)epi;
+  *ks_out = ks;
+  *splits_out = splits;
+}
+
+// partial: fp32 workspace of splits * M * wrows floats (wrows = N_out, or 2*N_out for SWIGLU);
+// may be null when the plan has a single split.
+extern "C" int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi,
+                        hipStream_t stream) {
+  if (M < 1 || M > 8 || K % 8 != 0 || N_out <= 0) return -1;
+  int ks, splits;
+  k8s_gemv_plan(M, N_out, K, epi, &ks, &splits);
+  if (splits > 1 && partial == nullptr) return -3;
+  float* part = splits > 1 ? (float*)partial : nullptr;
+  const int rpw = (M >= 4) ? 2 : 1;
+  dim3 grid((N_out + 4 * rpw - 1) / (4 * rpw), splits);
+  const size_t lds = (size_t)M * ks * 2;
+  const int half_rows = (epi == EPI_SWIGLU) ? N_out : 0;
+  const bf16_t* xx = (const bf16_t*)x;
+  const bf16_t* ww = (const bf16_t*)W;
+#define G(MM, RR, EE) gemv_kernel<MM, RR, EE><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks, half_rows)
+#define BY_EPI(MM, RR)                  \
+  switch (epi) {                        \
+    case EPI_BF16: G(MM, RR, EPI_BF16); break;       \
+    case EPI_F32: G(MM, RR, EPI_F32); break;         \
+    case EPI_SWIGLU: G(MM, RR, EPI_SWIGLU); break;   \
+    default: return -2;                 \
+  }
+  switch (M) {
+    case 1: BY_EPI(1, 1) break;
+    case 2: BY_EPI(2, 1) break;
+    case 3: BY_EPI(3, 1) break;
+    case 4: BY_EPI(4, 2) break;
+    case 5: BY_EPI(5, 2) break;
+    case 6: BY_EPI(6, 2) break;
+    case 7: BY_EPI(7, 2) break;
+    case 8: BY_EPI(8, 2) break;
+  }
+#undef BY_EPI
+#undef G
+  if (splits > 1) {
+    const int total = M * N_out;
+    const int blocks = (total + 255) / 256;
+    switch (epi) {
+      case EPI_BF16: gemv_finalize_kernel<EPI_BF16><<<blocks, 256, 0, stream>>>(out, part, M, N_out, splits, half_rows); break;
+      case EPI_F32: gemv_finalize_kernel<EPI_F32><<<blocks, 256, 0, stream>>>(out, part, M, N_out, splits, half_rows); break;
+      case EPI_SWIGLU: gemv_finalize_kernel<EPI_SWIGLU><<<blocks, 256, 0, stream>>>(out, part, M, N_out, splits, half_rows); break;
+    }
+  }
+  return (int)hipGetLastError();
+}

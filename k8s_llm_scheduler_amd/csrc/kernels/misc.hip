@@ -1,0 +1,79 @@
+// K1 embedding gather, K10 SiLU-and-mul (prefill path, where the GEMM is a library GEMM),
+// and deterministic weight initialisation (hash-uniform, identical on any device / TP split).
+#include "common.h"
+
+namespace k8sllm {
+
+// out[t, :] = table[ids[t], :]   (rows of H bf16, H % 8 == 0)
+__global__ void embedding_kernel(bf16_t* __restrict__ out, const int* __restrict__ ids,
+                                 const bf16_t* __restrict__ table, int H, int vocab) {
+  const int t = blockIdx.x;
+  int id = ids[t];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  const u32x4* src = reinterpret_cast<const u32x4*>(table + (size_t)id * H);
+  u32x4* dst = reinterpret_cast<u32x4*>(out + (size_t)t * H);
+  for (int i = threadIdx.x; i < H / 8; i += blockDim.x) dst[i] = src[i];
+}
+
+// out[t, j] = silu(gu[t, j]) * gu[t, I + j]
+__global__ void silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ gu, int T, int I) {
+  const size_t n8 = (size_t)T * (I / 8);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t t = i / (I / 8), c = i - t * (I / 8);
+    const u32x4 g = reinterpret_cast<const u32x4*>(gu + t * 2 * I)[c];
+    const u32x4 u = reinterpret_cast<const u32x4*>(gu + t * 2 * I + I)[c];
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float g0 = lo_bf(g[j]), g1 = hi_bf(g[j]);
+      o[j] = pack_bf2(g0 / (1.f + __expf(-g0)) * lo_bf(u[j]), g1 / (1.f + __expf(-g1)) * hi_bf(u[j]));
+    }
+    reinterpret_cast<u32x4*>(out + t * I)[c] = o;
+  }
+}
+
+// Deterministic init of a [rows, cols] shard of a global [*, gcols] tensor:
+// value(gr, gc) = (2 * u01(hash3(seed, tensor_id, gr * gcols + gc)) - 1) * scale + shift
+__global__ void hash_init_kernel(bf16_t* __restrict__ out, int rows, int cols, long long gcols, long long row0,
+                                 long long col0, uint32_t seed, uint32_t tensor_id, float scale, float shift) {
+  const size_t n = (size_t)rows * cols;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / cols, c = i - r * cols;
+    const uint32_t flat = (uint32_t)((row0 + (long long)r) * gcols + col0 + (long long)c);
+    const float u = u01(hash3(seed, tensor_id, flat));
+    out[i] = f2bf((2.f * u - 1.f) * scale + shift);
+  }
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+extern "C" int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab,
+                             hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8) return -1;
+  embedding_kernel<<<T, 256, 0, stream>>>((bf16_t*)out, ids, (const bf16_t*)table, H, vocab);
+  return (int)hipGetLastError();
+}
+
+extern "C" int k8s_silu_mul(void* out, const void* gu, int T, int I, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (I % 8) return -1;
+  const size_t n8 = (size_t)T * (I / 8);
+  int blocks = (int)((n8 + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  silu_mul_kernel<<<blocks, 256, 0, stream>>>((bf16_t*)out, (const bf16_t*)gu, T, I);
+  return (int)hipGetLastError();
+}
+
+extern "C" int k8s_hash_init(void* out, int rows, int cols, long long gcols, long long row0, long long col0,
+                             uint32_t seed, uint32_t tensor_id, float scale, float shift, hipStream_t stream) {
+  if ((size_t)rows * cols == 0) return 0;
+  const size_t n = (size_t)rows * cols;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 65536) blocks = 65536;
+  hash_init_kernel<<<blocks, 256, 0, stream>>>((bf16_t*)out, rows, cols, gcols, row0, col0, seed, tensor_id, scale,
+                                               shift);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,154 @@
+// K13 + K17: sampling over a (possibly vocab-sharded) fp32 logits buffer, fused with the
+// decode-state update so a whole decode step can be replayed from a hipGraph.
+//
+// Logits layout: [shards][B][Vs]; token id v = shard * Vs + j (vocab-parallel LM head output
+// after an all-gather, or a single shard).  Per row b:
+//   temperature <= 0       -> greedy argmax (lowest index wins ties, like torch.argmax)
+//   top_p >= 1             -> Gumbel-max: argmax(l / T + G), G = -log(-log(U)), one pass
+//   0 < top_p < 1          -> nucleus: exact logit threshold by a 4 x 8-bit radix select on
+//                             probability MASS (no sort), then Gumbel-max inside the nucleus.
+// U comes from a counter-based hash of (seed[b], counter[b], token) so results do not depend on
+// batch composition or on which rank samples (every TP rank draws the same token).
+// After sampling: tokens[b] = tok; hist[b][steps[b]] = tok; steps[b]++; ctx[b]++ (optional).
+#include "common.h"
+
+namespace k8sllm {
+
+constexpr int ST = 1024;  // threads per row
+
+__device__ __forceinline__ uint32_t ord_key(float f) {  // monotone float -> uint32
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+struct ArgMax {
+  float v;
+  int i;
+};
+__device__ __forceinline__ ArgMax better(ArgMax a, ArgMax b) {
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+__device__ ArgMax block_argmax(ArgMax a, float* sv, int* si) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgMax b{__shfl_xor(a.v, o, WAVE), __shfl_xor(a.i, o, WAVE)};
+    a = better(a, b);
+  }
+  if (lane == 0) { sv[wid] = a.v; si[wid] = a.i; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < ST / 64; ++w) a = better(a, ArgMax{sv[w], si[w]});
+    sv[0] = a.v;
+    si[0] = a.i;
+  }
+  __syncthreads();
+  ArgMax r{sv[0], si[0]};
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, const float* __restrict__ logits, int B,
+                                                    int Vs, int shards, const float* __restrict__ temperature,
+                                                    const float* __restrict__ top_p, const uint32_t* __restrict__ seeds,
+                                                    const int* __restrict__ counter, int* __restrict__ ctx_inc,
+                                                    int* __restrict__ hist, int hist_stride, int* __restrict__ steps) {
+  __shared__ float sv[ST / 64];
+  __shared__ int si[ST / 64];
+  __shared__ float hist_mass[256];
+  __shared__ float red[16];
+  __shared__ uint32_t sh_prefix;
+  __shared__ float sh_above;
+  const int b = blockIdx.x;
+  if (ctx_inc != nullptr && ctx_inc[b] <= 0) return;  // padded row
+  const int V = Vs * shards;
+  const float T = temperature[b];
+  const float P = top_p[b];
+  const uint32_t seed = seeds[b];
+  const uint32_t ctr = counter ? (uint32_t)counter[b] : 0u;
+  auto L = [&](int v) -> float {
+    const int s = v / Vs, j = v - s * Vs;
+    return logits[((size_t)s * B + b) * Vs + j];
+  };
+
+  ArgMax best{-INFINITY, 0x7fffffff};
+  if (T <= 0.f) {
+    for (int v = threadIdx.x; v < V; v += ST) best = better(best, ArgMax{L(v), v});
+    best = block_argmax(best, sv, si);
+  } else {
+    const float invT = 1.f / T;
+    uint32_t kthr = 0;  // include tokens whose ord_key >= kthr
+    if (P < 1.f) {
+      ArgMax mx{-INFINITY, 0};
+      for (int v = threadIdx.x; v < V; v += ST) mx = better(mx, ArgMax{L(v), v});
+      mx = block_argmax(mx, sv, si);
+      const float M = mx.v;
+      float z = 0.f;
+      for (int v = threadIdx.x; v < V; v += ST) z += __expf((L(v) - M) * invT);
+      z = block_sum(z, red);
+      const float target = P * z;
+      uint32_t prefix = 0;
+      float above = 0.f;  // mass of tokens strictly above the current prefix bucket
+      for (int round = 0; round < 4; ++round) {
+        const int shift = 24 - 8 * round;
+        for (int i = threadIdx.x; i < 256; i += ST) hist_mass[i] = 0.f;
+        __syncthreads();
+        for (int v = threadIdx.x; v < V; v += ST) {
+          const float l = L(v);
+          const uint32_t k = ord_key(l);
+          const bool match = round == 0 || (k >> (shift + 8)) == (prefix >> (shift + 8));
+          if (match) atomicAdd(&hist_mass[(k >> shift) & 255], __expf((l - M) * invT));
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          float cum = above;
+          int bsel = 0;
+          for (int bk = 255; bk >= 0; --bk) {
+            if (cum + hist_mass[bk] >= target || bk == 0) { bsel = bk; break; }
+            cum += hist_mass[bk];
+          }
+          sh_prefix = prefix | ((uint32_t)bsel << shift);
+          sh_above = cum;
+        }
+        __syncthreads();
+        prefix = sh_prefix;
+        above = sh_above;
+        __syncthreads();
+      }
+      kthr = prefix;
+    }
+    for (int v = threadIdx.x; v < V; v += ST) {
+      const float l = L(v);
+      if (P < 1.f && ord_key(l) < kthr) continue;
+      const float u = u01(hash3(seed, ctr, (uint32_t)v));
+      const float g = -__logf(-__logf(u));
+      best = better(best, ArgMax{l * invT + g, v});
+    }
+    best = block_argmax(best, sv, si);
+  }
+  if (threadIdx.x == 0) {
+    const int tok = best.i;
+    tokens[b] = tok;
+    if (hist != nullptr) {
+      const int st = steps[b];
+      if (st < hist_stride) hist[(size_t)b * hist_stride + st] = tok;
+      steps[b] = st + 1;
+    }
+    if (ctx_inc != nullptr) ctx_inc[b] += 1;
+  }
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+extern "C" int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
+                          const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist,
+                          int hist_stride, int* steps, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (hist != nullptr && steps == nullptr) return -1;
+  sample_kernel<<<B, ST, 0, stream>>>(tokens, logits, B, Vs, shards, temperature, top_p, seeds, counter, ctx_inc, hist,
+                                      hist_stride, steps);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,56 @@
+"""In-process decision engine (replaces the HuggingFace Inference API call of the reference)."""
+
+from __future__ import annotations
+
+import logging
+import time
+from typing import Optional
+
+from .sampling import SamplingParams  # noqa: F401
+from .tokenizer import Tokenizer  # noqa: F401
+
+log = logging.getLogger(__name__)
+
+
+def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str] = None, weights: Optional[str] = None,
+                 tokenizer: Optional[str] = None, seed: int = 0, max_batch: int = 64, block_size: int = 16,
+                 num_blocks: Optional[int] = None, kv_cache_gb: float = 0.0, kv_cache_fraction: float = 0.85,
+                 max_model_len: int = 16384, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
+                 prefix_caching: bool = True, decode_chunk: int = 4, metrics=None, capture: bool = True):
+    """Model + tokenizer + engine on this rank's GPU (or CPU when no GPU is present)."""
+    import torch
+
+    from ..models.config import get_config
+    from ..models.llama import LlamaModel
+    from ..parallel import TPGroup
+    from .engine import LLMEngine
+
+    tp = tp or TPGroup()
+    if device is None:
+        device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
+    cfg = get_config(weights or preset) if weights else get_config(preset)
+    t0 = time.perf_counter()
+    model = LlamaModel(cfg, tp, device=device, seed=seed, weights=weights, max_model_len=max_model_len)
+    if device.startswith("cuda"):
+        torch.cuda.synchronize()
+    log.info(f" Model {cfg.name} ready on {device} (tp {tp.rank}/{tp.world}, "
+             f"{model.weight_bytes() / 1e9:.1f} GB weights, {time.perf_counter() - t0:.1f}s)")
+    tok = Tokenizer(tokenizer, model_vocab=cfg.vocab)
+    eng = LLMEngine(model, tok, max_batch=max_batch, block_size=block_size, num_blocks=num_blocks,
+                    kv_cache_gb=kv_cache_gb, kv_cache_fraction=kv_cache_fraction, max_model_len=max_model_len,
+                    max_prefill_tokens=max_prefill_tokens, cuda_graphs=cuda_graphs, prefix_caching=prefix_caching,
+                    decode_chunk=decode_chunk, seed=seed, metrics=metrics)
+    if capture and eng.use_graphs:
+        t1 = time.perf_counter()
+        eng.capture_graphs()
+        log.info(f" Captured {len(eng.graphs)} decode graphs in {time.perf_counter() - t1:.1f}s")
+    return eng
+
+
+def engine_from_config(cfg, tp=None, metrics=None):
+    e = cfg.engine
+    return build_engine(e.preset, tp=tp, weights=e.weights, tokenizer=e.tokenizer, seed=e.seed,
+                        max_batch=e.max_batch, block_size=e.block_size, kv_cache_gb=e.kv_cache_gb,
+                        kv_cache_fraction=e.kv_cache_fraction, max_model_len=e.max_model_len,
+                        max_prefill_tokens=e.max_prefill_tokens, cuda_graphs=e.cuda_graphs,
+                        prefix_caching=e.prefix_caching, metrics=metrics)

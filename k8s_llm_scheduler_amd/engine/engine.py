@@ -1,0 +1,446 @@
+"""Decision engine: continuous-batched prefill + hipGraph-replayed decode over a paged KV cache.
+
+Replaces the remote ``chat_completion`` of the reference (``scheduler.py:425-433``) with an
+in-process Llama-3.
+
+Per engine iteration (:meth:`LLMEngine.step`):
+
+1. **Admit** waiting requests while a decode slot is free and the native block allocator can
+   reserve KV for prompt + max_tokens (decode never allocates: a decode step needs no host work).
+   Prompt prefixes already in the prefix cache (the scheduler's long system prompt) are skipped.
+2. **Prefill** (chunked): up to ``max_prefill_tokens`` prompt tokens of several requests in one
+   varlen forward; requests whose prompt completes sample their first token, which seeds the
+   device-resident decode state of their slot.
+3. **Decode**: ``decode_chunk`` steps over the active slots.  One step = embedding -> 80 x
+   (norm, QKV GEMV, RoPE+KV write, paged attention, O GEMV, all-reduce, fused add+norm, SwiGLU
+   GEMV, down GEMV, all-reduce) -> LM head -> sampler, where the sampler also advances the state
+   (token, context length, history).  The whole step is captured once per batch bucket into a
+   hipGraph (``torch.cuda.CUDAGraph``) and replayed, so the host only launches graphs; after the
+   chunk, one small D2H copy of the token history drives stop checks (EOS, closed JSON object,
+   max_tokens).
+
+Every TP rank runs the identical deterministic schedule; sampling is deterministic given
+(seed, position), so all ranks draw the same tokens without any extra broadcast.
+"""
+
+from __future__ import annotations
+
+import itertools
+import logging
+import math
+import random
+import threading
+import time
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Deque, Dict, List, Optional, Sequence, Union
+
+import torch
+
+from .. import ops
+from ..control.jsonextract import json_object_closed
+from ..models.llama import LlamaModel
+from .sampling import SamplingParams
+from .tokenizer import Tokenizer
+
+log = logging.getLogger(__name__)
+
+BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
+
+
+@dataclass
+class Request:
+    rid: int
+    prompt_ids: List[int]
+    params: SamplingParams
+    seed: int
+    arrival: float = field(default_factory=time.perf_counter)
+    slot: int = -1
+    blocks: List[int] = field(default_factory=list)
+    computed: int = 0          # prompt tokens whose KV is in the cache
+    cached: int = 0            # of which came from the prefix cache
+    output_ids: List[int] = field(default_factory=list)
+    finished: bool = False
+    finish_reason: str = ""
+    first_token_time: Optional[float] = None
+    finish_time: Optional[float] = None
+    aborted: bool = False
+
+
+@dataclass
+class Output:
+    rid: int
+    text: str
+    token_ids: List[int]
+    prompt_tokens: int
+    cached_tokens: int
+    finish_reason: str
+    ttft: float
+    latency: float
+
+
+class LLMEngine:
+    def __init__(self, model: LlamaModel, tokenizer: Tokenizer, *, max_batch: int = 64, block_size: int = 16,
+                 num_blocks: Optional[int] = None, kv_cache_gb: float = 0.0, kv_cache_fraction: float = 0.85,
+                 max_model_len: Optional[int] = None, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
+                 prefix_caching: bool = True, decode_chunk: int = 4, seed: int = 0, metrics=None):
+        self.model = model
+        self.tok = tokenizer
+        self.device = model.device
+        self.gpu = self.device.type == "cuda"
+        self.max_batch = max_batch
+        self.block_size = block_size
+        self.max_model_len = min(max_model_len or model.max_model_len, model.max_model_len)
+        self.max_blocks_per_seq = math.ceil(self.max_model_len / block_size)
+        self.max_prefill_tokens = max_prefill_tokens
+        self.decode_chunk = max(1, decode_chunk)
+        self.metrics = metrics
+        self._rng = random.Random(seed)
+        self._ids = itertools.count()
+        if num_blocks is None:
+            per_block = model.kv_bytes_per_block(block_size)
+            if kv_cache_gb > 0:
+                budget = kv_cache_gb * 1e9
+            elif self.gpu:
+                free, _ = torch.cuda.mem_get_info(self.device)
+                budget = max(0.0, free * kv_cache_fraction - 2e9)
+            else:
+                budget = 64 * 1024 * 1024
+            num_blocks = int(budget // per_block)
+            # never more than every slot at full length needs
+            num_blocks = min(num_blocks, max_batch * self.max_blocks_per_seq + 1)
+        if num_blocks < self.max_blocks_per_seq:
+            raise RuntimeError(f"KV cache too small: {num_blocks} blocks < one full sequence "
+                               f"({self.max_blocks_per_seq})")
+        self.num_blocks = num_blocks
+        model.allocate_kv(num_blocks, block_size)
+        self.allocator = ops.native().BlockAllocator(num_blocks, block_size, prefix_caching) if ops.available() \
+            else _PyBlockAllocator(num_blocks, block_size, prefix_caching)
+        self.max_new_cap = self.max_model_len
+        self._alloc_state()
+        self.waiting: Deque[Request] = deque()
+        self.prefilling: List[Request] = []
+        self.running: Dict[int, Request] = {}        # slot -> request
+        self.requests: Dict[int, Request] = {}
+        self.free_slots = list(range(max_batch - 1, -1, -1))
+        self.use_graphs = cuda_graphs and self.gpu
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self._graph_pool = None
+        self.lock = threading.RLock()
+        self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
+                      "graph_replays": 0, "prefill_time": 0.0, "decode_time": 0.0}
+
+    # ------------------------------------------------------------------ device state
+    def _alloc_state(self) -> None:
+        B, dev = self.max_batch, self.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.s_tokens = torch.zeros(B, **i32)
+        self.s_ctx = torch.zeros(B, **i32)
+        self.s_bt = torch.zeros(B, self.max_blocks_per_seq, **i32)
+        self.s_temp = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.s_top_p = torch.ones(B, dtype=torch.float32, device=dev)
+        self.s_seeds = torch.zeros(B, **i32)
+        self.s_steps = torch.zeros(B, **i32)
+        self.s_hist = torch.zeros(B, self.max_new_cap, **i32)
+
+    def _decode_step(self, B: int) -> None:
+        logits = self.model.forward_decode(self.s_tokens[:B], self.s_ctx[:B], self.s_bt[:B], self.max_model_len)
+        ops.sample(logits, self.s_temp[:B], self.s_top_p[:B], self.s_seeds[:B], self.s_ctx[:B],
+                   shards=logits.shape[0], tokens_out=self.s_tokens[:B], ctx_inc=self.s_ctx[:B],
+                   hist=self.s_hist[:B], steps=self.s_steps[:B])
+
+    def _bucket(self, n: int) -> int:
+        for b in BUCKETS:
+            if b >= n and b <= self.max_batch:
+                return b
+        return self.max_batch
+
+    def capture_graphs(self, buckets: Optional[Sequence[int]] = None) -> None:
+        """Capture one decode-step graph per batch bucket (all slots must be idle: the kernels
+        skip rows with context length 0, so warm-up and capture do not touch any state)."""
+        if not self.use_graphs:
+            return
+        assert not self.running and not self.prefilling, "capture needs an idle engine"
+        buckets = buckets or [b for b in BUCKETS if b <= self.max_batch]
+        stream = torch.cuda.Stream(self.device)
+        for B in sorted(set(buckets)):
+            if B in self.graphs:
+                continue
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(stream):
+                self._decode_step(B)   # warm-up: allocator + lazy init outside capture
+            torch.cuda.current_stream(self.device).wait_stream(stream)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._graph_pool, stream=stream):
+                self._decode_step(B)
+            if self._graph_pool is None:
+                self._graph_pool = g.pool()
+            self.graphs[B] = g
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ requests
+    def render_chat(self, system: str, user: str) -> List[int]:
+        return self.tok.chat_ids(system, user)
+
+    def add_request(self, prompt: Union[str, List[int]], params: Optional[SamplingParams] = None) -> Request:
+        params = (params or SamplingParams()).validate()
+        ids = self.tok.encode(prompt) if isinstance(prompt, str) else list(prompt)
+        if not ids:
+            raise ValueError("empty prompt")
+        max_new = min(params.max_tokens, self.max_model_len - len(ids))
+        if max_new < 1:
+            raise ValueError(f"prompt of {len(ids)} tokens exceeds max_model_len {self.max_model_len}")
+        if max_new != params.max_tokens:
+            params = SamplingParams(**{**params.__dict__, "max_tokens": max_new})
+        seed = params.seed if params.seed is not None else self._rng.getrandbits(31)
+        with self.lock:
+            r = Request(next(self._ids), ids, params, seed)
+            self.requests[r.rid] = r
+            self.waiting.append(r)
+        return r
+
+    def abort(self, rid: int) -> None:
+        with self.lock:
+            r = self.requests.get(rid)
+            if r is not None and not r.finished:
+                r.aborted = True
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.prefilling or self.running)
+
+    # ------------------------------------------------------------------ scheduling
+    def _admit(self) -> None:
+        while self.waiting and self.free_slots:
+            r = self.waiting[0]
+            if r.aborted:
+                self.waiting.popleft()
+                self._finish(r, "abort")
+                continue
+            total = len(r.prompt_ids) + r.params.max_tokens
+            if not self.allocator.can_allocate(r.prompt_ids, total):
+                if not self.running and not self.prefilling:
+                    raise RuntimeError("request does not fit in an empty KV cache")
+                break
+            self.waiting.popleft()
+            a = self.allocator.allocate(r.prompt_ids, total)
+            r.blocks = list(a.blocks)
+            r.cached = r.computed = int(a.cached_tokens)
+            r.slot = self.free_slots.pop()
+            self.prefilling.append(r)
+            self.stats["cached_tokens"] += r.cached
+
+    def _prefill(self) -> None:
+        if not self.prefilling:
+            return
+        budget = self.max_prefill_tokens
+        chunk = []  # (req, start, end)
+        for r in self.prefilling:
+            if budget <= 0:
+                break
+            n = min(len(r.prompt_ids) - r.computed, budget)
+            chunk.append((r, r.computed, r.computed + n))
+            budget -= n
+        bs = self.block_size
+        ids, pos, slots, cu, ctx, last = [], [], [], [0], [], []
+        bt = torch.zeros(len(chunk), self.max_blocks_per_seq, dtype=torch.int32)
+        for i, (r, s, e) in enumerate(chunk):
+            ids += r.prompt_ids[s:e]
+            pos += range(s, e)
+            slots += [r.blocks[p // bs] * bs + p % bs for p in range(s, e)]
+            cu.append(cu[-1] + (e - s))
+            ctx.append(e)
+            last.append(cu[-1] - 1)
+            bt[i, :len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
+        dev = self.device
+        t = lambda x: torch.tensor(x, dtype=torch.int32).to(dev, non_blocking=True)
+        t0 = time.perf_counter()
+        logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx), bt.to(dev, non_blocking=True),
+                                            max(e - s for _, s, e in chunk), t(last))
+        self.stats["prefill_tokens"] += len(ids)
+        done = [(i, r) for i, (r, s, e) in enumerate(chunk) if e == len(r.prompt_ids)]
+        for r, s, e in chunk:
+            r.computed = e
+            self.allocator.commit_prefix(r.blocks, r.prompt_ids, e)
+        if done:
+            idx = torch.tensor([i for i, _ in done], device=dev)
+            sub = logits.index_select(1, idx).contiguous()   # [tp, n, Vs]
+            rs = [r for _, r in done]
+            temp = torch.tensor([r.params.temperature for r in rs], dtype=torch.float32, device=dev)
+            top_p = torch.tensor([r.params.top_p for r in rs], dtype=torch.float32, device=dev)
+            seeds = torch.tensor([r.seed for r in rs], dtype=torch.int32, device=dev)
+            ctr = torch.tensor([len(r.prompt_ids) for r in rs], dtype=torch.int32, device=dev)
+            toks = ops.sample(sub, temp, top_p, seeds, ctr, shards=sub.shape[0])
+            slots_t = torch.tensor([r.slot for r in rs], dtype=torch.long, device=dev)
+            self.s_tokens[slots_t] = toks
+            self.s_ctx[slots_t] = ctr + 1
+            self.s_hist[slots_t, 0] = toks
+            self.s_steps[slots_t] = 1
+            self.s_temp[slots_t] = temp
+            self.s_top_p[slots_t] = top_p
+            self.s_seeds[slots_t] = seeds
+            for r in rs:
+                row = torch.zeros(self.max_blocks_per_seq, dtype=torch.int32)
+                row[:len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
+                self.s_bt[r.slot] = row.to(dev, non_blocking=True)
+            now = time.perf_counter()
+            for r in rs:
+                r.first_token_time = now
+                self.prefilling.remove(r)
+                self.running[r.slot] = r
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+        self.stats["prefill_time"] += time.perf_counter() - t0
+
+    def _decode(self) -> List[Request]:
+        if not self.running:
+            return []
+        # aborted requests leave before the next chunk
+        for slot, r in list(self.running.items()):
+            if r.aborted:
+                self._finish(r, "abort")
+        if not self.running:
+            return []
+        remaining = min(r.params.max_tokens - len(r.output_ids) - (1 if not r.output_ids else 0)
+                        for r in self.running.values())
+        steps = max(1, min(self.decode_chunk, remaining))
+        B = self._bucket(max(self.running) + 1)
+        t0 = time.perf_counter()
+        graph = self.graphs.get(B) if self.use_graphs else None
+        for _ in range(steps):
+            if graph is not None:
+                graph.replay()
+                self.stats["graph_replays"] += 1
+            else:
+                self._decode_step(B)
+        self.stats["decode_steps"] += steps
+        hist = self.s_hist[:B].cpu()     # syncs the stream
+        nsteps = self.s_steps[:B].cpu()
+        self.stats["decode_time"] += time.perf_counter() - t0
+        finished = []
+        for slot, r in list(self.running.items()):
+            n = int(nsteps[slot])
+            new = hist[slot, len(r.output_ids):n].tolist()
+            self.stats["decode_tokens"] += len(new)
+            for tkn in new:
+                r.output_ids.append(tkn)
+                if self._stopped(r, tkn):
+                    break
+            if r.finished:
+                finished.append(r)
+            elif len(r.output_ids) >= r.params.max_tokens:
+                self._finish(r, "length")
+                finished.append(r)
+        if self.metrics is not None:
+            self.metrics.engine_tokens(sum(len(r.output_ids) for r in finished), self.kv_utilization())
+        return finished
+
+    def _stopped(self, r: Request, tkn: int) -> bool:
+        p = r.params
+        if not p.ignore_eos and (tkn in self.tok.eos_ids or tkn in p.stop_token_ids):
+            r.output_ids.pop()
+            self._finish(r, "stop")
+            return True
+        if p.stop_on_json_close and not p.ignore_eos and tkn in self._brace_ids():
+            if json_object_closed(self.tok.decode(r.output_ids)):
+                self._finish(r, "json")
+                return True
+        if len(r.output_ids) >= p.max_tokens:
+            self._finish(r, "length")
+            return True
+        return False
+
+    _brace_cache: Optional[set] = None
+
+    def _brace_ids(self) -> set:
+        if self._brace_cache is None:
+            vocab = self.tok._tok.get_vocab()
+            self._brace_cache = {i for s, i in vocab.items() if "}" in s or "}" in s}
+        return self._brace_cache
+
+    def _finish(self, r: Request, reason: str) -> None:
+        if r.finished:
+            return
+        r.finished = True
+        r.finish_reason = reason
+        r.finish_time = time.perf_counter()
+        if r.slot >= 0:
+            self.s_ctx[r.slot] = 0
+            self.s_steps[r.slot] = 0
+            self.running.pop(r.slot, None)
+            if r in self.prefilling:
+                self.prefilling.remove(r)
+            self.free_slots.append(r.slot)
+            self.free_slots.sort(reverse=True)
+            r.slot = -1
+        if r.blocks:
+            self.allocator.release(r.blocks)
+            r.blocks = []
+
+    def step(self) -> List[Request]:
+        with self.lock:
+            self._admit()
+            self._prefill()
+            return self._decode()
+
+    def kv_utilization(self) -> float:
+        return 1.0 - self.allocator.num_free / self.allocator.num_blocks
+
+    # ------------------------------------------------------------------ blocking API
+    def output(self, r: Request) -> Output:
+        end = r.finish_time or time.perf_counter()
+        return Output(r.rid, self.tok.decode(r.output_ids), list(r.output_ids), len(r.prompt_ids), r.cached,
+                      r.finish_reason, (r.first_token_time or end) - r.arrival, end - r.arrival)
+
+    def generate(self, prompts: Sequence[Union[str, List[int]]],
+                 params: Union[SamplingParams, Sequence[SamplingParams], None] = None,
+                 deadline: Optional[float] = None) -> List[Output]:
+        """Run the given requests to completion (continuous batching with whatever else is
+        queued).  ``deadline`` (time.monotonic) aborts unfinished requests and raises
+        TimeoutError -- the decision service counts that as an engine failure."""
+        if params is None or isinstance(params, SamplingParams):
+            params = [params or SamplingParams()] * len(prompts)
+        with self.lock:
+            reqs = [self.add_request(p, sp) for p, sp in zip(prompts, params)]
+            while not all(r.finished for r in reqs):
+                if deadline is not None and time.monotonic() > deadline:
+                    for r in reqs:
+                        if not r.finished:
+                            self._finish(r, "timeout")
+                    raise TimeoutError("decision engine deadline exceeded")
+                self.step()
+            outs = [self.output(r) for r in reqs]
+            for r in reqs:
+                self.requests.pop(r.rid, None)
+            return outs
+
+
+class _PyBlockAllocator:
+    """Pure-Python stand-in used only when the native extension is unavailable (CPU tests)."""
+
+    class _A:
+        def __init__(self, blocks, cached):
+            self.blocks, self.cached_tokens = blocks, cached
+
+    def __init__(self, num_blocks: int, block_size: int, prefix_caching: bool):
+        self.num_blocks, self.block_size = num_blocks, block_size
+        self._free = list(range(num_blocks - 1, -1, -1))
+
+    @property
+    def num_free(self) -> int:
+        return len(self._free)
+
+    def can_allocate(self, tokens, total) -> bool:
+        return math.ceil(total / self.block_size) <= len(self._free)
+
+    def allocate(self, tokens, total):
+        n = math.ceil(total / self.block_size)
+        if n > len(self._free):
+            raise RuntimeError("KV cache exhausted")
+        return self._A([self._free.pop() for _ in range(n)], 0)
+
+    def commit_prefix(self, blocks, tokens, n) -> None:
+        pass
+
+    def release(self, blocks) -> None:
+        self._free.extend(blocks)

@@ -1,0 +1,257 @@
+"""Llama-3 decoder (8B / 70B / tiny) with Megatron-style tensor parallelism.
+
+Sharding per rank (TP = t): QKV and gate/up are column-parallel (this rank's heads / FFN slice,
+fused into one weight each: ``wqkv`` = [q; k; v] rows, ``wgu`` = [gate; up] rows), O and down are
+row-parallel (followed by an all-reduce), the LM head is vocabulary-parallel (fp32 logits are
+all-gathered shard-major), the embedding is replicated (no collective on the input side).
+
+Every op on a CUDA tensor is a hand-written gfx950 kernel from ``ops`` except the prefill
+projections with more than 8 rows, which are plain library GEMMs (hipBLASLt).  The same code
+runs on CPU through the fp32 reference ops, which is how TP=k == TP=1 is tested with gloo.
+
+Weights: deterministic hash-uniform random init (identical global tensors for every TP degree
+and device; BASELINE allows random-init weights) or a HuggingFace safetensors checkpoint,
+loaded shard-by-shard with ``safetensors`` (no pickle).
+"""
+
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Dict, List, Optional
+
+import torch
+
+from .. import ops
+from ..ops import reference as ref
+from ..parallel import TPGroup
+from .config import LlamaConfig
+
+_TID_EMBED, _TID_LM, _TID_NORM = 1_000_001, 1_000_002, 1_000_003
+
+
+def _tid(layer: int, k: int) -> int:
+    return layer * 16 + k
+
+
+@dataclass
+class LayerWeights:
+    ln1: torch.Tensor
+    wqkv: torch.Tensor
+    wo: torch.Tensor
+    ln2: torch.Tensor
+    wgu: torch.Tensor
+    wdown: torch.Tensor
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, tp: Optional[TPGroup] = None, device: str | torch.device = "cpu",
+                 dtype: torch.dtype = torch.bfloat16, seed: int = 0, weights: Optional[str] = None,
+                 max_model_len: int = 8192):
+        self.cfg = cfg
+        self.tp = tp or TPGroup()
+        cfg.validate_tp(self.tp.world)
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.seed = seed
+        t, r = self.tp.world, self.tp.rank
+        self.nq = cfg.num_heads // t
+        if cfg.num_kv_heads >= t:
+            self.nkv = cfg.num_kv_heads // t
+            self.kv0 = r * self.nkv
+        else:  # replicate kv heads when tp > num_kv_heads
+            self.nkv = 1
+            self.kv0 = r * cfg.num_kv_heads // t
+        self.I = cfg.intermediate // t
+        self.Vs = cfg.vocab // t
+        self.D = cfg.head_dim
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.max_model_len = min(max_model_len, cfg.max_position)
+        self.cos_sin = ref.rope_table(self.D, self.max_model_len, cfg.rope_theta, cfg.rope_scaling).to(self.device)
+        self.layers: List[LayerWeights] = []
+        if weights:
+            self._load_safetensors(Path(weights))
+        else:
+            self._random_init()
+        self.kv_cache: Optional[torch.Tensor] = None
+        self.block_size = 16
+
+    # ------------------------------------------------------------------ weights
+    def _new(self, rows: int, cols: int) -> torch.Tensor:
+        return torch.empty(rows, cols, dtype=self.dtype, device=self.device)
+
+    def _random_init(self) -> None:
+        c, r, s = self.cfg, self.tp.rank, self.seed
+        H, D = c.hidden, self.D
+        a = c.init_std * math.sqrt(3.0)          # uniform(-a, a) has std init_std
+        a_out = a / math.sqrt(2.0 * c.num_layers)  # GPT-2 style residual-branch scaling
+        ones = lambda tid: ops.hash_init_(self._new(1, H), H, 0, 0, s, tid, 0.05, 1.0).view(H)
+        self.embed = ops.hash_init_(self._new(c.vocab, H), H, 0, 0, s, _TID_EMBED, a * 10)
+        for l in range(c.num_layers):
+            wqkv = self._new((self.nq + 2 * self.nkv) * D, H)
+            nq_rows = self.nq * D
+            kv_rows = self.nkv * D
+            ops.hash_init_(wqkv[:nq_rows], H, r * nq_rows, 0, s, _tid(l, 0), a)
+            ops.hash_init_(wqkv[nq_rows:nq_rows + kv_rows], H, self.kv0 * D, 0, s, _tid(l, 1), a)
+            ops.hash_init_(wqkv[nq_rows + kv_rows:], H, self.kv0 * D, 0, s, _tid(l, 2), a)
+            wo = ops.hash_init_(self._new(H, nq_rows), c.num_heads * D, 0, r * nq_rows, s, _tid(l, 3), a_out)
+            wgu = self._new(2 * self.I, H)
+            ops.hash_init_(wgu[:self.I], H, r * self.I, 0, s, _tid(l, 4), a)
+            ops.hash_init_(wgu[self.I:], H, r * self.I, 0, s, _tid(l, 5), a)
+            wd = ops.hash_init_(self._new(H, self.I), c.intermediate, 0, r * self.I, s, _tid(l, 6), a_out)
+            self.layers.append(LayerWeights(ones(_tid(l, 7)), wqkv, wo, ones(_tid(l, 8)), wgu, wd))
+        self.norm = ones(_TID_NORM)
+        self.lm_head = ops.hash_init_(self._new(self.Vs, H), H, r * self.Vs, 0, s, _TID_LM, a)
+
+    def _load_safetensors(self, path: Path) -> None:
+        from safetensors import safe_open
+
+        files = sorted(path.glob("*.safetensors"))
+        if not files:
+            raise FileNotFoundError(f"no *.safetensors in {path}")
+        index: Dict[str, Path] = {}
+        for f in files:
+            with safe_open(str(f), framework="pt") as h:
+                for k in h.keys():
+                    index[k] = f
+        handles: Dict[Path, object] = {}
+
+        def sl(name: str, dim: int = -1, start: int = 0, stop: Optional[int] = None) -> torch.Tensor:
+            f = index[name]
+            if f not in handles:
+                handles[f] = safe_open(str(f), framework="pt")
+            s = handles[f].get_slice(name)
+            if dim == 0:
+                t = s[start:stop]
+            elif dim == 1:
+                t = s[:, start:stop]
+            else:
+                t = s[:]
+            return t.to(dtype=self.dtype).to(self.device)
+
+        c, r, D = self.cfg, self.tp.rank, self.D
+        p = "model.layers.{}."
+        q_rows, kv_rows = self.nq * D, self.nkv * D
+        self.embed = sl("model.embed_tokens.weight")
+        for l in range(c.num_layers):
+            pre = p.format(l)
+            q = sl(pre + "self_attn.q_proj.weight", 0, r * q_rows, (r + 1) * q_rows)
+            k = sl(pre + "self_attn.k_proj.weight", 0, self.kv0 * D, self.kv0 * D + kv_rows)
+            v = sl(pre + "self_attn.v_proj.weight", 0, self.kv0 * D, self.kv0 * D + kv_rows)
+            o = sl(pre + "self_attn.o_proj.weight", 1, r * q_rows, (r + 1) * q_rows)
+            g = sl(pre + "mlp.gate_proj.weight", 0, r * self.I, (r + 1) * self.I)
+            u = sl(pre + "mlp.up_proj.weight", 0, r * self.I, (r + 1) * self.I)
+            d = sl(pre + "mlp.down_proj.weight", 1, r * self.I, (r + 1) * self.I)
+            self.layers.append(LayerWeights(sl(pre + "input_layernorm.weight"), torch.cat([q, k, v]).contiguous(),
+                                            o.contiguous(), sl(pre + "post_attention_layernorm.weight"),
+                                            torch.cat([g, u]).contiguous(), d.contiguous()))
+        self.norm = sl("model.norm.weight")
+        lm = "lm_head.weight" if "lm_head.weight" in index else "model.embed_tokens.weight"
+        self.lm_head = sl(lm, 0, r * self.Vs, (r + 1) * self.Vs).contiguous()
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + self.norm.numel() + self.lm_head.numel()
+        for w in self.layers:
+            n += sum(t.numel() for t in (w.ln1, w.wqkv, w.wo, w.ln2, w.wgu, w.wdown))
+        return n * self.embed.element_size()
+
+    # ------------------------------------------------------------------ KV cache
+    def allocate_kv(self, num_blocks: int, block_size: int) -> torch.Tensor:
+        self.block_size = block_size
+        self.kv_cache = torch.zeros(self.cfg.num_layers, 2, num_blocks * block_size, self.nkv, self.D,
+                                    dtype=self.dtype, device=self.device)
+        return self.kv_cache
+
+    def kv_bytes_per_block(self, block_size: int) -> int:
+        return self.cfg.num_layers * 2 * block_size * self.nkv * self.D * torch.finfo(self.dtype).bits // 8
+
+    # ------------------------------------------------------------------ forward
+    def _layers(self, h: torch.Tensor, attn) -> tuple:
+        """Run all decoder layers.  ``attn(l, qkv) -> [T, nq*D]`` does rope + KV write + attention."""
+        c = self.cfg
+        res = h.clone()
+        x = ops.rmsnorm(h, self.layers[0].ln1, c.rms_eps)
+        for l, w in enumerate(self.layers):
+            if l > 0:
+                x = ops.rmsnorm(h, w.ln1, c.rms_eps, residual=res)
+            qkv = ops.linear(x, w.wqkv)
+            a = attn(l, qkv)
+            o = ops.linear(a, w.wo)
+            self.tp.all_reduce_(o)
+            x = ops.rmsnorm(o, w.ln2, c.rms_eps, residual=res)
+            g = ops.linear_swiglu(x, w.wgu)
+            h = ops.linear(g, w.wdown)
+            self.tp.all_reduce_(h)
+        return h, res
+
+    def _logits(self, h: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
+        x = ops.rmsnorm(h, self.norm, self.cfg.rms_eps, residual=res)
+        logits = ops.linear(x, self.lm_head, out_dtype=torch.float32)   # [S, Vs]
+        return self.tp.all_gather_shards(logits)                         # [tp, S, Vs]
+
+    def forward_prefill(self, ids: torch.Tensor, positions: torch.Tensor, slot_mapping: torch.Tensor,
+                        cu_q: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
+                        max_qlen: int, last_idx: torch.Tensor) -> torch.Tensor:
+        """Varlen prefill (chunks of several sequences).  Returns gathered logits [tp, S, Vs] for
+        the token at ``last_idx`` of each sequence."""
+        T = ids.shape[0]
+        kv = self.kv_cache
+
+        def attn(l: int, qkv: torch.Tensor) -> torch.Tensor:
+            q = ops.rope_kv_write(qkv, self.cos_sin, kv[l, 0], kv[l, 1], self.nq, self.nkv, self.D,
+                                  positions=positions, slot_mapping=slot_mapping)
+            a = ops.paged_prefill_attention(q, kv[l, 0], kv[l, 1], cu_q, context_lens, block_tables,
+                                            self.scale, self.block_size, max_qlen)
+            return a.view(T, self.nq * self.D)
+
+        h, res = self._layers(ops.embedding(ids, self.embed), attn)
+        li = last_idx.long()
+        return self._logits(h.index_select(0, li).contiguous(), res.index_select(0, li).contiguous())
+
+    def forward_decode(self, tokens: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
+                       max_context: int) -> torch.Tensor:
+        """One decode step for B sequences (one token each, positions from context_lens)."""
+        B = tokens.shape[0]
+        kv = self.kv_cache
+
+        def attn(l: int, qkv: torch.Tensor) -> torch.Tensor:
+            q = ops.rope_kv_write(qkv, self.cos_sin, kv[l, 0], kv[l, 1], self.nq, self.nkv, self.D,
+                                  context_lens=context_lens, block_tables=block_tables, block_size=self.block_size)
+            a = ops.paged_decode_attention(q, kv[l, 0], kv[l, 1], block_tables, context_lens, self.scale,
+                                           self.block_size, max_context)
+            return a.view(B, self.nq * self.D)
+
+        h, res = self._layers(ops.embedding(tokens, self.embed), attn)
+        return self._logits(h, res)
+
+
+def save_hf_checkpoint(model: LlamaModel, path: Path) -> None:
+    """Write a TP=1 model as a HuggingFace-layout safetensors checkpoint (tests/tools)."""
+    from safetensors.torch import save_file
+
+    assert model.tp.world == 1
+    c, D = model.cfg, model.D
+    t: Dict[str, torch.Tensor] = {"model.embed_tokens.weight": model.embed, "model.norm.weight": model.norm,
+                                  "lm_head.weight": model.lm_head}
+    for l, w in enumerate(model.layers):
+        p = f"model.layers.{l}."
+        q_rows, kv_rows = c.num_heads * D, c.num_kv_heads * D
+        t[p + "self_attn.q_proj.weight"] = w.wqkv[:q_rows]
+        t[p + "self_attn.k_proj.weight"] = w.wqkv[q_rows:q_rows + kv_rows]
+        t[p + "self_attn.v_proj.weight"] = w.wqkv[q_rows + kv_rows:]
+        t[p + "self_attn.o_proj.weight"] = w.wo
+        t[p + "mlp.gate_proj.weight"] = w.wgu[:c.intermediate]
+        t[p + "mlp.up_proj.weight"] = w.wgu[c.intermediate:]
+        t[p + "mlp.down_proj.weight"] = w.wdown
+        t[p + "input_layernorm.weight"] = w.ln1
+        t[p + "post_attention_layernorm.weight"] = w.ln2
+    path.mkdir(parents=True, exist_ok=True)
+    save_file({k: v.contiguous().cpu() for k, v in t.items()}, str(path / "model.safetensors"))
+    (path / "config.json").write_text(json.dumps({
+        "hidden_size": c.hidden, "num_attention_heads": c.num_heads, "num_key_value_heads": c.num_kv_heads,
+        "head_dim": c.head_dim, "intermediate_size": c.intermediate, "vocab_size": c.vocab,
+        "num_hidden_layers": c.num_layers, "rms_norm_eps": c.rms_eps, "rope_theta": c.rope_theta,
+        "rope_scaling": c.rope_scaling, "max_position_embeddings": c.max_position, "bos_token_id": c.bos_id,
+        "eos_token_id": list(c.eos_ids)}))

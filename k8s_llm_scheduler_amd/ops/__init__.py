@@ -1,0 +1,263 @@
+"""Device ops: gfx950 HIP kernels (``_C``) behind shape-checked wrappers.
+
+Dispatch rule: CUDA (= HIP) tensors ALWAYS run the hand-written kernels; if the extension is
+missing on a GPU the call raises (no silent PyTorch fallback).  CPU tensors run the fp32
+reference in :mod:`.reference` -- that path exists for the CPU test-suite (gloo multi-process
+tensor-parallel tests) and is the numerics oracle of the kernel tests.
+"""
+
+from __future__ import annotations
+
+import importlib
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import reference as ref
+
+_C = None
+_C_ERR: Optional[BaseException] = None
+try:  # torch must be imported first: the extension binds to torch's HIP runtime
+    _C = importlib.import_module("k8s_llm_scheduler_amd.ops._C")
+except Exception as e:  # pragma: no cover - reported loudly on first GPU use
+    _C_ERR = e
+
+EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
+DECODE_PARTITION = 256
+
+
+def native():
+    """The loaded extension module; raises with the build hint if it is missing."""
+    if _C is None:
+        raise RuntimeError("k8s_llm_scheduler_amd native extension (_C) is not built/loadable: "
+                           f"{_C_ERR!r}. Run: python -m k8s_llm_scheduler_amd._build")
+    return _C
+
+
+def available() -> bool:
+    return _C is not None
+
+
+def _gpu(*ts: torch.Tensor) -> bool:
+    cuda = [t.is_cuda for t in ts if t is not None]
+    if any(cuda) and not all(cuda):
+        raise ValueError("mixed CPU/GPU tensors")
+    return bool(cuda) and cuda[0]
+
+
+def _chk(t: torch.Tensor, dtype, name: str) -> int:
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    return t.data_ptr()
+
+
+BF16, F32, I32 = torch.bfloat16, torch.float32, torch.int32
+
+
+# ----------------------------------------------------------------------------- norms
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """RMSNorm; with ``residual`` the kernel first does residual += x (in place) and normalises
+    the sum (fused add + norm)."""
+    if not _gpu(x, w, residual):
+        y, _ = ref.rmsnorm(x, w, eps, residual)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    H = x.shape[-1]
+    rows = x.numel() // H
+    out = torch.empty_like(x) if out is None else out
+    native().rmsnorm(_chk(out, BF16, "out"), _chk(x, BF16, "x"),
+                     _chk(residual, BF16, "residual") if residual is not None else 0,
+                     _chk(w, BF16, "w"), rows, H, float(eps), -1)
+    return out
+
+
+# ----------------------------------------------------------------------------- rope + kv
+def rope_kv_write(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                  nq: int, nkv: int, D: int, *, positions: Optional[torch.Tensor] = None,
+                  slot_mapping: Optional[torch.Tensor] = None, context_lens: Optional[torch.Tensor] = None,
+                  block_tables: Optional[torch.Tensor] = None, block_size: int = 16) -> torch.Tensor:
+    """Rotate q/k, write k/v into the paged cache; returns rotated q [T, nq, D].
+    Prefill mode: positions + slot_mapping.  Decode mode: context_lens + block_tables."""
+    T = qkv.shape[0]
+    if qkv.shape[-1] != (nq + 2 * nkv) * D:
+        raise ValueError("qkv width mismatch")
+    if not _gpu(qkv, k_cache):
+        if positions is None:
+            positions, slot_mapping = ref.decode_positions(context_lens, block_tables, block_size)
+        return ref.rope_kv_write(qkv, cos_sin, positions, slot_mapping, k_cache, v_cache, nq, nkv, D).view(T, nq, D)
+    q = torch.empty(T, nq, D, dtype=qkv.dtype, device=qkv.device)
+    if positions is not None:
+        p_pos, p_slot, p_ctx, p_bt, mb = _chk(positions, I32, "positions"), _chk(slot_mapping, I32, "slots"), 0, 0, 0
+    else:
+        p_pos = p_slot = 0
+        p_ctx, p_bt, mb = _chk(context_lens, I32, "context_lens"), _chk(block_tables, I32, "block_tables"), \
+            block_tables.shape[1]
+    native().rope_kv_write(q.data_ptr(), _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
+                           _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"), p_pos, p_slot, p_ctx, p_bt,
+                           mb, block_size, T, nq, nkv, D, -1)
+    return q
+
+
+# ----------------------------------------------------------------------------- attention
+def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                           context_lens: torch.Tensor, scale: float, block_size: int, max_context: int) -> torch.Tensor:
+    """q [B, nq, D]; returns [B, nq, D].  ``max_context`` bounds the partition grid (fixed for
+    a captured graph)."""
+    if not _gpu(q, k_cache):
+        return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, context_lens, scale, block_size)
+    B, nq, D = q.shape
+    nkv = k_cache.shape[-2]
+    pmax = max(1, math.ceil(max_context / DECODE_PARTITION))
+    out = torch.empty_like(q)
+    if pmax > 1:
+        pacc = torch.empty(B * nq * pmax * D, dtype=F32, device=q.device)
+        pml = torch.empty(B * nq * pmax * 2, dtype=F32, device=q.device)
+        pa, pm = pacc.data_ptr(), pml.data_ptr()
+    else:
+        pa = pm = 0
+    native().paged_decode_attention(out.data_ptr(), pa, pm, _chk(q, BF16, "q"), _chk(k_cache, BF16, "k_cache"),
+                                    _chk(v_cache, BF16, "v_cache"), _chk(block_tables, I32, "block_tables"),
+                                    _chk(context_lens, I32, "context_lens"), float(scale), B, nq, nkv, D, block_size,
+                                    block_tables.shape[1], DECODE_PARTITION, pmax, -1)
+    return out
+
+
+def paged_prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, cu_q: torch.Tensor,
+                            context_lens: torch.Tensor, block_tables: torch.Tensor, scale: float, block_size: int,
+                            max_qlen: int) -> torch.Tensor:
+    """q [T, nq, D] (varlen over sequences by cu_q); causal over the paged cache."""
+    if not _gpu(q, k_cache):
+        return ref.paged_prefill_attention(q, k_cache, v_cache, cu_q, context_lens, block_tables, scale, block_size)
+    T, nq, D = q.shape
+    nkv = k_cache.shape[-2]
+    out = torch.empty_like(q)
+    native().paged_prefill_attention(out.data_ptr(), _chk(q, BF16, "q"), _chk(k_cache, BF16, "k_cache"),
+                                     _chk(v_cache, BF16, "v_cache"), _chk(cu_q, I32, "cu_q"),
+                                     _chk(context_lens, I32, "context_lens"), _chk(block_tables, I32, "block_tables"),
+                                     float(scale), context_lens.shape[0], int(max_qlen), nq, nkv, D, block_size,
+                                     block_tables.shape[1], -1)
+    return out
+
+
+# ----------------------------------------------------------------------------- linear
+GEMV_MAX_M = 8
+
+
+def _gemv(x: torch.Tensor, w: torch.Tensor, epi: int, out_dtype) -> torch.Tensor:
+    M, K = x.shape
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    out = torch.empty(M, N, dtype=out_dtype, device=x.device)
+    ks, splits = native().gemv_plan(M, N, K, epi)
+    part = 0
+    if splits > 1:
+        wrows = w.shape[0]
+        part = torch.empty(splits * M * wrows, dtype=F32, device=x.device)
+        pp = part.data_ptr()
+    else:
+        pp = 0
+    native().gemv(out.data_ptr(), pp, _chk(x, BF16, "x"), _chk(w, BF16, "w"), M, N, K, epi, -1)
+    del part
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
+    """y = x @ w.T with w [N, K] bf16.  M <= 8 rows: hand-written HBM-streaming GEMV;
+    larger M (prefill): library GEMM (hipBLASLt via torch)."""
+    if not _gpu(x, w):
+        return ref.linear(x, w, out_dtype)
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.shape[0] <= GEMV_MAX_M:
+        y = _gemv(x2.contiguous(), w, EPI_F32 if out_dtype == F32 else EPI_BF16, out_dtype or BF16)
+    else:
+        y = torch.nn.functional.linear(x2, w)
+        if out_dtype is not None and out_dtype != y.dtype:
+            y = y.to(out_dtype)
+    return y.view(*x.shape[:-1], y.shape[-1])
+
+
+def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
+    """silu(x @ Wg.T) * (x @ Wu.T) with w_gate_up = [Wg; Wu] ([2I, K])."""
+    if not _gpu(x, w_gate_up):
+        return ref.linear_swiglu(x, w_gate_up)
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.shape[0] <= GEMV_MAX_M:
+        y = _gemv(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
+    else:
+        y = silu_mul(torch.nn.functional.linear(x2, w_gate_up))
+    return y.view(*x.shape[:-1], y.shape[-1])
+
+
+def silu_mul(gu: torch.Tensor) -> torch.Tensor:
+    if not _gpu(gu):
+        return ref.silu_mul(gu)
+    I = gu.shape[-1] // 2
+    T = gu.numel() // (2 * I)
+    out = torch.empty(*gu.shape[:-1], I, dtype=gu.dtype, device=gu.device)
+    native().silu_mul(out.data_ptr(), _chk(gu, BF16, "gu"), T, I, -1)
+    return out
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    if not _gpu(ids, table):
+        return ref.embedding(ids, table)
+    T = ids.numel()
+    out = torch.empty(T, table.shape[1], dtype=table.dtype, device=table.device)
+    native().embedding(out.data_ptr(), _chk(ids, I32, "ids"), _chk(table, BF16, "table"), T, table.shape[1],
+                       table.shape[0], -1)
+    return out
+
+
+# ----------------------------------------------------------------------------- sampling
+def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor,
+           counter: torch.Tensor, *, shards: int = 1, tokens_out: Optional[torch.Tensor] = None,
+           ctx_inc: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None,
+           steps: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sample one token per row.  logits: [B, V] or sharded [shards, B, Vs] fp32.  Optionally
+    updates decode state in place: tokens_out[b] = tok, ctx_inc[b] += 1, hist[b, steps[b]] = tok,
+    steps[b] += 1 (rows with ctx_inc[b] <= 0 are padding and untouched)."""
+    if logits.dim() == 3:
+        S, B, Vs = logits.shape
+    else:
+        (B, Vs), S = logits.shape, 1
+    if not _gpu(logits):
+        full = logits.permute(1, 0, 2).reshape(B, S * Vs) if logits.dim() == 3 else logits
+        toks = ref.sample(full, temperature, top_p, seeds, counter)
+        active = ctx_inc > 0 if ctx_inc is not None else torch.ones(B, dtype=torch.bool)
+        if tokens_out is not None:
+            tokens_out[:B] = torch.where(active, toks, tokens_out[:B])
+        if hist is not None:
+            for b in range(B):
+                if active[b] and int(steps[b]) < hist.shape[1]:
+                    hist[b, int(steps[b])] = toks[b]
+            steps[:B] += active.to(steps.dtype)
+        if ctx_inc is not None:
+            ctx_inc[:B] += active.to(ctx_inc.dtype)
+        return toks
+    out = tokens_out if tokens_out is not None else torch.empty(B, dtype=I32, device=logits.device)
+    native().sample(_chk(out, I32, "tokens"), _chk(logits, F32, "logits"), B, Vs, S,
+                    _chk(temperature, F32, "temperature"), _chk(top_p, F32, "top_p"),
+                    _chk(seeds, I32, "seeds"), _chk(counter, I32, "counter"),
+                    _chk(ctx_inc, I32, "ctx_inc") if ctx_inc is not None else 0,
+                    _chk(hist, I32, "hist") if hist is not None else 0,
+                    hist.shape[1] if hist is not None else 0,
+                    _chk(steps, I32, "steps") if steps is not None else 0, -1)
+    return out
+
+
+# ----------------------------------------------------------------------------- init
+def hash_init_(out: torch.Tensor, gcols: int, row0: int, col0: int, seed: int, tensor_id: int,
+               scale: float, shift: float = 0.0) -> torch.Tensor:
+    """Fill a 2-D bf16 shard with the deterministic hash-uniform init (see reference.hash_init)."""
+    rows, cols = out.shape
+    if not out.is_cuda:
+        out.copy_(ref.hash_init(rows, cols, gcols, row0, col0, seed, tensor_id, scale, shift, out.dtype))
+        return out
+    native().hash_init(_chk(out, BF16, "out"), rows, cols, gcols, row0, col0, seed & 0xFFFFFFFF,
+                       tensor_id & 0xFFFFFFFF, float(scale), float(shift), -1)
+    return out

@@ -1,0 +1,221 @@
+"""Plain-PyTorch fp32 reference implementations of every HIP kernel.
+
+They define the semantics the kernels are tested against (T3 numerics tests compare a kernel
+with the function of the same name here) and they run the model on CPU for the multi-process
+``gloo`` tests (TP=k vs TP=1).  They are never used for CUDA tensors: the wrappers in
+``ops/__init__.py`` refuse to fall back on a GPU.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+U32 = 0xFFFFFFFF
+
+
+# ----------------------------------------------------------------------------- hashing / RNG
+def _fmix32(h: torch.Tensor) -> torch.Tensor:
+    h = h & U32
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & U32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & U32
+    h = h ^ (h >> 16)
+    return h
+
+
+def hash3(a, b, c: torch.Tensor) -> torch.Tensor:
+    """Same bits as common.h hash3 (int64 tensors holding uint32 values)."""
+    c = torch.as_tensor(c, dtype=torch.int64)
+    b = torch.as_tensor(b, dtype=torch.int64, device=c.device)
+    a = torch.as_tensor(a, dtype=torch.int64, device=c.device)
+    inner = _fmix32((c + 0x7F4A7C15) & U32)
+    mid = _fmix32((((b + 0x9E3779B9) & U32) ^ inner) & U32)
+    return _fmix32((a ^ mid) & U32)
+
+
+def u01(h: torch.Tensor) -> torch.Tensor:
+    return ((h >> 8).to(torch.float64) + 0.5) * (1.0 / 16777216.0)
+
+
+def hash_init(rows: int, cols: int, gcols: int, row0: int, col0: int, seed: int, tensor_id: int,
+              scale: float, shift: float, dtype=torch.bfloat16, device="cpu") -> torch.Tensor:
+    r = torch.arange(rows, dtype=torch.int64, device=device).unsqueeze(1) + row0
+    c = torch.arange(cols, dtype=torch.int64, device=device).unsqueeze(0) + col0
+    flat = (r * gcols + c) & U32
+    u = u01(hash3(seed, tensor_id, flat)).to(torch.float32)
+    return ((2.0 * u - 1.0) * scale + shift).to(dtype)
+
+
+# ----------------------------------------------------------------------------- layers
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float,
+            residual: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    if residual is not None:
+        r = (x.float() + residual.float()).to(x.dtype)
+        residual.copy_(r)
+        x = r
+    xf = x.float()
+    out = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return out.to(x.dtype), residual
+
+
+def rope_table(head_dim: int, max_pos: int, theta: float, scaling: Optional[dict] = None) -> torch.Tensor:
+    """[max_pos, head_dim] fp32: cos in [:, :D/2], sin in [:, D/2:] (llama3 scaling if given)."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling["factor"]
+        lo, hi = scaling["low_freq_factor"], scaling["high_freq_factor"]
+        old = scaling["original_max_position_embeddings"]
+        lo_wl, hi_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv
+        inv_l = torch.where(wl > lo_wl, inv / factor, inv)
+        smooth = (old / wl - lo) / (hi - lo)
+        smoothed = (1 - smooth) * inv_l / factor + smooth * inv_l
+        medium = (wl >= hi_wl) & (wl <= lo_wl)
+        inv = torch.where(medium, smoothed, inv_l)
+    pos = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(pos, inv)
+    return torch.cat([f.cos(), f.sin()], dim=-1).float()
+
+
+def _rotate(x: torch.Tensor, cs: torch.Tensor) -> torch.Tensor:
+    # x [..., D] fp32, cs [..., D] (cos | sin)
+    h = x.shape[-1] // 2
+    c, s = cs[..., :h], cs[..., h:]
+    x1, x2 = x[..., :h], x[..., h:]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+def rope_kv_write(qkv: torch.Tensor, cos_sin: torch.Tensor, positions: torch.Tensor, slot_mapping: torch.Tensor,
+                  k_cache: torch.Tensor, v_cache: torch.Tensor, nq: int, nkv: int, D: int) -> torch.Tensor:
+    T = qkv.shape[0]
+    x = qkv.view(T, nq + 2 * nkv, D).float()
+    cs = cos_sin[positions.long()].unsqueeze(1)
+    q = _rotate(x[:, :nq], cs).to(qkv.dtype)
+    k = _rotate(x[:, nq:nq + nkv], cs).to(qkv.dtype)
+    v = x[:, nq + nkv:].to(qkv.dtype)
+    keep = slot_mapping >= 0
+    sl = slot_mapping[keep].long()
+    k_cache.view(-1, nkv, D)[sl] = k[keep]
+    v_cache.view(-1, nkv, D)[sl] = v[keep]
+    return q.contiguous()
+
+
+def decode_positions(context_lens: torch.Tensor, block_tables: torch.Tensor, block_size: int):
+    pos = (context_lens - 1).clamp(min=0).long()
+    blk = block_tables.long().gather(1, (pos // block_size).unsqueeze(1)).squeeze(1)
+    slots = blk * block_size + pos % block_size
+    slots = torch.where(context_lens > 0, slots, torch.full_like(slots, -1))
+    return pos.int(), slots.int()
+
+
+def _gather_kv(cache: torch.Tensor, bt_row: torch.Tensor, n: int, block_size: int, kvh: int) -> torch.Tensor:
+    idx = torch.arange(n, device=cache.device)
+    slots = bt_row.long()[idx // block_size] * block_size + idx % block_size
+    return cache.view(-1, cache.shape[-2], cache.shape[-1])[slots, kvh].float()   # [n, D]
+
+
+def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                           context_lens: torch.Tensor, scale: float, block_size: int) -> torch.Tensor:
+    B, nq, D = q.shape
+    nkv = k_cache.shape[-2]
+    G = nq // nkv
+    out = torch.zeros_like(q)
+    for b in range(B):
+        n = int(context_lens[b])
+        if n <= 0:
+            continue
+        for kvh in range(nkv):
+            K = _gather_kv(k_cache, block_tables[b], n, block_size, kvh)
+            V = _gather_kv(v_cache, block_tables[b], n, block_size, kvh)
+            qq = q[b, kvh * G:(kvh + 1) * G].float()
+            p = torch.softmax(qq @ K.T * scale, dim=-1)
+            out[b, kvh * G:(kvh + 1) * G] = (p @ V).to(q.dtype)
+    return out
+
+
+def paged_prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, cu_q: torch.Tensor,
+                            context_lens: torch.Tensor, block_tables: torch.Tensor, scale: float,
+                            block_size: int) -> torch.Tensor:
+    T, nq, D = q.shape
+    nkv = k_cache.shape[-2]
+    G = nq // nkv
+    out = torch.zeros_like(q)
+    cu = cu_q.tolist()
+    for s in range(len(cu) - 1):
+        q0, q1 = cu[s], cu[s + 1]
+        qlen = q1 - q0
+        if qlen == 0:
+            continue
+        ctx = int(context_lens[s])
+        qpos = torch.arange(ctx - qlen, ctx, device=q.device)
+        kpos = torch.arange(ctx, device=q.device)
+        mask = kpos[None, :] <= qpos[:, None]
+        for kvh in range(nkv):
+            K = _gather_kv(k_cache, block_tables[s], ctx, block_size, kvh)
+            V = _gather_kv(v_cache, block_tables[s], ctx, block_size, kvh)
+            for g in range(G):
+                h = kvh * G + g
+                sc = (q[q0:q1, h].float() @ K.T) * scale
+                sc = sc.masked_fill(~mask, float("-inf"))
+                out[q0:q1, h] = (torch.softmax(sc, -1) @ V).to(q.dtype)
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
+    y = x.float() @ w.float().T
+    return y.to(out_dtype or x.dtype)
+
+
+def silu_mul(gu: torch.Tensor) -> torch.Tensor:
+    I = gu.shape[-1] // 2
+    g, u = gu[..., :I].float(), gu[..., I:].float()
+    return (torch.nn.functional.silu(g) * u).to(gu.dtype)
+
+
+def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
+    gu = x.float() @ w_gate_up.float().T
+    I = gu.shape[-1] // 2
+    return (torch.nn.functional.silu(gu[..., :I]) * gu[..., I:]).to(x.dtype)
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    return table[ids.long().clamp(0, table.shape[0] - 1)]
+
+
+def _ord_key(l: torch.Tensor) -> torch.Tensor:
+    u = l.float().contiguous().view(torch.int32).to(torch.int64) & U32
+    neg = (u & 0x80000000) != 0
+    return torch.where(neg, (~u) & U32, u | 0x80000000)
+
+
+def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor,
+           counter: torch.Tensor) -> torch.Tensor:
+    """logits [B, V] fp32 -> tokens [B] int32, bit-compatible with sampler.hip (up to fp rounding
+    of the Gumbel scores)."""
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    vid = torch.arange(V, dtype=torch.int64, device=logits.device)
+    for b in range(B):
+        l = logits[b].float()
+        T = float(temperature[b])
+        if T <= 0:
+            out[b] = int(torch.argmax(l))
+            continue
+        keep = torch.ones(V, dtype=torch.bool, device=l.device)
+        P = float(top_p[b])
+        if P < 1.0:
+            probs = torch.softmax(l / T, -1).double()
+            order = torch.argsort(l, descending=True, stable=True)
+            cum = torch.cumsum(probs[order], 0)
+            k = int(torch.searchsorted(cum, torch.tensor(P * float(cum[-1]), dtype=cum.dtype, device=cum.device)))
+            thr = _ord_key(l[order[min(k, V - 1)]].reshape(1))
+            keep = _ord_key(l) >= thr
+        u = u01(hash3(int(seeds[b]), int(counter[b]), vid)).float()
+        g = -torch.log(-torch.log(u))
+        score = torch.where(keep, l / T + g, torch.full_like(l, float("-inf")))
+        out[b] = int(torch.argmax(score))
+    return out

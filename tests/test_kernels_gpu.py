@@ -1,0 +1,227 @@
+"""T3: every HIP kernel vs its plain-PyTorch fp32 reference (ops/reference.py) on an MI355X,
+at Llama-3 shapes per TP slice."""
+
+import math
+
+import pytest
+import torch
+
+from k8s_llm_scheduler_amd import ops
+from k8s_llm_scheduler_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ops.native()  # loud failure if the extension is missing on a GPU box
+
+
+def rnd(*shape, scale=1.0, dtype=torch.bfloat16, gen=None):
+    return (torch.randn(*shape, generator=gen, device=DEV) * scale).to(dtype)
+
+
+def close(a, b, atol, rtol=2e-2):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
+
+
+@pytest.mark.parametrize("H,rows", [(8192, 1), (8192, 5), (4096, 33), (512, 3)])
+def test_rmsnorm(H, rows):
+    x, w = rnd(rows, H), rnd(H, scale=0.5) + 1
+    r = rnd(rows, H)
+    got = ops.rmsnorm(x, w, 1e-5)
+    want, _ = ref.rmsnorm(x.cpu(), w.cpu(), 1e-5)
+    close(got, want, 2e-2)
+    r_gpu, r_cpu = r.clone(), r.cpu().clone()
+    got = ops.rmsnorm(x, w, 1e-5, residual=r_gpu)
+    want, _ = ref.rmsnorm(x.cpu(), w.cpu(), 1e-5, residual=r_cpu)
+    close(r_gpu, r_cpu, 0, 0)
+    close(got, want, 2e-2)
+
+
+@pytest.mark.parametrize("nq,nkv", [(8, 1), (64, 8), (16, 2)])
+def test_rope_kv_write_prefill_and_decode(nq, nkv):
+    D, T, bs = 128, 37, 16
+    scaling = dict(rope_type="llama3", factor=8.0, low_freq_factor=1.0, high_freq_factor=4.0,
+                   original_max_position_embeddings=8192)
+    cs = ref.rope_table(D, 4096, 500000.0, scaling).to(DEV)
+    qkv = rnd(T, (nq + 2 * nkv) * D)
+    nslots = 64 * bs
+    kc = torch.zeros(nslots, nkv, D, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(nslots, device=DEV)[:T].int()
+    slots[3] = -1
+    q = ops.rope_kv_write(qkv, cs, kc, vc, nq, nkv, D, positions=pos, slot_mapping=slots)
+    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    qr = ref.rope_kv_write(qkv.cpu(), cs.cpu(), pos.cpu(), slots.cpu(), kr, vr, nq, nkv, D)
+    close(q, qr.view(T, nq, D), 2e-2)
+    close(kc, kr, 2e-2)
+    close(vc, vr, 0, 0)
+    # decode addressing: ctx lens + block tables
+    B = 4
+    bt = torch.randperm(64, device=DEV)[: B * 8].view(B, 8).int()
+    ctx = torch.tensor([1, 17, 128, 0], device=DEV, dtype=torch.int32)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    q2 = ops.rope_kv_write(qkv[:B], cs, kc2, vc2, nq, nkv, D, context_lens=ctx, block_tables=bt, block_size=bs)
+    p, s = ref.decode_positions(ctx.cpu(), bt.cpu(), bs)
+    kr2, vr2 = torch.zeros_like(kc2).cpu(), torch.zeros_like(vc2).cpu()
+    qr2 = ref.rope_kv_write(qkv[:B].cpu(), cs.cpu(), p, s, kr2, vr2, nq, nkv, D)
+    close(q2[:3], qr2.view(B, nq, D)[:3], 2e-2)
+    close(kc2, kr2, 2e-2)
+
+
+def _paged_cache(nkv, D, bs, nblocks, gen=None):
+    kc = rnd(nblocks * bs, nkv, D, gen=gen)
+    vc = rnd(nblocks * bs, nkv, D, gen=gen)
+    return kc, vc
+
+
+@pytest.mark.parametrize("nq,nkv", [(8, 1), (64, 8), (32, 8), (16, 16)])
+@pytest.mark.parametrize("ctxs", [[1, 5, 300], [1000, 2, 513], [4097]])
+def test_paged_decode_attention(nq, nkv, ctxs):
+    D, bs = 128, 16
+    B = len(ctxs)
+    maxb = (max(ctxs) + bs - 1) // bs
+    nblocks = B * maxb + 3
+    kc, vc = _paged_cache(nkv, D, bs, nblocks)
+    bt = torch.randperm(nblocks, device=DEV)[: B * maxb].view(B, maxb).int()
+    ctx = torch.tensor(ctxs, device=DEV, dtype=torch.int32)
+    q = rnd(B, nq, D)
+    scale = 1 / math.sqrt(D)
+    for max_context in (max(ctxs), 8192):
+        got = ops.paged_decode_attention(q, kc, vc, bt, ctx, scale, bs, max_context)
+        want = ref.paged_decode_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), ctx.cpu(), scale, bs)
+        close(got, want, 2e-2)
+
+
+@pytest.mark.parametrize("nq,nkv", [(8, 1), (64, 8), (4, 2)])
+@pytest.mark.parametrize("qlens,cached", [([37], [0]), ([130, 1, 64], [0, 5, 17]), ([200], [160])])
+def test_paged_prefill_attention(nq, nkv, qlens, cached):
+    D, bs = 128, 16
+    S = len(qlens)
+    ctxs = [q + c for q, c in zip(qlens, cached)]
+    maxb = (max(ctxs) + bs - 1) // bs
+    nblocks = S * maxb + 2
+    kc, vc = _paged_cache(nkv, D, bs, nblocks)
+    bt = torch.randperm(nblocks, device=DEV)[: S * maxb].view(S, maxb).int()
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), device=DEV, dtype=torch.int32)
+    ctx = torch.tensor(ctxs, device=DEV, dtype=torch.int32)
+    q = rnd(sum(qlens), nq, D)
+    scale = 1 / math.sqrt(D)
+    got = ops.paged_prefill_attention(q, kc, vc, cu, ctx, bt, scale, bs, max(qlens))
+    want = ref.paged_prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), cu.cpu(), ctx.cpu(), bt.cpu(), scale, bs)
+    close(got, want, 2e-2)
+
+
+def test_prefill_attention_spike_forces_rescale():
+    """T13-style: a late key with a huge score forces the online-softmax rescale branch."""
+    nq, nkv, D, bs = 8, 1, 128, 16
+    L = 300
+    kc, vc = _paged_cache(nkv, D, bs, 32)
+    bt = torch.arange(32, device=DEV, dtype=torch.int32).view(1, 32)
+    q = rnd(L, nq, D)
+    kc[250, 0] = q[280, 3] * 4  # key 250 dominates query 280 / head 3
+    cu = torch.tensor([0, L], device=DEV, dtype=torch.int32)
+    ctx = torch.tensor([L], device=DEV, dtype=torch.int32)
+    got = ops.paged_prefill_attention(q, kc, vc, cu, ctx, bt, 1 / math.sqrt(D), bs, L)
+    want = ref.paged_prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), cu.cpu(), ctx.cpu(), bt.cpu(), 1 / math.sqrt(D), bs)
+    close(got, want, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("N,K", [(1280, 8192), (8192, 1024), (16032, 8192), (8192, 3584), (96, 512)])
+def test_gemv(M, N, K):
+    x, w = rnd(M, K), rnd(N, K, scale=0.05)
+    got = ops.linear(x, w)
+    want = ref.linear(x.cpu(), w.cpu())
+    close(got, want, 3e-2)
+    got32 = ops.linear(x, w, out_dtype=torch.float32)
+    close(got32, ref.linear(x.cpu(), w.cpu(), torch.float32), 1e-2, 1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 4, 8])
+@pytest.mark.parametrize("I,K", [(3584, 8192), (128, 512)])
+def test_gemv_swiglu(M, I, K):
+    x, w = rnd(M, K), rnd(2 * I, K, scale=0.05)
+    close(ops.linear_swiglu(x, w), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)
+
+
+def test_prefill_linear_and_silu_mul():
+    x, w = rnd(300, 1024), rnd(2 * 512, 1024, scale=0.05)
+    close(ops.linear_swiglu(x, w), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)
+
+
+def test_embedding():
+    table = rnd(1000, 512)
+    ids = torch.tensor([0, 999, 5, 5, 17], device=DEV, dtype=torch.int32)
+    close(ops.embedding(ids, table), ref.embedding(ids.cpu(), table.cpu()), 0, 0)
+
+
+def test_sampler_greedy_and_state_update():
+    B, V = 3, 128256
+    logits = torch.randn(B, V, device=DEV)
+    logits[1, 77777] = 50.0
+    t = torch.zeros(B, device=DEV)
+    p = torch.ones(B, device=DEV)
+    seeds = torch.arange(B, device=DEV, dtype=torch.int32)
+    ctx = torch.tensor([5, 9, 0], device=DEV, dtype=torch.int32)
+    hist = torch.full((B, 4), -1, device=DEV, dtype=torch.int32)
+    steps = torch.zeros(B, device=DEV, dtype=torch.int32)
+    toks = torch.zeros(B, device=DEV, dtype=torch.int32)
+    ops.sample(logits, t, p, seeds, ctx, tokens_out=toks, ctx_inc=ctx, hist=hist, steps=steps)
+    want = logits.argmax(-1).int()
+    assert toks[:2].tolist() == want[:2].tolist() and toks[1].item() == 77777
+    assert ctx.tolist() == [6, 10, 0] and steps.tolist() == [1, 1, 0] and hist[:, 0].tolist()[:2] == want[:2].tolist()
+
+
+def test_sampler_sharded_layout_matches_flat():
+    S, B, Vs = 8, 2, 16032
+    logits = torch.randn(S, B, Vs, device=DEV)
+    flat = logits.permute(1, 0, 2).reshape(B, S * Vs).contiguous()
+    t = torch.full((B,), 0.7, device=DEV)
+    p = torch.tensor([1.0, 0.9], device=DEV)
+    seeds = torch.tensor([11, 12], device=DEV, dtype=torch.int32)
+    ctr = torch.tensor([3, 4], device=DEV, dtype=torch.int32)
+    a = ops.sample(logits, t, p, seeds, ctr, shards=S)
+    b = ops.sample(flat, t, p, seeds, ctr)
+    assert a.tolist() == b.tolist()
+
+
+def test_sampler_matches_reference_and_distribution():
+    V = 64
+    logits = torch.randn(1, V, device=DEV, generator=torch.Generator(DEV).manual_seed(0)) * 2
+    t = torch.tensor([0.8], device=DEV)
+    for top_p in (1.0, 0.5):
+        p = torch.tensor([top_p], device=DEV)
+        agree = 0
+        counts = torch.zeros(V)
+        N = 4000
+        for c in range(N):
+            ctr = torch.tensor([c], device=DEV, dtype=torch.int32)
+            seeds = torch.tensor([1234], device=DEV, dtype=torch.int32)
+            tok = int(ops.sample(logits, t, p, seeds, ctr)[0])
+            if c < 200:
+                agree += tok == int(ref.sample(logits.cpu(), t.cpu(), p.cpu(), seeds.cpu(), ctr.cpu())[0])
+            counts[tok] += 1
+        assert agree >= 195
+        probs = torch.softmax(logits[0].cpu() / 0.8, -1)
+        if top_p < 1:
+            order = torch.argsort(probs, descending=True)
+            keep = order[: int((probs[order].cumsum(0) < top_p).sum()) + 1]
+            assert counts[keep].sum() == N            # never samples outside the nucleus
+            probs = torch.zeros_like(probs).index_put_((keep,), probs[keep])
+            probs /= probs.sum()
+        emp = counts / N
+        assert (emp - probs).abs().sum() < 0.12       # L1 distance (expected ~0.05 at N=4000)
+
+
+def test_hash_init_matches_reference():
+    out = torch.empty(300, 257, dtype=torch.bfloat16, device=DEV)
+    ops.hash_init_(out, gcols=1000, row0=7, col0=11, seed=3, tensor_id=9, scale=0.02)
+    want = ref.hash_init(300, 257, 1000, 7, 11, 3, 9, 0.02, 0.0)
+    close(out, want, 0, 0)
