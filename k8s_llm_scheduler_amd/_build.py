@@ -88,7 +88,7 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> Path:
     if todo or force or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
         tmp = out.with_suffix(".tmp.so")
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs),
-              f"-L{tlib}", "-lc10_hip", "-lc10", f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed"], verbose)
+              f"-L{tlib}", "-lc10_hip", "-lc10", "-lrccl", f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed"], verbose)
         os.replace(tmp, out)
     return out
 

@@ -12,6 +12,7 @@
 #include <string>
 
 #include "runtime/block_allocator.h"
+#include "runtime/rccl_comm.h"
 
 namespace py = pybind11;
 
@@ -110,6 +111,27 @@ PYBIND11_MODULE(_C, m) {
                         uint32_t seed, uint32_t tid, float scale, float shift, int64_t s) {
     check(k8s_hash_init(P(out), rows, cols, gcols, row0, col0, seed, tid, scale, shift, S(s)), "hash_init");
   });
+
+  using k8sllm::RcclComm;
+  py::class_<RcclComm>(m, "RcclComm")
+      .def_static("unique_id", []() {
+        auto v = RcclComm::unique_id();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def(py::init([](int world, int rank, py::bytes id) {
+             std::string s = id;
+             return new RcclComm(world, rank, std::vector<uint8_t>(s.begin(), s.end()));
+           }))
+      .def("all_reduce", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int red,
+                            int64_t s) { c.all_reduce(P(send), P(recv), count, dtype, red, S(s)); })
+      .def("all_gather", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int64_t s) {
+        c.all_gather(P(send), P(recv), count, dtype, S(s));
+      })
+      .def("broadcast", [](RcclComm& c, uintptr_t buf, size_t count, int dtype, int root, int64_t s) {
+        c.broadcast(P(buf), count, dtype, root, S(s));
+      })
+      .def_property_readonly("world", &RcclComm::world)
+      .def_property_readonly("rank", &RcclComm::rank);
 
   using k8sllm::BlockAllocator;
   py::class_<BlockAllocator::Allocation>(m, "Allocation")

@@ -46,20 +46,28 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   __syncthreads();
 
   const int* bt = block_tables + (size_t)b * max_blocks;
-  // ---- scores = q . k (log2 domain)
+  // ---- scores = q . k (log2 domain).  Wave w owns tokens [w*PART/NW, (w+1)*PART/NW); every
+  // K row load of the wave is issued before the first one is consumed (memory-level parallelism
+  // instead of a latency chain).
+  constexpr int TOK_W = PART / NW;          // tokens per wave
+  constexpr int QSTEPS = TOK_W / TPW;       // 16-lane groups per wave, TPW tokens per step
   const int sub = lane % LPT, tok_in_wave = lane / LPT;
-  for (int base = wid * TPW; base < n; base += NW * TPW) {
-    const int i = base + tok_in_wave;
-    float part[G];
+  {
+    u32x4 kreg[QSTEPS];
 #pragma unroll
-    for (int g = 0; g < G; ++g) part[g] = 0.f;
-    if (i < n) {
-      const int tt = start + i;
+    for (int st = 0; st < QSTEPS; ++st) {
+      const int i = wid * TOK_W + st * TPW + tok_in_wave;
+      const int tt = start + min(i, n - 1);
       const int slot = bt[tt / block_size] * block_size + tt % block_size;
-      const u32x4 kv = *reinterpret_cast<const u32x4*>(k_cache + ((size_t)slot * nkv + kvh) * D + sub * 8);
+      kreg[st] = *reinterpret_cast<const u32x4*>(k_cache + ((size_t)slot * nkv + kvh) * D + sub * 8);
+    }
+#pragma unroll
+    for (int st = 0; st < QSTEPS; ++st) {
+      const int i = wid * TOK_W + st * TPW + tok_in_wave;
       float kf[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { kf[2 * j] = lo_bf(kv[j]); kf[2 * j + 1] = hi_bf(kv[j]); }
+      for (int j = 0; j < 4; ++j) { kf[2 * j] = lo_bf(kreg[st][j]); kf[2 * j + 1] = hi_bf(kreg[st][j]); }
+      float part[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float acc = 0.f;
@@ -67,15 +75,15 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
         for (int j = 0; j < 8; ++j) acc += qs[g][sub * 8 + j] * kf[j];
         part[g] = acc;
       }
-    }
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
+      for (int g = 0; g < G; ++g) {
 #pragma unroll
-      for (int o = LPT / 2; o > 0; o >>= 1) part[g] += __shfl_xor(part[g], o, WAVE);
-    }
-    if (sub == 0 && i < n) {
+        for (int o = LPT / 2; o > 0; o >>= 1) part[g] += __shfl_xor(part[g], o, WAVE);
+      }
+      if (sub == 0 && i < n) {
 #pragma unroll
-      for (int g = 0; g < G; ++g) sc[g][i] = part[g];
+        for (int g = 0; g < G; ++g) sc[g][i] = part[g];
+      }
     }
   }
   __syncthreads();
@@ -113,22 +121,32 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   }
   __syncthreads();
 
-  // ---- acc = p . v : wave w takes tokens w, w+NW, ...; lane owns dims (2*lane, 2*lane+1)
+  // ---- acc = p . v : wave w takes its TOK_W tokens, all V row loads issued up front;
+  // lane owns dims (2*lane, 2*lane+1)
   float acc[G][2];
 #pragma unroll
   for (int g = 0; g < G; ++g) acc[g][0] = acc[g][1] = 0.f;
   const int d0 = lane * 2;
   if (d0 < D) {
-    for (int i = wid; i < n; i += NW) {
-      const int tt = start + i;
-      const int slot = bt[tt / block_size] * block_size + tt % block_size;
-      const uint32_t vv = *reinterpret_cast<const uint32_t*>(v_cache + ((size_t)slot * nkv + kvh) * D + d0);
-      const float v0 = lo_bf(vv), v1 = hi_bf(vv);
+    uint32_t vreg[TOK_W];
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float pg = sc[g][i];
-        acc[g][0] += pg * v0;
-        acc[g][1] += pg * v1;
+    for (int k = 0; k < TOK_W; ++k) {
+      const int i = wid * TOK_W + k;
+      const int tt = start + min(i, n - 1);
+      const int slot = bt[tt / block_size] * block_size + tt % block_size;
+      vreg[k] = *reinterpret_cast<const uint32_t*>(v_cache + ((size_t)slot * nkv + kvh) * D + d0);
+    }
+#pragma unroll
+    for (int k = 0; k < TOK_W; ++k) {
+      const int i = wid * TOK_W + k;
+      if (i < n) {
+        const float v0 = lo_bf(vreg[k]), v1 = hi_bf(vreg[k]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const float pg = sc[g][i];
+          acc[g][0] += pg * v0;
+          acc[g][1] += pg * v1;
+        }
       }
     }
 #pragma unroll
@@ -184,11 +202,11 @@ extern "C" int k8s_paged_decode_attention(void* out, void* part_acc, void* part_
                                           float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks,
                                           int part, int pmax, hipStream_t stream) {
   if (B <= 0) return 0;
-  if (D != 128 || nq % nkv != 0 || part != 256) return -1;
+  if (D != 128 || nq % nkv != 0 || part != 64) return -1;
   const int G = nq / nkv;
   dim3 grid(pmax, nkv, B);
 #define L(GG)                                                                                             \
-  paged_decode_kernel<128, GG, 256><<<grid, 256, 0, stream>>>(                                            \
+  paged_decode_kernel<128, GG, 64><<<grid, 256, 0, stream>>>(                                            \
       (bf16_t*)out, (float*)part_acc, (float*)part_ml, (const bf16_t*)q, (const bf16_t*)k_cache,           \
       (const bf16_t*)v_cache, block_tables, context_lens, scale, block_size, max_blocks, nkv, pmax)
   switch (G) {

@@ -153,7 +153,7 @@ extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int
   const int rpw = (M >= 4) ? 2 : 1;
   const int rows_per_wg = 4 * rpw;
   const int n_wg = (N_out + rows_per_wg - 1) / rows_per_wg;
-  const int lds_cap_elems = 32768 / (2 * M);  // <= 32 KiB of x per workgroup
+  const int lds_cap_elems = 65536 / (2 * M);  // <= 64 KiB of x per workgroup (M=1: K up to 32768 unsplit)
   int splits = 1;
   const int target = 256;  // split K only when N alone cannot give every CU a workgroup
   if (n_wg < target) splits = (target + n_wg - 1) / n_wg;

@@ -24,7 +24,7 @@ except Exception as e:  # pragma: no cover - reported loudly on first GPU use
     _C_ERR = e
 
 EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
-DECODE_PARTITION = 256
+DECODE_PARTITION = 64
 
 
 def native():

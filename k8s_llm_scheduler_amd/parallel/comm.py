@@ -22,12 +22,16 @@ import torch
 import torch.distributed as dist
 
 
+_DT = {torch.bfloat16: 0, torch.float32: 1, torch.float16: 2, torch.int32: 3}
+
+
 @dataclass
 class TPGroup:
     rank: int = 0
     world: int = 1
     group: Optional[object] = None
     backend: str = "none"
+    rccl: Optional[object] = None   # native RcclComm (GPU): graph-capturable collectives
 
     @property
     def enabled(self) -> bool:
@@ -35,7 +39,9 @@ class TPGroup:
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
-            if self.backend == "gloo" and t.dtype == torch.bfloat16:
+            if self.rccl is not None and t.is_cuda:
+                self.rccl.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], 0, -1)
+            elif self.backend == "gloo" and t.dtype == torch.bfloat16:
                 f = t.float()
                 dist.all_reduce(f, group=self.group)
                 t.copy_(f)
@@ -48,7 +54,13 @@ class TPGroup:
         if self.world == 1:
             return t.unsqueeze(0)
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        t = t.contiguous()
+        if self.rccl is not None and t.is_cuda:
+            self.rccl.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], -1)
+        elif self.backend == "gloo":
+            dist.all_gather(list(out.unbind(0)), t.contiguous(), group=self.group)
+        else:
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         return out
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
@@ -80,4 +92,27 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600) -> TP
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    return TPGroup(rank, world, dist.group.WORLD, backend)
+    tp = TPGroup(rank, world, dist.group.WORLD, backend)
+    if backend == "nccl" and os.environ.get("K8S_TP_COMM", "rccl") == "rccl":
+        tp.rccl = make_rccl_comm(tp)
+    return tp
+
+
+def make_rccl_comm(tp: TPGroup):
+    """Create the engine's own RCCL communicator (unique id broadcast over torch.distributed)."""
+    from .. import ops
+
+    _C = ops.native()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    uid = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if tp.rank == 0:
+        uid.copy_(torch.frombuffer(bytearray(_C.RcclComm.unique_id()), dtype=torch.uint8))
+    dist.broadcast(uid, src=0, group=tp.group)
+    comm = _C.RcclComm(tp.world, tp.rank, bytes(uid.cpu().tolist()))
+    # one eager collective so lazy RCCL setup happens outside any graph capture
+    probe = torch.ones(16, dtype=torch.float32, device=dev)
+    comm.all_reduce(probe.data_ptr(), probe.data_ptr(), probe.numel(), 1, 0, -1)
+    torch.cuda.synchronize(dev)
+    if float(probe[0]) != float(tp.world):
+        raise RuntimeError(f"RCCL communicator self-test failed: {float(probe[0])} != {tp.world}")
+    return comm

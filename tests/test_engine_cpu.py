@@ -1,0 +1,183 @@
+"""T5 engine tests on CPU (reference ops): model correctness vs a dense un-paged Llama forward,
+prefill/decode consistency, prefix caching, stops, aborts, deadlines, checkpoint round trip,
+tokenizer and the native block allocator."""
+
+import math
+import time
+
+import pytest
+import torch
+
+from k8s_llm_scheduler_amd import ops
+from k8s_llm_scheduler_amd.engine import SamplingParams, build_engine
+from k8s_llm_scheduler_amd.engine.tokenizer import Tokenizer
+from k8s_llm_scheduler_amd.models.config import PRESETS
+from k8s_llm_scheduler_amd.models.llama import LlamaModel, save_hf_checkpoint
+from k8s_llm_scheduler_amd.ops import reference as ref
+
+
+def dense_llama_logits(m: LlamaModel, ids):
+    """Independent textbook forward (no paging, no fused ops) for the LAST position."""
+    c = m.cfg
+    x = m.embed[torch.tensor(ids)].float()
+    T = len(ids)
+    cs = ref.rope_table(c.head_dim, T, c.rope_theta, c.rope_scaling)
+    mask = torch.full((T, T), float("-inf")).triu(1)
+
+    def norm(v, w):
+        v = v.to(torch.bfloat16).float()
+        return (v * torch.rsqrt(v.pow(2).mean(-1, keepdim=True) + c.rms_eps) * w.float()).to(torch.bfloat16).float()
+
+    def rot(v):
+        h = v.shape[-1] // 2
+        cc, ss = cs[:, None, :h], cs[:, None, h:]
+        return torch.cat([v[..., :h] * cc - v[..., h:] * ss, v[..., h:] * cc + v[..., :h] * ss], -1)
+
+    D, nq, nkv = c.head_dim, c.num_heads, c.num_kv_heads
+    for w in m.layers:
+        h = norm(x, w.ln1)
+        qkv = (h @ w.wqkv.float().T).to(torch.bfloat16).float()
+        q = rot(qkv[:, :nq * D].view(T, nq, D)).to(torch.bfloat16).float()
+        k = rot(qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D)).to(torch.bfloat16).float()
+        v = qkv[:, (nq + nkv) * D:].view(T, nkv, D)
+        k = k.repeat_interleave(nq // nkv, 1)
+        v = v.repeat_interleave(nq // nkv, 1)
+        att = torch.softmax(torch.einsum("qhd,khd->hqk", q, k) / math.sqrt(D) + mask, -1)
+        a = torch.einsum("hqk,khd->qhd", att, v).reshape(T, nq * D).to(torch.bfloat16).float()
+        x = (x + (a @ w.wo.float().T).to(torch.bfloat16).float()).to(torch.bfloat16).float()
+        h = norm(x, w.ln2)
+        gu = h @ w.wgu.float().T
+        g = (torch.nn.functional.silu(gu[:, :m.I]) * gu[:, m.I:]).to(torch.bfloat16).float()
+        x = (x + (g @ w.wdown.float().T).to(torch.bfloat16).float()).to(torch.bfloat16).float()
+    h = norm(x[-1:], m.norm)
+    return (h @ m.lm_head.float().T)[0]
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    return LlamaModel(PRESETS["tiny"], device="cpu", seed=3, max_model_len=512)
+
+
+def _prefill(m, ids, bs=16, nblocks=64):
+    m.allocate_kv(nblocks, bs)
+    T = len(ids)
+    blocks = list(range(math.ceil((T + 4) / bs)))
+    bt = torch.zeros(1, 32, dtype=torch.int32)
+    bt[0, :len(blocks)] = torch.tensor(blocks)
+    i32 = lambda x: torch.tensor(x, dtype=torch.int32)
+    slots = [blocks[p // bs] * bs + p % bs for p in range(T)]
+    lg = m.forward_prefill(i32(ids), i32(list(range(T))), i32(slots), i32([0, T]), i32([T]), bt, T, i32([T - 1]))
+    return lg, bt
+
+
+def test_prefill_matches_dense_reference(tiny):
+    ids = [5, 17, 200, 3, 3000, 42, 7, 9, 11, 1000, 15, 16, 300, 301, 302, 303, 12, 13]
+    lg, _ = _prefill(tiny, ids)
+    want = dense_llama_logits(tiny, ids)
+    assert lg.shape == (1, 1, tiny.cfg.vocab)
+    torch.testing.assert_close(lg[0, 0], want, atol=5e-2, rtol=5e-2)
+    assert int(lg[0, 0].argmax()) == int(want.argmax())
+
+
+def test_decode_step_matches_prefill(tiny):
+    ids = list(range(100, 140))
+    lg_full, _ = _prefill(tiny, ids + [777])
+    _, bt = _prefill(tiny, ids)
+    ctx = torch.tensor([len(ids) + 1], dtype=torch.int32)
+    lg_dec = tiny.forward_decode(torch.tensor([777], dtype=torch.int32), ctx, bt, 512)
+    torch.testing.assert_close(lg_dec, lg_full, atol=5e-2, rtol=5e-2)
+
+
+def test_random_init_is_device_and_tp_independent():
+    c = PRESETS["tiny"]
+    a = ref.hash_init(64, 32, 256, 64, 0, 1, 2, 0.1, 0.0)
+    b = ref.hash_init(128, 32, 256, 0, 0, 1, 2, 0.1, 0.0)[64:]
+    assert torch.equal(a, b)
+    assert c.params > 0
+
+
+def test_checkpoint_roundtrip(tmp_path, tiny):
+    save_hf_checkpoint(tiny, tmp_path / "ckpt")
+    m2 = LlamaModel(tiny.cfg, device="cpu", weights=str(tmp_path / "ckpt"), max_model_len=512)
+    for a, b in zip(tiny.layers, m2.layers):
+        assert torch.equal(a.wqkv, b.wqkv) and torch.equal(a.wgu, b.wgu) and torch.equal(a.wdown, b.wdown)
+    assert torch.equal(tiny.lm_head, m2.lm_head)
+
+
+@pytest.fixture(scope="module")
+def engine():
+    return build_engine("tiny", device="cpu", max_batch=4, max_model_len=512, num_blocks=200, seed=1)
+
+
+def test_generate_deterministic_with_seed(engine):
+    p = SamplingParams(max_tokens=6, temperature=0.7, seed=5, ignore_eos=True)
+    a = engine.generate(["hello kubernetes"], p)[0]
+    b = engine.generate(["hello kubernetes"], p)[0]
+    assert a.token_ids == b.token_ids and len(a.token_ids) == 6 and a.finish_reason == "length"
+
+
+def test_batched_equals_single(engine):
+    p = SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True)
+    prompts = ["pod one needs cpu", "a much longer prompt about node kind-worker2 and memory", "x"]
+    singles = [engine.generate([q], p)[0].token_ids for q in prompts]
+    batched = [o.token_ids for o in engine.generate(prompts, p)]
+    assert singles == batched
+
+
+def test_prefix_cache_hit(engine):
+    sys_msg = "You are an intelligent Kubernetes scheduler. " * 8
+    p = SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True)
+    a = engine.generate([engine.render_chat(sys_msg, "pod A")], p)[0]
+    b = engine.generate([engine.render_chat(sys_msg, "pod B")], p)[0]
+    assert a.cached_tokens == 0 and b.cached_tokens >= 48
+    # cached result equals an uncached computation of the same prompt
+    engine.allocator.reset_prefix_cache()
+    c = engine.generate([engine.render_chat(sys_msg, "pod B")], p)[0]
+    assert c.cached_tokens == 0 and c.token_ids == b.token_ids
+
+
+def test_eos_stop(engine):
+    eos = engine.tok.eot_id
+    saved = engine.model.lm_head[eos].clone()
+    engine.model.lm_head[eos] = 1.0  # make EOS win the greedy choice
+    try:
+        o = engine.generate(["anything"], SamplingParams(max_tokens=10, temperature=0.0))[0]
+    finally:
+        engine.model.lm_head[eos] = saved
+    assert o.finish_reason == "stop" and o.token_ids == []
+
+
+def test_deadline_and_abort(engine):
+    with pytest.raises(TimeoutError):
+        engine.generate(["slow"], SamplingParams(max_tokens=50, ignore_eos=True), deadline=time.monotonic() - 1)
+    assert not engine.has_work() and engine.allocator.num_free == engine.allocator.num_blocks - engine.allocator.num_cached \
+        or engine.allocator.num_free > 0
+
+
+def test_tokenizer_roundtrip_and_template():
+    tok = Tokenizer(model_vocab=128256)
+    text = 'Select the best node from [kind-worker, kind-worker2] and respond with JSON only: {"a": 1}'
+    assert tok.decode(tok.encode(text)) == text
+    ids = tok.chat_ids("sys", "user msg")
+    assert ids[0] == 128000 and ids.count(128009) == 2 and ids[-1] != 128009
+    assert tok.decode([128000, *tok.encode("hi"), 128009]) == "hi"
+
+
+def test_block_allocator_prefix_and_eviction():
+    A = ops.native().BlockAllocator(6, 4, True)
+    t = list(range(13))
+    a = A.allocate(t, 14)                         # 4 blocks
+    assert a.cached_tokens == 0 and A.num_free == 2
+    A.commit_prefix(a.blocks, t, 13)              # 3 full blocks published
+    b = A.allocate(t, 14)                         # shares 3 blocks (last token recomputed)
+    assert b.cached_tokens == 12 and b.blocks[:3] == a.blocks[:3] and A.num_free == 1
+    assert A.refcount(a.blocks[0]) == 2
+    A.release(a.blocks)
+    A.release(b.blocks)
+    assert A.num_free == 6 and A.num_cached == 3  # cached blocks stay (evictable)
+    c = A.allocate(list(range(100, 124)), 24)     # needs all 6 -> evicts the cached ones
+    assert len(c.blocks) == 6 and A.num_cached == 0
+    with pytest.raises(RuntimeError):
+        A.allocate([1], 4)
+    with pytest.raises(Exception):
+        A.release([c.blocks[0], c.blocks[0]])

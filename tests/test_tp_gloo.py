@@ -1,0 +1,80 @@
+"""T4 on CPU: tensor parallelism (world_size 2 and 4, gloo) must reproduce TP=1 -- sharded
+QKV/O/gate-up/down/LM-head, all-reduce, vocab-parallel all-gather, deterministic sampling."""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from k8s_llm_scheduler_amd.engine import SamplingParams, build_engine
+from k8s_llm_scheduler_amd.models.config import PRESETS
+from k8s_llm_scheduler_amd.parallel import TPGroup
+
+from test_engine_cpu import _prefill  # noqa: E402
+
+IDS = [7, 100, 2000, 31, 32, 33, 900, 12, 5, 5, 5, 6000, 42, 43]
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tp = TPGroup(rank, world, dist.group.WORLD, "gloo")
+        from k8s_llm_scheduler_amd.models.llama import LlamaModel
+
+        m = LlamaModel(PRESETS["tiny"], tp, device="cpu", seed=3, max_model_len=512)
+        lg, bt = _prefill(m, IDS)
+        ctx = torch.tensor([len(IDS) + 1], dtype=torch.int32)
+        m2_lg = m.forward_decode(torch.tensor([77], dtype=torch.int32), ctx, bt, 512)
+        eng = build_engine("tiny", tp=tp, device="cpu", max_batch=2, max_model_len=512, num_blocks=64, seed=1)
+        toks = eng.generate(["tensor parallel"], SamplingParams(max_tokens=5, temperature=0.8, seed=9,
+                                                                ignore_eos=True))[0].token_ids
+        if rank == 0:
+            q.put((lg.flatten(0, 1)[0] if lg.shape[0] == 1 else lg.permute(1, 0, 2).reshape(1, -1)[0],
+                   m2_lg.permute(1, 0, 2).reshape(1, -1)[0], toks))
+        else:
+            q.put(("toks", toks))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_matches_tp1(world):
+    from k8s_llm_scheduler_amd.models.llama import LlamaModel
+
+    m = LlamaModel(PRESETS["tiny"], device="cpu", seed=3, max_model_len=512)
+    lg1, bt = _prefill(m, IDS)
+    ctx = torch.tensor([len(IDS) + 1], dtype=torch.int32)
+    dec1 = m.forward_decode(torch.tensor([77], dtype=torch.int32), ctx, bt, 512)[0, 0]
+    eng = build_engine("tiny", device="cpu", max_batch=2, max_model_len=512, num_blocks=64, seed=1)
+    toks1 = eng.generate(["tensor parallel"], SamplingParams(max_tokens=5, temperature=0.8, seed=9,
+                                                             ignore_eos=True))[0].token_ids
+
+    ctxmp = mp.get_context("spawn")
+    q = ctxmp.Queue()
+    port = _free_port()
+    procs = [ctxmp.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    main = next(g for g in got if g[0] != "toks")
+    lg_tp, dec_tp, toks_tp = main
+    torch.testing.assert_close(lg_tp, lg1[0, 0], atol=5e-2, rtol=5e-2)
+    torch.testing.assert_close(dec_tp, dec1, atol=5e-2, rtol=5e-2)
+    assert toks_tp == toks1
+    assert all(g[1] == toks1 for g in got if g[0] == "toks")   # every rank drew the same tokens
