@@ -47,6 +47,8 @@ def main() -> int:
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--simulate-tp", type=int, default=0,
+                    help="PROFILING ONLY: run one TP rank's shapes on one GPU with collectives skipped")
     args = ap.parse_args()
 
     import torch
@@ -66,6 +68,9 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     tp = init_from_env("cuda")
+    if args.simulate_tp > 1:
+        from k8s_llm_scheduler_amd.parallel import TPGroup
+        tp = TPGroup(0, args.simulate_tp, None, "none", simulate=True)
     rank = tp.rank
 
     t_init = time.perf_counter()
@@ -102,7 +107,7 @@ def main() -> int:
     prompt_tokens = len(eng.render_chat(svc.system_message, make_items()[0][0]))
 
     def barrier():
-        if tp.world > 1:
+        if tp.world > 1 and not tp.simulate:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -120,7 +125,7 @@ def main() -> int:
         fallbacks += sum(d.fallback_needed for d in ds)
     barrier()
     elapsed = time.perf_counter() - t0
-    if tp.world > 1:
+    if tp.world > 1 and not tp.simulate:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -149,7 +154,7 @@ def main() -> int:
             "prompt_tokens": prompt_tokens,
             "gen_tokens": args.gen_tokens,
             "cluster_nodes": args.nodes,
-            "parallelism": f"tp{tp.world}",
+            "parallelism": f"tp{tp.world}" + ("-SIMULATED-no-comm" if tp.simulate else ""),
             "cuda_graphs": eng.use_graphs,
             "prefix_cache": not args.no_prefix_cache,
         },
@@ -168,7 +173,7 @@ def main() -> int:
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    if tp.world > 1:
+    if tp.world > 1 and not tp.simulate:
         dist.barrier()
         dist.destroy_process_group()
     return 0

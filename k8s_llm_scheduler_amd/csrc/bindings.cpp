@@ -31,6 +31,12 @@ int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, c
                                 int max_qlen, int nq, int nkv, int D, int block_size, int max_blocks, hipStream_t s);
 void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int* splits_out);
 int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi, hipStream_t s);
+int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi,
+                  const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
+int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const void* qkv, const float* cos_sin,
+                               void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
+                               float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax,
+                               hipStream_t s);
 int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
                const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist,
                int hist_stride, int* steps, hipStream_t s);
@@ -93,6 +99,18 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemv", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, int M, int N, int K, int epi,
                    int64_t s) { check(k8s_gemv(P(out), P(partial), P(x), P(W), M, N, K, epi, S(s)), "gemv"); });
+  m.def("gemv_norm", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, int M, int N, int K, int epi,
+                        uintptr_t res_in, uintptr_t res_out, uintptr_t nw, float eps, int64_t s) {
+    check(k8s_gemv_norm(P(out), P(partial), P(x), P(W), M, N, K, epi, P(res_in), P(res_out), P(nw), eps, S(s)),
+          "gemv_norm");
+  });
+  m.def("decode_attention_fused", [](uintptr_t out, uintptr_t pacc, uintptr_t pml, uintptr_t qkv, uintptr_t cos_sin,
+                                     uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx, float scale, int B, int nq,
+                                     int nkv, int D, int bs, int max_blocks, int pmax, int64_t s) {
+    check(k8s_decode_attention_fused(P(out), P(pacc), P(pml), P(qkv), P<float>(cos_sin), P(kc), P(vc), P<int>(bt),
+                                     P<int>(ctx), scale, B, nq, nkv, D, bs, max_blocks, pmax, S(s)),
+          "decode_attention_fused");
+  });
   m.def("sample", [](uintptr_t tokens, uintptr_t logits, int B, int Vs, int shards, uintptr_t temp, uintptr_t top_p,
                      uintptr_t seeds, uintptr_t counter, uintptr_t ctx_inc, uintptr_t hist, int hist_stride,
                      uintptr_t steps, int64_t s) {

@@ -34,21 +34,74 @@ __device__ __forceinline__ float dot8(u32x4 w, u32x4 x, float acc) {
 
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
-template <int M, int RPW, int EPI>
+// Fused pre-norm prologue (NORM): the GEMV input is rmsnorm(x + res_in) * nw, computed by every
+// workgroup from the full rows (L2-resident, M x K x 4 bytes), and workgroup (0, 0) writes the
+// updated residual r = x + res_in to res_out.  res_in and res_out must be different buffers
+// (the model ping-pongs two residual buffers) because other workgroups are still reading res_in.
+template <int M>
+__device__ __forceinline__ void norm_row_chunk(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res_in,
+                                               int m, int K, int c, u32x4& r) {
+  const u32x4 a = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + c * 8);
+  if (res_in == nullptr) { r = a; return; }
+  const u32x4 b = *reinterpret_cast<const u32x4*>(res_in + (size_t)m * K + c * 8);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = pack_bf2(lo_bf(a[j]) + lo_bf(b[j]), hi_bf(a[j]) + hi_bf(b[j]));
+}
+
+template <int M, int RPW, int EPI, bool NORM>
 __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float* __restrict__ partial,
                                                    const bf16_t* __restrict__ x, const bf16_t* __restrict__ W,
-                                                   int N_out, int K, int KS, int half_rows) {
+                                                   int N_out, int K, int KS, int half_rows,
+                                                   const bf16_t* __restrict__ res_in, bf16_t* __restrict__ res_out,
+                                                   const bf16_t* __restrict__ nw, float eps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u32x4* xs = reinterpret_cast<u32x4*>(smem);  // [M][KS/8]
+  __shared__ float nred[4][M];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int kb = blockIdx.y * KS;
   const int klen = min(KS, K - kb);
   const int nch = klen >> 3;  // 16-byte chunks in this slice
 
-  // stage x[:, kb:kb+klen] into LDS
-  for (int i = threadIdx.x; i < M * nch; i += blockDim.x) {
-    const int m = i / nch, c = i - m * nch;
-    xs[m * (KS >> 3) + c] = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + kb + c * 8);
+  if (NORM) {
+    const bool writer = blockIdx.x == 0 && blockIdx.y == 0 && res_out != nullptr;
+    float inv[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float ss = 0.f;
+      for (int c = threadIdx.x; c < (K >> 3); c += blockDim.x) {
+        u32x4 r;
+        norm_row_chunk<M>(x, res_in, m, K, c, r);
+        if (writer) reinterpret_cast<u32x4*>(res_out + (size_t)m * K)[c] = r;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float l = lo_bf(r[j]), h = hi_bf(r[j]);
+          ss += l * l + h * h;
+        }
+      }
+      ss = wave_sum(ss);
+      if (lane == 0) nred[wid][m] = ss;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < M; ++m) inv[m] = rsqrtf((nred[0][m] + nred[1][m] + nred[2][m] + nred[3][m]) / (float)K + eps);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+        u32x4 r, o;
+        norm_row_chunk<M>(x, res_in, m, K, (kb >> 3) + c, r);
+        const u32x4 g = reinterpret_cast<const u32x4*>(nw + kb)[c];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = pack_bf2(lo_bf(r[j]) * inv[m] * lo_bf(g[j]), hi_bf(r[j]) * inv[m] * hi_bf(g[j]));
+        xs[m * (KS >> 3) + c] = o;
+      }
+    }
+  } else {
+    // stage x[:, kb:kb+klen] into LDS
+    for (int i = threadIdx.x; i < M * nch; i += blockDim.x) {
+      const int m = i / nch, c = i - m * nch;
+      xs[m * (KS >> 3) + c] = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + kb + c * 8);
+    }
   }
   __syncthreads();
 
@@ -170,8 +223,9 @@ extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int
 
 // partial: fp32 workspace of splits * M * wrows floats (wrows = N_out, or 2*N_out for SWIGLU);
 // may be null when the plan has a single split.
-extern "C" int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi,
-                        hipStream_t stream) {
+extern "C" int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K,
+                             int epi, const void* res_in, void* res_out, const void* nw, float eps,
+                             hipStream_t stream) {
   if (M < 1 || M > 8 || K % 8 != 0 || N_out <= 0) return -1;
   int ks, splits;
   k8s_gemv_plan(M, N_out, K, epi, &ks, &splits);
@@ -183,7 +237,14 @@ extern "C" int k8s_gemv(void* out, void* partial, const void* x, const void* W, 
   const int half_rows = (epi == EPI_SWIGLU) ? N_out : 0;
   const bf16_t* xx = (const bf16_t*)x;
   const bf16_t* ww = (const bf16_t*)W;
-#define G(MM, RR, EE) gemv_kernel<MM, RR, EE><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks, half_rows)
+  const bf16_t* ri = (const bf16_t*)res_in;
+  bf16_t* ro = (bf16_t*)res_out;
+  const bf16_t* gw = (const bf16_t*)nw;
+#define G(MM, RR, EE)                                                                                     \
+  if (gw) gemv_kernel<MM, RR, EE, true><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,      \
+                                                                    half_rows, ri, ro, gw, eps);         \
+  else gemv_kernel<MM, RR, EE, false><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,        \
+                                                                  half_rows, ri, ro, gw, eps)
 #define BY_EPI(MM, RR)                  \
   switch (epi) {                        \
     case EPI_BF16: G(MM, RR, EPI_BF16); break;       \
@@ -213,4 +274,9 @@ extern "C" int k8s_gemv(void* out, void* partial, const void* x, const void* W, 
     }
   }
   return (int)hipGetLastError();
+}
+
+extern "C" int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi,
+                        hipStream_t stream) {
+  return k8s_gemv_norm(out, partial, x, W, M, N_out, K, epi, nullptr, nullptr, nullptr, 0.f, stream);
 }

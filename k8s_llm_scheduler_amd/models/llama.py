@@ -214,6 +214,8 @@ class LlamaModel:
                        max_context: int) -> torch.Tensor:
         """One decode step for B sequences (one token each, positions from context_lens)."""
         B = tokens.shape[0]
+        if self.device.type == "cuda" and B <= ops.GEMV_MAX_M and self.fused_decode:
+            return self._forward_decode_fused(tokens, context_lens, block_tables, max_context)
         kv = self.kv_cache
 
         def attn(l: int, qkv: torch.Tensor) -> torch.Tensor:
@@ -225,6 +227,32 @@ class LlamaModel:
 
         h, res = self._layers(ops.embedding(tokens, self.embed), attn)
         return self._logits(h, res)
+
+
+    fused_decode = True
+
+    def _forward_decode_fused(self, tokens: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
+                              max_context: int) -> torch.Tensor:
+        """Decode step with 5 kernels per layer: [norm+QKV GEMV] -> [RoPE+KV write+attention] ->
+        [O GEMV] -> all-reduce -> [norm+gate/up GEMV+SwiGLU] -> [down GEMV] -> all-reduce.
+        The residual stream ping-pongs between two buffers (a norm-GEMV reads one, writes the other)."""
+        c, kv = self.cfg, self.kv_cache
+        h = ops.embedding(tokens, self.embed)
+        res_a = torch.empty_like(h)
+        res_b = torch.empty_like(h)
+        res_in = None
+        for w_l, w in enumerate(self.layers):
+            qkv = ops.linear_norm(h, w.wqkv, w.ln1, c.rms_eps, res_in, res_b)
+            a = ops.decode_attention_fused(qkv, self.cos_sin, kv[w_l, 0], kv[w_l, 1], block_tables, context_lens,
+                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
+            o = ops.linear(a, w.wo)
+            self.tp.all_reduce_(o)
+            g = ops.linear_norm(o, w.wgu, w.ln2, c.rms_eps, res_b, res_a, epi=ops.EPI_SWIGLU)
+            h = ops.linear(g, w.wdown)
+            self.tp.all_reduce_(h)
+            res_in = res_a
+        logits = ops.linear_norm(h, self.lm_head, self.norm, c.rms_eps, res_in, None, epi=ops.EPI_F32)
+        return self.tp.all_gather_shards(logits)
 
 
 def save_hf_checkpoint(model: LlamaModel, path: Path) -> None:

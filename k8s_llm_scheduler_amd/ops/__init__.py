@@ -25,6 +25,7 @@ except Exception as e:  # pragma: no cover - reported loudly on first GPU use
 
 EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
 DECODE_PARTITION = 64
+FUSED_PARTITION = 1024
 
 
 def native():
@@ -179,6 +180,61 @@ def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
         if out_dtype is not None and out_dtype != y.dtype:
             y = y.to(out_dtype)
     return y.view(*x.shape[:-1], y.shape[-1])
+
+
+def linear_norm(x: torch.Tensor, w: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                res_in: Optional[torch.Tensor], res_out: Optional[torch.Tensor], epi: int = EPI_BF16) -> torch.Tensor:
+    """Decode-path fused pre-norm projection (M <= 8 rows):
+    r = x + res_in (or x), res_out <- r, y = epi(rmsnorm(r) * norm_w @ w.T).
+    res_in and res_out must be distinct buffers (ping-pong)."""
+    if res_in is not None and res_out is not None and res_in.data_ptr() == res_out.data_ptr():
+        raise ValueError("res_in and res_out must be different buffers")
+    M, K = x.shape
+    if not _gpu(x, w):
+        r = x if res_in is None else (x.float() + res_in.float()).to(x.dtype)
+        if res_out is not None:
+            res_out.copy_(r)
+        h, _ = ref.rmsnorm(r, norm_w, eps)
+        if epi == EPI_SWIGLU:
+            return ref.linear_swiglu(h, w)
+        return ref.linear(h, w, F32 if epi == EPI_F32 else None)
+    if M > GEMV_MAX_M:
+        raise ValueError("linear_norm is the decode path (M <= 8)")
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
+    ks, splits = native().gemv_plan(M, N, K, epi)
+    part = torch.empty(splits * M * w.shape[0], dtype=F32, device=x.device) if splits > 1 else None
+    native().gemv_norm(out.data_ptr(), part.data_ptr() if part is not None else 0, _chk(x, BF16, "x"),
+                       _chk(w, BF16, "w"), M, N, K, epi,
+                       _chk(res_in, BF16, "res_in") if res_in is not None else 0,
+                       _chk(res_out, BF16, "res_out") if res_out is not None else 0,
+                       _chk(norm_w, BF16, "norm_w"), float(eps), -1)
+    return out
+
+
+def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                           block_tables: torch.Tensor, context_lens: torch.Tensor, scale: float, block_size: int,
+                           max_context: int, nq: int, nkv: int, D: int) -> torch.Tensor:
+    """RoPE + KV write of the new token + paged GQA attention, one kernel.  Returns [B, nq*D]."""
+    B = qkv.shape[0]
+    if not _gpu(qkv, k_cache):
+        q = rope_kv_write(qkv, cos_sin, k_cache, v_cache, nq, nkv, D, context_lens=context_lens,
+                          block_tables=block_tables, block_size=block_size)
+        return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, context_lens, scale,
+                                          block_size).view(B, nq * D)
+    pmax = max(1, math.ceil(max_context / FUSED_PARTITION))
+    out = torch.empty(B, nq * D, dtype=BF16, device=qkv.device)
+    if pmax > 1:
+        pacc = torch.empty(B * nq * pmax * D, dtype=F32, device=qkv.device)
+        pml = torch.empty(B * nq * pmax * 2, dtype=F32, device=qkv.device)
+        pa, pm = pacc.data_ptr(), pml.data_ptr()
+    else:
+        pa = pm = 0
+    native().decode_attention_fused(out.data_ptr(), pa, pm, _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"),
+                                    _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
+                                    _chk(block_tables, I32, "block_tables"), _chk(context_lens, I32, "context_lens"),
+                                    float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], pmax, -1)
+    return out
 
 
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:

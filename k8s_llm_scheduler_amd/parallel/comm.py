@@ -32,13 +32,14 @@ class TPGroup:
     group: Optional[object] = None
     backend: str = "none"
     rccl: Optional[object] = None   # native RcclComm (GPU): graph-capturable collectives
+    simulate: bool = False          # shapes of a TP rank, collectives skipped (profiling only)
 
     @property
     def enabled(self) -> bool:
         return self.world > 1
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.world > 1 and not self.simulate:
             if self.rccl is not None and t.is_cuda:
                 self.rccl.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], 0, -1)
             elif self.backend == "gloo" and t.dtype == torch.bfloat16:
@@ -53,6 +54,8 @@ class TPGroup:
         """[..] local -> [world, ..] (shard-major)."""
         if self.world == 1:
             return t.unsqueeze(0)
+        if self.simulate:
+            return t.unsqueeze(0).expand(self.world, *t.shape).contiguous()
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         t = t.contiguous()
         if self.rccl is not None and t.is_cuda:

@@ -225,3 +225,46 @@ def test_hash_init_matches_reference():
     ops.hash_init_(out, gcols=1000, row0=7, col0=11, seed=3, tensor_id=9, scale=0.02)
     want = ref.hash_init(300, 257, 1000, 7, 11, 3, 9, 0.02, 0.0)
     close(out, want, 0, 0)
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_linear_norm_fused(M, epi, with_res):
+    K, N = 8192, 1280
+    x = rnd(M, K)
+    res_in = rnd(M, K) if with_res else None
+    nw = rnd(K, scale=0.1) + 1
+    w = rnd(2 * N if epi == 2 else N, K, scale=0.05)
+    res_out = torch.zeros(M, K, dtype=torch.bfloat16, device=DEV)
+    got = ops.linear_norm(x, w, nw, 1e-5, res_in, res_out, epi=epi)
+    ro_cpu = torch.zeros(M, K, dtype=torch.bfloat16)
+    want = ops.linear_norm(x.cpu(), w.cpu(), nw.cpu(), 1e-5, res_in.cpu() if with_res else None, ro_cpu, epi=epi)
+    close(res_out, ro_cpu, 0, 0)
+    close(got, want, 3e-2 if epi != 1 else 2e-2)
+
+
+@pytest.mark.parametrize("nq,nkv", [(8, 1), (64, 8), (32, 8), (4, 2)])
+@pytest.mark.parametrize("ctxs", [[1, 37, 600], [1024, 1025], [3000]])
+def test_decode_attention_fused(nq, nkv, ctxs):
+    D, bs = 128, 16
+    B = len(ctxs)
+    maxb = (max(ctxs) + bs - 1) // bs
+    nblocks = B * maxb + 3
+    kc, vc = _paged_cache(nkv, D, bs, nblocks)
+    bt = torch.randperm(nblocks, device=DEV)[: B * maxb].view(B, maxb).int()
+    ctx = torch.tensor(ctxs, device=DEV, dtype=torch.int32)
+    qkv = rnd(B, (nq + 2 * nkv) * D)
+    scaling = dict(rope_type="llama3", factor=8.0, low_freq_factor=1.0, high_freq_factor=4.0,
+                   original_max_position_embeddings=8192)
+    cs = ref.rope_table(D, 4096, 500000.0, scaling).to(DEV)
+    kc_ref, vc_ref = kc.cpu().clone(), vc.cpu().clone()
+    for max_context in (max(ctxs), 4096):
+        kc2, vc2 = kc.clone(), vc.clone()
+        got = ops.decode_attention_fused(qkv, cs, kc2, vc2, bt, ctx, 1 / math.sqrt(D), bs, max_context, nq, nkv, D)
+        kr, vr = kc_ref.clone(), vc_ref.clone()
+        want = ops.decode_attention_fused(qkv.cpu(), cs.cpu(), kr, vr, bt.cpu(), ctx.cpu(), 1 / math.sqrt(D), bs,
+                                          max_context, nq, nkv, D)
+        close(got, want, 2e-2)
+        close(kc2, kr, 2e-2)
+        close(vc2, vr, 0, 0)
