@@ -1,16 +1,21 @@
 // K4 + K5 + K7 fused for decode: RoPE of the new token's q/k, its paged-KV write, and GQA
-// attention over the paged cache, in ONE kernel that reads the QKV projection output directly.
+// attention over the paged cache in ONE kernel that reads the QKV projection output directly.
 //
-// Why: at TP=8 a decode layer is ~70 us of which the small kernels (rope, attention merge) are
-// ~4.5 us each of mostly launch gap and dependent-load latency.  Here:
-//  * one workgroup (8 waves) covers PART = 1024 context tokens of one (sequence, kv head), so
-//    any context up to 1024 tokens (the reference's 3-node prompts are ~0.5k) is a single pass
-//    that writes the final output -- no merge kernel work;
-//  * longer contexts split into partitions and the merge kernel combines them (it exits at once
-//    when the context fits one partition, so a captured graph serves every length);
-//  * the workgroup owning the new token's position rotates k, writes k/v into the cache and uses
-//    the rotated values from LDS for its own scores (no cross-workgroup ordering needed);
-//  * every K row load of a wave is issued before the first is consumed, V loads likewise.
+// Structure (one workgroup = 16 waves x 64 tokens = PART = 1024 context tokens of one (sequence,
+// kv head); each wave issues all its K loads, then all its V loads, before consuming any):
+//  * MFMA v_mfma_f32_16x16x32_bf16 in the "swapped" orientation S^T = K . Q^T: the 16 rows are
+//    16 context tokens, the 16 columns the query heads of the GQA group (G <= 16, padded with
+//    zero heads), so each K row is read once for all heads, with 16 rows x 64 B per load
+//    instruction (coalesced), and every lane ends up holding 4 scores of ONE head;
+//  * softmax statistics: registers -> 2 cross-lane steps -> one LDS exchange between waves;
+//  * P.V: P feeds the MFMA A operand straight from registers (keys permuted inside each 32-key
+//    step exactly as on the V side); V is staged through LDS (XOR swizzle) and read with the
+//    gfx950 transposing read ds_read_b64_tr_b16;
+//  * contexts up to 1024 tokens (the reference's prompts are ~0.5k) are a single pass that
+//    writes the final output; longer ones split into partitions merged by a second kernel that
+//    exits immediately for single-partition rows (one captured graph serves every length);
+//  * the workgroup owning the new token's position rotates its k, writes k/v to the cache and
+//    substitutes the fresh values for its own use (no cross-workgroup ordering).
 //
 // Layouts: qkv [B, (nq + 2*nkv) * D] bf16 (pre-RoPE); cos_sin [max_pos, D] f32 (cos | sin);
 // caches [num_slots, nkv, D] bf16; context_lens[b] INCLUDES the new token (pos = ctx - 1).
@@ -19,210 +24,257 @@
 namespace k8sllm {
 
 constexpr float LOG2E_F = 1.4426950408889634f;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+
+__device__ __forceinline__ int vswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
 template <int D, int G, int PART>
-__global__ void __launch_bounds__(512) decode_fused_kernel(
+__global__ void __launch_bounds__(1024) decode_fused_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_acc, float* __restrict__ part_ml, const bf16_t* __restrict__ qkv,
     const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ context_lens, float scale, int block_size,
     int max_blocks, int nkv, int pmax) {
-  constexpr int NW = 8;
+  static_assert(D == 128 && G <= 16, "head_dim 128, group <= 16");
+  constexpr int NW = 16;
   constexpr int NT = NW * WAVE;
-  constexpr int LPT = D / 8;        // lanes per K row (16 B each)
-  constexpr int TPW = WAVE / LPT;   // K rows per wave per step
-  constexpr int TOK_W = PART / NW;  // tokens per wave
-  constexpr int KB = 8;             // K loads in flight per lane
-  constexpr int VB = 32;            // V loads in flight per lane
+  constexpr int TW = PART / NW;   // tokens per wave (64)
+  constexpr int NTILE = TW / 16;  // 16-token tiles per wave
   constexpr int HALF = D / 2;
-  __shared__ float qs[G][D];
-  __shared__ float sc[G][PART];
+  __shared__ __attribute__((aligned(16))) bf16_t qs[16][D];             // rotated q, zero heads >= G
+  __shared__ __attribute__((aligned(16))) char vbuf[NW][32 * D * 2];    // per-wave V stage (32 keys)
+  __shared__ __attribute__((aligned(16))) bf16_t kcur[D];
+  __shared__ __attribute__((aligned(16))) bf16_t vcur[D];
   __shared__ float red[G][D];
-  __shared__ float kcur[D], vcur[D];
-  __shared__ float wm[NW][G], wl[NW][G];
-  __shared__ float stat[G][2];
+  __shared__ float wm[NW][16], wl[NW][16];
 
   const int b = blockIdx.z, kvh = blockIdx.y, p = blockIdx.x;
-  const int ctx = context_lens[b];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 15, g4 = lane >> 4;
+  const int* bt = block_tables + (size_t)b * max_blocks;
+  const size_t kvs = (size_t)nkv * D;
   const int start = p * PART;
+  const int wbase = wid * TW;
+  // With 16-token blocks a 16-token tile is exactly one cache block, so the K rows of this
+  // wave depend only on 4 block-table entries -- not on the context length.  Partition 0 (live
+  // for every sequence) issues its K loads before anything else; the unused tail of a block
+  // table holds valid ids, so these speculative loads are always in bounds.
+  bf16x8 kf[NTILE][D / 32];
+  int tblk[NTILE];  // cache block of each 16-token tile of this wave (reused for V)
+  auto load_k = [&]() {
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      const int blk = bt[min((start + wbase) / 16 + t, max_blocks - 1)];
+      tblk[t] = blk;
+      const bf16_t* kp = k_cache + (size_t)(blk * 16 + li) * kvs + (size_t)kvh * D + g4 * 8;
+#pragma unroll
+      for (int kk = 0; kk < D / 32; ++kk) kf[t][kk] = *reinterpret_cast<const bf16x8*>(kp + kk * 32);
+    }
+  };
+  if (p == 0) load_k();
+  const int ctx = context_lens[b];
   if (ctx <= 0 || start >= ctx) return;
+  if (p != 0) load_k();
   const int n = min(PART, ctx - start);
   const int pos = ctx - 1;
-  const bool owner = pos < start + n;  // this partition holds the new token
+  const bool owner = pos < start + n;
   const int nq = nkv * G;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bf16_t* row = qkv + (size_t)b * (nq + 2 * nkv) * D;
   const float* cs = cos_sin + (size_t)pos * D;
-  const int* bt = block_tables + (size_t)b * max_blocks;
-  const float qscale = scale * LOG2E_F;
+  const int pslot = bt[pos / 16] * 16 + pos % 16;
 
-  // ---- rotate q (and k / copy v when owner); rotate-half pairs (i, i + D/2)
-  for (int i = tid; i < (G + 2) * HALF; i += NT) {
-    const int h = i / HALF, d = i - h * HALF;
-    if (h < G) {
-      const bf16_t* x = row + (size_t)(kvh * G + h) * D;
-      const float x1 = bf2f(x[d]), x2 = bf2f(x[d + HALF]);
-      const float c = cs[d], s = cs[d + HALF];
-      // round to bf16 like the unfused path (q is stored as bf16 there)
-      qs[h][d] = bf2f(f2bf(x1 * c - x2 * s)) * qscale;
-      qs[h][d + HALF] = bf2f(f2bf(x2 * c + x1 * s)) * qscale;
-    } else if (owner) {
-      if (h == G) {
-        const bf16_t* x = row + (size_t)(nq + kvh) * D;
-        const float x1 = bf2f(x[d]), x2 = bf2f(x[d + HALF]);
-        const float c = cs[d], s = cs[d + HALF];
-        const bf16_t k1 = f2bf(x1 * c - x2 * s), k2 = f2bf(x2 * c + x1 * s);
-        kcur[d] = bf2f(k1);
-        kcur[d + HALF] = bf2f(k2);
-        const int slot = bt[pos / block_size] * block_size + pos % block_size;
-        bf16_t* kd = k_cache + ((size_t)slot * nkv + kvh) * D;
-        kd[d] = k1;
-        kd[d + HALF] = k2;
-      } else {
-        const bf16_t* x = row + (size_t)(nq + nkv + kvh) * D;
-        const bf16_t v1 = x[d], v2 = x[d + HALF];
-        vcur[d] = bf2f(v1);
-        vcur[d + HALF] = bf2f(v2);
-        const int slot = bt[pos / block_size] * block_size + pos % block_size;
-        bf16_t* vd = v_cache + ((size_t)slot * nkv + kvh) * D;
-        vd[d] = v1;
-        vd[d + HALF] = v2;
+  // ---- prologue: RoPE (two rotation pairs per item), zero padding heads, clear accumulators
+  for (int i = tid; i < 16 * (HALF / 2) + 2 * (HALF / 2); i += NT) {
+    const int h = i / (HALF / 2), d = 2 * (i - h * (HALF / 2));
+    if (h < 16) {
+      uint32_t lo_pair = 0, hi_pair = 0;
+      if (h < G) {
+        const bf16_t* x = row + (size_t)(kvh * G + h) * D;
+        const uint32_t a = *reinterpret_cast<const uint32_t*>(x + d);
+        const uint32_t c2 = *reinterpret_cast<const uint32_t*>(x + d + HALF);
+        const float c0 = cs[d], c1 = cs[d + 1], s0 = cs[d + HALF], s1 = cs[d + HALF + 1];
+        lo_pair = pack_bf2(lo_bf(a) * c0 - lo_bf(c2) * s0, hi_bf(a) * c1 - hi_bf(c2) * s1);
+        hi_pair = pack_bf2(lo_bf(c2) * c0 + lo_bf(a) * s0, hi_bf(c2) * c1 + hi_bf(a) * s1);
       }
+      *reinterpret_cast<uint32_t*>(&qs[h][d]) = lo_pair;
+      *reinterpret_cast<uint32_t*>(&qs[h][d + HALF]) = hi_pair;
+    } else if (owner) {
+      const bool isk = (h == 16);
+      const bf16_t* x = row + (size_t)(isk ? nq + kvh : nq + nkv + kvh) * D;
+      const uint32_t a = *reinterpret_cast<const uint32_t*>(x + d);
+      const uint32_t c2 = *reinterpret_cast<const uint32_t*>(x + d + HALF);
+      uint32_t lo_pair = a, hi_pair = c2;
+      if (isk) {
+        const float c0 = cs[d], c1 = cs[d + 1], s0 = cs[d + HALF], s1 = cs[d + HALF + 1];
+        lo_pair = pack_bf2(lo_bf(a) * c0 - lo_bf(c2) * s0, hi_bf(a) * c1 - hi_bf(c2) * s1);
+        hi_pair = pack_bf2(lo_bf(c2) * c0 + lo_bf(a) * s0, hi_bf(c2) * c1 + hi_bf(a) * s1);
+      }
+      bf16_t* dst = (isk ? k_cache : v_cache) + (size_t)pslot * kvs + (size_t)kvh * D;
+      *reinterpret_cast<uint32_t*>(dst + d) = lo_pair;
+      *reinterpret_cast<uint32_t*>(dst + d + HALF) = hi_pair;
+      bf16_t* keep = isk ? kcur : vcur;
+      *reinterpret_cast<uint32_t*>(keep + d) = lo_pair;
+      *reinterpret_cast<uint32_t*>(keep + d + HALF) = hi_pair;
     }
   }
   for (int i = tid; i < G * D; i += NT) (&red[0][0])[i] = 0.f;
   __syncthreads();
 
-  // ---- scores (log2 domain): wave w owns tokens [w*TOK_W, (w+1)*TOK_W) of the partition
-  const int sub = lane % LPT, tiw = lane / LPT;
-  const int wbase = wid * TOK_W;
-  const int wn = max(0, min(TOK_W, n - wbase));  // valid tokens of this wave
-  for (int s0 = 0; s0 < wn; s0 += KB * TPW) {
-    u32x4 kreg[KB];
+  // Q^T fragments (B operand): lane holds Q[head li][d = 32kk + 8*g4 + j]
+  bf16x8 qf[D / 32];
 #pragma unroll
-    for (int st = 0; st < KB; ++st) {
-      const int i = wbase + s0 + st * TPW + tiw;
-      const int tt = start + min(i, n - 1);
-      const int slot = bt[tt / block_size] * block_size + tt % block_size;
-      kreg[st] = *reinterpret_cast<const u32x4*>(k_cache + ((size_t)slot * nkv + kvh) * D + sub * 8);
+  for (int kk = 0; kk < D / 32; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(&qs[li][kk * 32 + g4 * 8]);
+
+  // ---- S^T = K . Q^T over this wave's tokens; lane holds S[token 16t + 4*g4 + i][head li]
+  const int wn = max(0, min(TW, n - wbase));
+  const float qscale = scale * LOG2E_F;
+  f32x4 sacc[NTILE];
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t) {
+    if (start + wbase + 16 * t + li == pos) {  // the fresh key (cache write may not be visible yet)
+#pragma unroll
+      for (int kk = 0; kk < D / 32; ++kk) kf[t][kk] = *reinterpret_cast<const bf16x8*>(&kcur[kk * 32 + g4 * 8]);
     }
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int st = 0; st < KB; ++st) {
-      const int i = wbase + s0 + st * TPW + tiw;
-      float kf[8];
-      if (start + i == pos) {
+    for (int kk = 0; kk < D / 32; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][kk], qf[kk], acc, 0, 0, 0);
+    sacc[t] = acc;
+  }
+  // V rows of the first 32-key step: loads issued now (K registers are free), consumed after the
+  // softmax exchange; the second step's loads are issued once the first is staged in LDS
+  u32x4 vv[8];
+  auto load_v = [&](int st) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) kf[j] = kcur[sub * 8 + j];
-      } else {
+    for (int q = 0; q < 8; ++q) {
+      const int c = lane + 64 * q, r = c >> 4, ch = c & 15;
+      const int blk = (r < 16) ? tblk[2 * st] : tblk[2 * st + 1];  // r < 16 <=> q < 4 (lane-independent)
+      vv[q] = *reinterpret_cast<const u32x4*>(v_cache + (size_t)(blk * 16 + (r & 15)) * kvs + (size_t)kvh * D + ch * 8);
+    }
+  };
+  if (wn > 0) load_v(0);
+  // scale, mask, wave-local max per head
+  float m = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { kf[2 * j] = lo_bf(kreg[st][j]); kf[2 * j + 1] = hi_bf(kreg[st][j]); }
+  for (int t = 0; t < NTILE; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = 16 * t + 4 * g4 + i;
+      const float v = k < wn ? sacc[t][i] * qscale : -INFINITY;
+      sacc[t][i] = v;
+      m = fmaxf(m, v);
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 16, WAVE));
+  m = fmaxf(m, __shfl_xor(m, 32, WAVE));
+  if (g4 == 0) wm[wid][li] = m;
+  __syncthreads();
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w][li]);
+  float l = 0.f;
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float e = exp2f(sacc[t][i] - M);
+      sacc[t][i] = e;
+      l += e;
+    }
+  }
+  l += __shfl_xor(l, 16, WAVE);
+  l += __shfl_xor(l, 32, WAVE);
+  if (g4 == 0) wl[wid][li] = l;
+
+  // ---- O = P . V over 32-key steps; V staged per wave in LDS (swizzled 16-byte chunks)
+  f32x4 o[D / 16];
+#pragma unroll
+  for (int nn = 0; nn < D / 16; ++nn) o[nn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  char* vb = vbuf[wid];
+  const int qd = li >> 2, pd = li & 3;
+#pragma unroll
+  for (int st = 0; st < NTILE / 2; ++st) {
+    if (32 * st < wn) {  // wave-uniform
+      // stage the 32 keys x 128 d loaded above (fresh token from LDS, keys past the wave zeroed)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int c = lane + 64 * q, r = c >> 4, ch = c & 15;
+        const int k = 32 * st + r;
+        if (start + wbase + k == pos) vv[q] = *reinterpret_cast<const u32x4*>(&vcur[ch * 8]);
+        if (k >= wn) vv[q] = u32x4{0u, 0u, 0u, 0u};
       }
-      float part[G];
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        float acc = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc += qs[g][sub * 8 + j] * kf[j];
-        part[g] = acc;
+      for (int q = 0; q < 8; ++q) {
+        const int c = lane + 64 * q, r = c >> 4, ch = c & 15;
+        *reinterpret_cast<u32x4*>(vb + r * (D * 2) + 16 * (ch ^ vswz(r))) = vv[q];
       }
+      if (st + 1 < NTILE / 2 && 32 * (st + 1) < wn) load_v(st + 1);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // A operand: P with the key order (4*g4 + j | 16 + 4*g4 + j) of the 32-key step
+      bf16x8 pa;
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-#pragma unroll
-        for (int o = LPT / 2; o > 0; o >>= 1) part[g] += __shfl_xor(part[g], o, WAVE);
+      for (int j = 0; j < 4; ++j) {
+        pa[j] = (__bf16)sacc[2 * st][j];
+        pa[4 + j] = (__bf16)sacc[2 * st + 1][j];
       }
-      if (sub == 0 && i < wbase + wn) {
+      const int r0 = 4 * g4 + qd, r1 = r0 + 16;
 #pragma unroll
-        for (int g = 0; g < G; ++g) sc[g][i] = part[g];
+      for (int nn = 0; nn < D / 16; ++nn) {
+        const int col = 16 * nn + 4 * pd;
+        const int ch = col >> 3, hb = (col & 7) * 2;
+        const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4_t*)(vb + r0 * (D * 2) + 16 * (ch ^ vswz(r0)) + hb));
+        const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4_t*)(vb + r1 * (D * 2) + 16 * (ch ^ vswz(r1)) + hb));
+        bf16x8 vbf;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { vbf[j] = v0[j]; vbf[4 + j] = v1[j]; }
+        o[nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vbf, o[nn], 0, 0, 0);
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // tr reads done before the next step overwrites vbuf
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  // o[nn][i] = O[head 4*g4 + i][d = 16nn + li].  Cross-wave sum: every wave parks its partial in
+  // the (now idle) V staging area, then each thread adds one (head, d) over the waves -- no LDS
+  // atomics (16 waves adding into the same addresses serialise).
+  __syncthreads();  // all waves done with vbuf
+  float* part = reinterpret_cast<float*>(&vbuf[0][0]);  // [NW][G][D] floats (G*D*4*NW <= sizeof vbuf)
+  static_assert(NW * G * D * 4 <= NW * 32 * D * 2, "partials fit in the V staging area");
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int h = 4 * g4 + i;
+    if (h < G) {
+#pragma unroll
+      for (int nn = 0; nn < D / 16; ++nn) part[(wid * G + h) * D + 16 * nn + li] = wn > 0 ? o[nn][i] : 0.f;
     }
   }
   __syncthreads();
-
-  // ---- per-wave softmax over the wave's own slice (no barrier): local max m_w and sum l_w per
-  // head; p = exp2(s - m_w) stays in sc.  The waves are combined once, below.
-  float mloc[G];
+  for (int i = tid; i < G * D; i += NT) {
+    float a = 0.f;
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float m = -INFINITY;
-    for (int i = lane; i < wn; i += WAVE) m = fmaxf(m, sc[g][wbase + i]);
-    m = wave_max(m);
-    const float mu = (m == -INFINITY) ? 0.f : m;
-    float l = 0.f;
-    for (int i = lane; i < wn; i += WAVE) {
-      const float e = exp2f(sc[g][wbase + i] - mu);
-      sc[g][wbase + i] = e;
-      l += e;
-    }
-    l = wave_sum(l);
-    mloc[g] = m;
-    if (lane == 0) { wm[wid][g] = m; wl[wid][g] = l; }
-  }
-
-  // ---- p . v : lane owns dims (2*lane, 2*lane+1); V row loads in batches of VB per lane
-  float acc[G][2];
-#pragma unroll
-  for (int g = 0; g < G; ++g) acc[g][0] = acc[g][1] = 0.f;
-  const int d0 = 2 * lane;
-  if (d0 < D && wn > 0) {
-    for (int k0 = 0; k0 < wn; k0 += VB) {
-      uint32_t vreg[VB];
-#pragma unroll
-      for (int k = 0; k < VB; ++k) {
-        const int tt = start + wbase + min(k0 + k, wn - 1);
-        const int slot = bt[tt / block_size] * block_size + tt % block_size;
-        vreg[k] = *reinterpret_cast<const uint32_t*>(v_cache + ((size_t)slot * nkv + kvh) * D + d0);
-      }
-#pragma unroll
-      for (int k = 0; k < VB; ++k) {
-        const int i = wbase + k0 + k;
-        if (k0 + k < wn) {
-          float v0, v1;
-          if (start + i == pos) { v0 = vcur[d0]; v1 = vcur[d0 + 1]; }
-          else { v0 = lo_bf(vreg[k]); v1 = hi_bf(vreg[k]); }
-#pragma unroll
-          for (int g = 0; g < G; ++g) {
-            const float pg = sc[g][i];
-            acc[g][0] += pg * v0;
-            acc[g][1] += pg * v1;
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();  // wm / wl of every wave visible
-  if (tid < G) {
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w][tid]);
-    float L = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w)
-      if (wm[w][tid] != -INFINITY) L += wl[w][tid] * exp2f(wm[w][tid] - M);
-    stat[tid][0] = M;
-    stat[tid][1] = L;
-  }
-  if (d0 < D && wn > 0) {
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float M = -INFINITY;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w][g]);
-      const float f = exp2f(mloc[g] - M);
-      atomicAdd(&red[g][d0], acc[g][0] * f);
-      atomicAdd(&red[g][d0 + 1], acc[g][1] * f);
-    }
+    for (int w = 0; w < NW; ++w) a += part[w * G * D + i];
+    (&red[0][0])[i] = a;
   }
   __syncthreads();
   const bool single = ctx <= PART;
   for (int i = tid; i < G * D; i += NT) {
     const int g = i / D, d = i - g * D;
+    float L = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) L += wl[w][g];
     const int h = kvh * G + g;
-    const float s = red[g][d];
+    const float sacc_v = red[g][d];
     if (single) {
-      out[((size_t)b * nq + h) * D + d] = f2bf(s / stat[g][1]);
+      out[((size_t)b * nq + h) * D + d] = f2bf(sacc_v / L);
     } else {
+      float Mx = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) Mx = fmaxf(Mx, wm[w][g]);
       const size_t pi = ((size_t)b * nq + h) * pmax + p;
-      part_acc[pi * D + d] = s;
-      if (d == 0) { part_ml[pi * 2] = stat[g][0]; part_ml[pi * 2 + 1] = stat[g][1]; }
+      part_acc[pi * D + d] = sacc_v;
+      if (d == 0) { part_ml[pi * 2] = Mx; part_ml[pi * 2 + 1] = L; }
     }
   }
 }
@@ -259,11 +311,12 @@ extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_
                                           int block_size, int max_blocks, int pmax, hipStream_t stream) {
   if (B <= 0) return 0;
   if (D != 128 || nq % nkv != 0) return -1;
+  if (block_size != 16) return -4;  // the speculative K loads assume one 16-token block per tile
   if (pmax > 1 && (part_acc == nullptr || part_ml == nullptr)) return -3;
   const int G = nq / nkv;
   dim3 grid(pmax, nkv, B);
 #define L(GG)                                                                                               \
-  decode_fused_kernel<128, GG, 1024><<<grid, 512, 0, stream>>>(                                             \
+  decode_fused_kernel<128, GG, 1024><<<grid, 1024, 0, stream>>>(                                             \
       (bf16_t*)out, (float*)part_acc, (float*)part_ml, (const bf16_t*)qkv, cos_sin, (bf16_t*)k_cache,       \
       (bf16_t*)v_cache, block_tables, context_lens, scale, block_size, max_blocks, nkv, pmax)
   switch (G) {
@@ -271,6 +324,7 @@ extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_
     case 2: L(2); break;
     case 4: L(4); break;
     case 8: L(8); break;
+    case 16: L(16); break;
     default: return -2;
   }
 #undef L

@@ -62,6 +62,25 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
   const int klen = min(KS, K - kb);
   const int nch = klen >> 3;  // 16-byte chunks in this slice
 
+  constexpr int NR = (EPI == EPI_SWIGLU) ? 2 * RPW : RPW;  // weight rows per wave
+  constexpr int U = (NR >= 4) ? 2 : ((NR >= 2) ? 4 : 8);  // chunks per lane in flight per row
+  const int r0 = (blockIdx.x * 4 + wid) * RPW;               // first output row of this wave
+  const bool active = r0 < N_out;
+  const bf16_t* wrow[NR];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int n = min(r0 + r, N_out - 1);
+    wrow[r] = W + (size_t)n * K + kb;
+    if (EPI == EPI_SWIGLU) wrow[RPW + r] = W + (size_t)(n + half_rows) * K + kb;
+  }
+  // weights do not depend on x: start streaming them before the x staging / norm prologue
+  u32x4 wv[U][NR];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + min(lane + 64 * u, nch - 1));
+
   if (NORM) {
     const bool writer = blockIdx.x == 0 && blockIdx.y == 0 && res_out != nullptr;
     float inv[M];
@@ -105,50 +124,38 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
   }
   __syncthreads();
 
-  constexpr int NR = (EPI == EPI_SWIGLU) ? 2 * RPW : RPW;  // weight rows per wave
-  const int r0 = (blockIdx.x * 4 + wid) * RPW;               // first output row of this wave
-  if (r0 >= N_out) return;
-  const bf16_t* wrow[NR];
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) {
-    const int n = min(r0 + r, N_out - 1);
-    wrow[r] = W + (size_t)n * K + kb;
-    if (EPI == EPI_SWIGLU) wrow[RPW + r] = W + (size_t)(n + half_rows) * K + kb;
-  }
+  // main loop: software-pipelined weight stream (the loads of block i+1 are in flight while block
+  // i is consumed); the first block was issued before the x / norm prologue
   float acc[NR][M];
 #pragma unroll
   for (int r = 0; r < NR; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
-
-  constexpr int U = (NR >= 4) ? 2 : ((NR >= 2) ? 4 : 8);  // chunks per lane in flight per row
-  int c = lane;
-  for (; c + 64 * (U - 1) < nch; c += 64 * U) {
-    u32x4 wv[U][NR];
+  if (!active) return;
+  for (int c = lane; c < nch; c += 64 * U) {
+    u32x4 cur[U][NR];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int r = 0; r < NR; ++r)
-        wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + c + 64 * u);
+      for (int r = 0; r < NR; ++r) cur[u][r] = wv[u][r];
+    const int cn = c + 64 * U;
+    if (cn < nch) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+          wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + min(cn + 64 * u, nch - 1));
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      if (c + 64 * u < nch) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const u32x4 xv = xs[m * (KS >> 3) + c + 64 * u];
+        for (int m = 0; m < M; ++m) {
+          const u32x4 xv = xs[m * (KS >> 3) + c + 64 * u];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) acc[r][m] = dot8(wv[u][r], xv, acc[r][m]);
+          for (int r = 0; r < NR; ++r) acc[r][m] = dot8(cur[u][r], xv, acc[r][m]);
+        }
       }
-    }
-  }
-  for (; c < nch; c += 64) {
-    u32x4 wv[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) wv[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + c);
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const u32x4 xv = xs[m * (KS >> 3) + c];
-#pragma unroll
-      for (int r = 0; r < NR; ++r) acc[r][m] = dot8(wv[r], xv, acc[r][m]);
     }
   }
 #pragma unroll

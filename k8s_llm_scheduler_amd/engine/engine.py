@@ -124,7 +124,7 @@ class LLMEngine:
         self.requests: Dict[int, Request] = {}
         self.free_slots = list(range(max_batch - 1, -1, -1))
         self.use_graphs = cuda_graphs and self.gpu
-        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}   # (batch bucket, context class)
         self._graph_pool = None
         self.lock = threading.RLock()
         self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
@@ -143,8 +143,14 @@ class LLMEngine:
         self.s_steps = torch.zeros(B, **i32)
         self.s_hist = torch.zeros(B, self.max_new_cap, **i32)
 
-    def _decode_step(self, B: int) -> None:
-        logits = self.model.forward_decode(self.s_tokens[:B], self.s_ctx[:B], self.s_bt[:B], self.max_model_len)
+    def _ctx_classes(self) -> List[int]:
+        """Context-length classes with their own decode graph: contexts <= 1024 tokens (one
+        attention partition per sequence: no partial buffers, no merge kernel) and the rest."""
+        return sorted({min(1024, self.max_model_len), self.max_model_len})
+
+    def _decode_step(self, B: int, max_context: Optional[int] = None) -> None:
+        logits = self.model.forward_decode(self.s_tokens[:B], self.s_ctx[:B], self.s_bt[:B],
+                                           max_context or self.max_model_len)
         ops.sample(logits, self.s_temp[:B], self.s_top_p[:B], self.s_seeds[:B], self.s_ctx[:B],
                    shards=logits.shape[0], tokens_out=self.s_tokens[:B], ctx_inc=self.s_ctx[:B],
                    hist=self.s_hist[:B], steps=self.s_steps[:B])
@@ -164,19 +170,20 @@ class LLMEngine:
         buckets = buckets or [b for b in BUCKETS if b <= self.max_batch]
         stream = torch.cuda.Stream(self.device)
         for B in sorted(set(buckets)):
-            if B in self.graphs:
-                continue
-            stream.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(stream):
-                self._decode_step(B)   # warm-up: allocator + lazy init outside capture
-            torch.cuda.current_stream(self.device).wait_stream(stream)
-            torch.cuda.synchronize(self.device)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self._graph_pool, stream=stream):
-                self._decode_step(B)
-            if self._graph_pool is None:
-                self._graph_pool = g.pool()
-            self.graphs[B] = g
+            for mc in self._ctx_classes():
+                if (B, mc) in self.graphs:
+                    continue
+                stream.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(stream):
+                    self._decode_step(B, mc)   # warm-up: allocator + lazy init outside capture
+                torch.cuda.current_stream(self.device).wait_stream(stream)
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._graph_pool, stream=stream):
+                    self._decode_step(B, mc)
+                if self._graph_pool is None:
+                    self._graph_pool = g.pool()
+                self.graphs[(B, mc)] = g
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ requests
@@ -305,14 +312,17 @@ class LLMEngine:
                         for r in self.running.values())
         steps = max(1, min(self.decode_chunk, remaining))
         B = self._bucket(max(self.running) + 1)
+        # context length reached by the end of this chunk decides the graph variant
+        top = max(len(r.prompt_ids) + max(len(r.output_ids), 1) for r in self.running.values()) + steps
+        mc = next(c for c in self._ctx_classes() if top <= c)
         t0 = time.perf_counter()
-        graph = self.graphs.get(B) if self.use_graphs else None
+        graph = self.graphs.get((B, mc)) if self.use_graphs else None
         for _ in range(steps):
             if graph is not None:
                 graph.replay()
                 self.stats["graph_replays"] += 1
             else:
-                self._decode_step(B)
+                self._decode_step(B, mc)
         self.stats["decode_steps"] += steps
         hist = self.s_hist[:B].cpu()     # syncs the stream
         nsteps = self.s_steps[:B].cpu()
@@ -355,7 +365,7 @@ class LLMEngine:
     def _brace_ids(self) -> set:
         if self._brace_cache is None:
             vocab = self.tok._tok.get_vocab()
-            self._brace_cache = {i for s, i in vocab.items() if "}" in s or "}" in s}
+            self._brace_cache = {i for s, i in vocab.items() if "}" in s}
         return self._brace_cache
 
     def _finish(self, r: Request, reason: str) -> None:

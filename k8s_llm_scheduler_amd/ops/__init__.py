@@ -217,7 +217,12 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
                            max_context: int, nq: int, nkv: int, D: int) -> torch.Tensor:
     """RoPE + KV write of the new token + paged GQA attention, one kernel.  Returns [B, nq*D]."""
     B = qkv.shape[0]
-    if not _gpu(qkv, k_cache):
+    if not _gpu(qkv, k_cache) or block_size != 16:
+        if _gpu(qkv, k_cache):  # general block sizes: unfused kernels
+            q = rope_kv_write(qkv, cos_sin, k_cache, v_cache, nq, nkv, D, context_lens=context_lens,
+                              block_tables=block_tables, block_size=block_size)
+            return paged_decode_attention(q, k_cache, v_cache, block_tables, context_lens, scale, block_size,
+                                          max_context).view(B, nq * D)
         q = rope_kv_write(qkv, cos_sin, k_cache, v_cache, nq, nkv, D, context_lens=context_lens,
                           block_tables=block_tables, block_size=block_size)
         return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, context_lens, scale,
