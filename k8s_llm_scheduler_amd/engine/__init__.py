@@ -16,7 +16,7 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
                  tokenizer: Optional[str] = None, seed: int = 0, max_batch: int = 64, block_size: int = 16,
                  num_blocks: Optional[int] = None, kv_cache_gb: float = 0.0, kv_cache_fraction: float = 0.85,
                  max_model_len: int = 16384, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
-                 prefix_caching: bool = True, decode_chunk: int = 4, metrics=None, capture: bool = True):
+                 prefix_caching: bool = True, decode_chunk: int = 4, metrics=None, capture: bool = True, control=None):
     """Model + tokenizer + engine on this rank's GPU (or CPU when no GPU is present)."""
     import torch
 
@@ -39,7 +39,7 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
     eng = LLMEngine(model, tok, max_batch=max_batch, block_size=block_size, num_blocks=num_blocks,
                     kv_cache_gb=kv_cache_gb, kv_cache_fraction=kv_cache_fraction, max_model_len=max_model_len,
                     max_prefill_tokens=max_prefill_tokens, cuda_graphs=cuda_graphs, prefix_caching=prefix_caching,
-                    decode_chunk=decode_chunk, seed=seed, metrics=metrics)
+                    decode_chunk=decode_chunk, seed=seed, metrics=metrics, control=control)
     if capture and eng.use_graphs:
         t1 = time.perf_counter()
         eng.capture_graphs()
@@ -47,10 +47,10 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
     return eng
 
 
-def engine_from_config(cfg, tp=None, metrics=None):
+def engine_from_config(cfg, tp=None, metrics=None, control=None):
     e = cfg.engine
     return build_engine(e.preset, tp=tp, weights=e.weights, tokenizer=e.tokenizer, seed=e.seed,
                         max_batch=e.max_batch, block_size=e.block_size, kv_cache_gb=e.kv_cache_gb,
                         kv_cache_fraction=e.kv_cache_fraction, max_model_len=e.max_model_len,
                         max_prefill_tokens=e.max_prefill_tokens, cuda_graphs=e.cuda_graphs,
-                        prefix_caching=e.prefix_caching, metrics=metrics)
+                        prefix_caching=e.prefix_caching, metrics=metrics, control=control)

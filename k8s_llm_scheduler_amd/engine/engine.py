@@ -83,8 +83,14 @@ class LLMEngine:
     def __init__(self, model: LlamaModel, tokenizer: Tokenizer, *, max_batch: int = 64, block_size: int = 16,
                  num_blocks: Optional[int] = None, kv_cache_gb: float = 0.0, kv_cache_fraction: float = 0.85,
                  max_model_len: Optional[int] = None, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
-                 prefix_caching: bool = True, decode_chunk: int = 4, seed: int = 0, metrics=None):
+                 prefix_caching: bool = True, decode_chunk: int = 4, seed: int = 0, metrics=None,
+                 control=None):
         self.model = model
+        # Multi-rank serving: rank 0 announces new requests / aborts to the other TP ranks at the
+        # start of every step, so all ranks run the identical schedule (None: single rank, or
+        # every rank is fed identical requests, as in bench.py).
+        self.control = control
+        self._outbox: List[Request] = []
         self.tok = tokenizer
         self.device = model.device
         self.gpu = self.device.type == "cuda"
@@ -205,9 +211,48 @@ class LLMEngine:
             r = Request(next(self._ids), ids, params, seed)
             self.requests[r.rid] = r
             self.waiting.append(r)
+            if self.control is not None:
+                self._outbox.append(r)
         return r
 
+    def _sync(self) -> bool:
+        """Replicate rank 0's new requests and aborts to every rank.  Returns False on a stop
+        command (worker shutdown)."""
+        if self.control is None:
+            return True
+        if self.control.rank == 0:
+            msg = {"new": [(r.rid, r.prompt_ids, r.params.__dict__, r.seed) for r in self._outbox],
+                   "abort": sorted(r.rid for r in self.requests.values() if r.aborted and not r.finished),
+                   "stop": False}
+            self._outbox = []
+            self.control.exchange(msg)
+            return True
+        msg = self.control.exchange(None)
+        if msg.get("stop"):
+            return False
+        for rid, ids, pd, seed in msg["new"]:
+            r = Request(rid, list(ids), SamplingParams(**pd), seed)
+            self.requests[rid] = r
+            self.waiting.append(r)
+        for rid in msg["abort"]:
+            if rid in self.requests:
+                self.requests[rid].aborted = True
+        return True
+
+    def shutdown_workers(self) -> None:
+        if self.control is not None and self.control.rank == 0:
+            self.control.exchange({"new": [], "abort": [], "stop": True})
+
+    def _reap_aborted(self) -> None:
+        for r in sorted((r for r in self.requests.values() if r.aborted and not r.finished), key=lambda r: r.rid):
+            if r in self.waiting:
+                self.waiting.remove(r)
+            self._finish(r, "abort")
+        for rid in [rid for rid, r in self.requests.items() if r.aborted and r.finished]:
+            self.requests.pop(rid, None)
+
     def abort(self, rid: int) -> None:
+        """Mark a request aborted; it is removed at the start of the next step (on every rank)."""
         with self.lock:
             r = self.requests.get(rid)
             if r is not None and not r.finished:
@@ -302,12 +347,6 @@ class LLMEngine:
     def _decode(self) -> List[Request]:
         if not self.running:
             return []
-        # aborted requests leave before the next chunk
-        for slot, r in list(self.running.items()):
-            if r.aborted:
-                self._finish(r, "abort")
-        if not self.running:
-            return []
         remaining = min(r.params.max_tokens - len(r.output_ids) - (1 if not r.output_ids else 0)
                         for r in self.running.values())
         steps = max(1, min(self.decode_chunk, remaining))
@@ -389,9 +428,21 @@ class LLMEngine:
 
     def step(self) -> List[Request]:
         with self.lock:
+            if not self._sync():
+                raise StopIteration("engine stopped by rank 0")
+            self._reap_aborted()
             self._admit()
             self._prefill()
             return self._decode()
+
+    def serve_worker(self) -> None:
+        """Non-zero TP ranks: follow rank 0's schedule until it sends stop."""
+        assert self.control is not None and self.control.rank != 0
+        while True:
+            try:
+                self.step()
+            except StopIteration:
+                return
 
     def kv_utilization(self) -> float:
         return 1.0 - self.allocator.num_free / self.allocator.num_blocks
@@ -416,7 +467,11 @@ class LLMEngine:
                 if deadline is not None and time.monotonic() > deadline:
                     for r in reqs:
                         if not r.finished:
-                            self._finish(r, "timeout")
+                            r.aborted = True
+                    if self.control is None:
+                        self._reap_aborted()
+                    for r in reqs:
+                        self.requests.pop(r.rid, None) if r.finished else None
                     raise TimeoutError("decision engine deadline exceeded")
                 self.step()
             outs = [self.output(r) for r in reqs]

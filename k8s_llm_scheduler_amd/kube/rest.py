@@ -145,3 +145,22 @@ class RestKubeAPI:
                               data=json.dumps(body), headers={"Content-Type": "application/json"},
                               timeout=self.timeout)
         return self._check(r)
+
+    # ---- used by the smoke tool (kubectl apply/delete equivalents)
+    def create_pod(self, pod: Obj) -> Obj:
+        ns = pod.get("metadata", {}).get("namespace", "default")
+        r = self.session.post(f"{self.conn.server}/api/v1/namespaces/{ns}/pods", data=json.dumps(pod),
+                              headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        return self._check(r)
+
+    def delete_pod(self, namespace: str, name: str) -> None:
+        r = self.session.delete(f"{self.conn.server}/api/v1/namespaces/{namespace}/pods/{name}",
+                                timeout=self.timeout)
+        if r.status_code not in (200, 202, 404):
+            raise ApiError(r.status_code, r.reason or "", r.text)
+
+    def get_pod(self, namespace: str, name: str) -> Optional[Obj]:
+        r = self.session.get(f"{self.conn.server}/api/v1/namespaces/{namespace}/pods/{name}", timeout=self.timeout)
+        if r.status_code == 404:
+            return None
+        return self._check(r)

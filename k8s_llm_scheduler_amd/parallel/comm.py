@@ -76,6 +76,27 @@ class TPGroup:
             dist.barrier(group=self.group)
 
 
+class ControlChannel:
+    """Rank 0 -> all ranks object broadcast on a CPU (gloo) group: the serving control plane runs
+    on rank 0 and every other TP rank follows its engine schedule (engine.LLMEngine._sync)."""
+
+    def __init__(self, rank: int, group=None):
+        self.rank = rank
+        self.group = group
+
+    def exchange(self, payload):
+        obj = [payload]
+        dist.broadcast_object_list(obj, src=0, group=self.group)
+        return obj[0]
+
+
+def make_control_channel(tp: TPGroup) -> Optional[ControlChannel]:
+    if tp.world <= 1 or tp.simulate:
+        return None
+    grp = dist.new_group(backend="gloo", timeout=datetime.timedelta(days=7))
+    return ControlChannel(tp.rank, grp)
+
+
 def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600) -> TPGroup:
     """Initialise torch.distributed from torchrun env (RANK/WORLD_SIZE/MASTER_*).  Single
     process when WORLD_SIZE is unset or 1."""
