@@ -164,6 +164,8 @@ ENV_OVERRIDES = {
     "ENGINE_PRESET": ("engine", "preset", str),
     "ENGINE_BACKEND": ("engine", "backend", str),
     "ENGINE_WEIGHTS": ("engine", "weights", str),
+    "ENGINE_TOKENIZER": ("engine", "tokenizer", str),
+    "SCHEDULER_MODE": ("scheduler", "mode", str),
 }
 
 # The reference's LOG_LEVEL/LOG_FORMAT come only from env; config.yaml's logging section is
