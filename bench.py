@@ -66,7 +66,7 @@ def main() -> int:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     tp = init_from_env("cuda")
     if args.simulate_tp > 1:
         from k8s_llm_scheduler_amd.parallel import TPGroup
@@ -165,6 +165,7 @@ def main() -> int:
         "prefill_tokens_per_decision": round(st["prefill_tokens"] / max(1, decisions), 1),
         "fallback_rate": round(fallbacks / decisions, 3),
         "init_s": round(init_s, 1),
+        "tp_comm": tp.comm_info,
         "baseline_note": "BASELINE.md publishes no numbers; vs_baseline uses the implied 0.3 decisions/s of test_e2e.py",
     }
     if rank == 0:

@@ -13,6 +13,7 @@
 
 #include "runtime/block_allocator.h"
 #include "runtime/rccl_comm.h"
+#include "runtime/xgmi_comm.h"
 
 namespace py = pybind11;
 
@@ -150,6 +151,30 @@ PYBIND11_MODULE(_C, m) {
       })
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("rank", &RcclComm::rank);
+
+  using k8sllm::XgmiComm;
+  py::class_<XgmiComm>(m, "XgmiComm")
+      .def(py::init<int, int, long long, int, double>(), py::arg("world"), py::arg("rank"), py::arg("slot_bytes"),
+           py::arg("blocks") = 16, py::arg("timeout_s") = 30.0)
+      .def("handle", [](const XgmiComm& c) { return py::bytes(c.handle()); })
+      .def("open", [](XgmiComm& c, const std::vector<py::bytes>& hs) {
+        std::vector<std::string> v;
+        for (const auto& h : hs) v.emplace_back(h);
+        c.open(v);
+      })
+      .def("all_reduce_bf16", [](XgmiComm& c, uintptr_t in, uintptr_t out, long long bytes, int64_t s) {
+        c.all_reduce_bf16(P(in), P(out), bytes, S(s));
+      })
+      .def("all_gather", [](XgmiComm& c, uintptr_t in, uintptr_t out, long long bytes, int64_t s) {
+        c.all_gather(P(in), P(out), bytes, S(s));
+      })
+      .def("error", &XgmiComm::error)
+      .def("reset_error", &XgmiComm::reset_error)
+      .def_property_readonly("world", &XgmiComm::world)
+      .def_property_readonly("rank", &XgmiComm::rank)
+      .def_property_readonly("slot_bytes", &XgmiComm::slot_bytes)
+      .def_property_readonly("blocks", &XgmiComm::blocks)
+      .def_property_readonly("is_open", &XgmiComm::is_open);
 
   using k8sllm::BlockAllocator;
   py::class_<BlockAllocator::Allocation>(m, "Allocation")

@@ -1,0 +1,104 @@
+// Host side of the xGMI peer-memory communicator: IPC region allocation, handle exchange, launch.
+#include "runtime/xgmi_comm.h"
+
+#include <cstring>
+#include <stdexcept>
+
+extern "C" {
+long long k8s_xgmi_flag_bytes();
+int k8s_xgmi_max_blocks();
+int k8s_xgmi_allreduce_bf16(void* const* bases, uint32_t* counters, uint32_t* err, const void* in, void* out,
+                            long long bytes, long long slot_bytes, int rank, int world, int blocks,
+                            long long timeout_ticks, hipStream_t s);
+int k8s_xgmi_allgather(void* const* bases, uint32_t* counters, uint32_t* err, const void* in, void* out,
+                       long long bytes, long long slot_bytes, int rank, int world, int blocks,
+                       long long timeout_ticks, hipStream_t s);
+}
+
+namespace k8sllm {
+
+namespace {
+void ck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+void ckrc(int rc, const char* what) {
+  if (rc == 0) return;
+  if (rc < 0) throw std::invalid_argument(std::string(what) + ": invalid arguments (code " + std::to_string(rc) + ")");
+  throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(static_cast<hipError_t>(rc)));
+}
+}  // namespace
+
+XgmiComm::XgmiComm(int world, int rank, long long slot_bytes, int blocks, double timeout_s)
+    : world_(world), rank_(rank), blocks_(blocks), slot_bytes_(slot_bytes) {
+  if (world < 2 || world > 8 || rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad world/rank");
+  if (slot_bytes <= 0 || (slot_bytes & 4095)) throw std::invalid_argument("XgmiComm: slot_bytes must be a multiple of 4096");
+  if (blocks < 1 || blocks > k8s_xgmi_max_blocks()) throw std::invalid_argument("XgmiComm: bad block count");
+  region_bytes_ = k8s_xgmi_flag_bytes() + 2LL * world * slot_bytes;
+  if (region_bytes_ > 0x7fffffffLL) throw std::invalid_argument("XgmiComm: region larger than 2 GiB");
+  timeout_ticks_ = static_cast<long long>(timeout_s * 100e6);  // s_memrealtime runs at 100 MHz
+  ck(hipGetDevice(&device_), "hipGetDevice");
+  ck(hipExtMallocWithFlags(&region_, region_bytes_, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
+  ck(hipMemset(region_, 0, region_bytes_), "hipMemset");
+  ck(hipMalloc(&counters_, (k8s_xgmi_max_blocks() + 1) * sizeof(uint32_t)), "hipMalloc");
+  ck(hipMemset(counters_, 0, (k8s_xgmi_max_blocks() + 1) * sizeof(uint32_t)), "hipMemset");
+  ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  bases_.assign(world, nullptr);
+  mapped_.assign(world, false);
+  bases_[rank] = region_;
+}
+
+XgmiComm::~XgmiComm() {
+  for (int i = 0; i < world_; ++i)
+    if (mapped_[i] && bases_[i]) (void)hipIpcCloseMemHandle(bases_[i]);
+  if (region_) (void)hipFree(region_);
+  if (counters_) (void)hipFree(counters_);
+}
+
+std::string XgmiComm::handle() const {
+  hipIpcMemHandle_t h;
+  ck(hipIpcGetMemHandle(&h, region_), "hipIpcGetMemHandle");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void XgmiComm::open(const std::vector<std::string>& handles) {
+  if (opened_) throw std::runtime_error("XgmiComm: already open");
+  if ((int)handles.size() != world_) throw std::invalid_argument("XgmiComm::open: need one handle per rank");
+  for (int i = 0; i < world_; ++i) {
+    if (i == rank_) continue;
+    if (handles[i].size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("XgmiComm::open: bad handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles[i].data(), sizeof(h));
+    void* p = nullptr;
+    ck(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    bases_[i] = p;
+    mapped_[i] = true;
+  }
+  opened_ = true;
+}
+
+void XgmiComm::all_reduce_bf16(const void* in, void* out, long long bytes, hipStream_t s) {
+  if (!opened_) throw std::runtime_error("XgmiComm: not open");
+  ckrc(k8s_xgmi_allreduce_bf16(bases_.data(), counters_, counters_ + k8s_xgmi_max_blocks(), in, out, bytes,
+                               slot_bytes_, rank_, world_, blocks_, timeout_ticks_, s),
+       "xgmi all_reduce");
+}
+
+void XgmiComm::all_gather(const void* in, void* out, long long bytes, hipStream_t s) {
+  if (!opened_) throw std::runtime_error("XgmiComm: not open");
+  ckrc(k8s_xgmi_allgather(bases_.data(), counters_, counters_ + k8s_xgmi_max_blocks(), in, out, bytes, slot_bytes_,
+                          rank_, world_, blocks_, timeout_ticks_, s),
+       "xgmi all_gather");
+}
+
+uint32_t XgmiComm::error() {
+  uint32_t v = 0;
+  ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  ck(hipMemcpy(&v, counters_ + k8s_xgmi_max_blocks(), sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy");
+  return v;
+}
+
+void XgmiComm::reset_error() {
+  ck(hipMemset(counters_ + k8s_xgmi_max_blocks(), 0, sizeof(uint32_t)), "hipMemset");
+}
+
+}  // namespace k8sllm

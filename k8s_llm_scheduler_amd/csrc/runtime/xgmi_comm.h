@@ -1,0 +1,44 @@
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace k8sllm {
+
+// Peer-memory communicator for the decode-time collectives (see kernels/xgmi.hip for the protocol).
+// Lifecycle: construct on every rank -> exchange handle() bytes (torch.distributed) -> open(all
+// handles) -> all_reduce_bf16 / all_gather on any stream, graph-capturable.
+class XgmiComm {
+ public:
+  XgmiComm(int world, int rank, long long slot_bytes, int blocks, double timeout_s);
+  ~XgmiComm();
+  XgmiComm(const XgmiComm&) = delete;
+  XgmiComm& operator=(const XgmiComm&) = delete;
+
+  std::string handle() const;                        // hipIpcMemHandle_t bytes of this rank's region
+  void open(const std::vector<std::string>& handles);  // map every peer's region (index = rank)
+  void all_reduce_bf16(const void* in, void* out, long long bytes, hipStream_t s);
+  void all_gather(const void* in, void* out, long long bytes_per_rank, hipStream_t s);
+  uint32_t error();                                   // poll-timeout bitmask (synchronizes the device)
+  void reset_error();
+
+  int world() const { return world_; }
+  int rank() const { return rank_; }
+  long long slot_bytes() const { return slot_bytes_; }
+  int blocks() const { return blocks_; }
+  bool is_open() const { return opened_; }
+
+ private:
+  int world_, rank_, blocks_;
+  long long slot_bytes_, region_bytes_, timeout_ticks_;
+  int device_ = 0;
+  void* region_ = nullptr;      // own IPC region (uncached)
+  uint32_t* counters_ = nullptr;  // [max_blocks] epochs + 1 error word
+  std::vector<void*> bases_;    // every rank's region in this address space
+  std::vector<bool> mapped_;    // true where bases_[i] came from hipIpcOpenMemHandle
+  bool opened_ = false;
+};
+
+}  // namespace k8sllm

@@ -9,13 +9,21 @@ Design choices for 8 x MI355X over point-to-point xGMI (7 links x ~153 GB/s per 
   is issued in-place on the producing tensor (no staging copies) and captured in the graph.
 * The vocabulary-parallel LM head gathers fp32 logits [tp, B, V/tp] directly in shard-major
   order; the sampler consumes that layout without a transpose.
+* Messages up to ``slot_bytes`` go through the native one-shot xGMI peer-memory collectives
+  (``XgmiComm``, csrc/kernels/xgmi.hip): one fabric crossing instead of a ring's 2(W-1) hops.
+  It is enabled only when every rank can map every peer's memory, it passes a self-test, and
+  (``K8S_TP_COMM=auto``) it beats RCCL in a graph-timed probe on this node.  Larger messages
+  (batched prefill) use RCCL.
 """
 
 from __future__ import annotations
 
 import datetime
+import logging
 import os
-from dataclasses import dataclass
+import socket
+import time
+from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
@@ -23,6 +31,7 @@ import torch.distributed as dist
 
 
 _DT = {torch.bfloat16: 0, torch.float32: 1, torch.float16: 2, torch.int32: 3}
+log = logging.getLogger(__name__)
 
 
 @dataclass
@@ -33,6 +42,12 @@ class TPGroup:
     backend: str = "none"
     rccl: Optional[object] = None   # native RcclComm (GPU): graph-capturable collectives
     simulate: bool = False          # shapes of a TP rank, collectives skipped (profiling only)
+    xgmi: Optional[object] = None   # native XgmiComm: one-shot peer-memory collectives (small messages)
+    comm_info: dict = field(default_factory=dict)
+
+    def _xgmi_ok(self, t: torch.Tensor) -> bool:
+        n = t.numel() * t.element_size()
+        return self.xgmi is not None and t.is_cuda and n % 16 == 0 and 0 < n <= self.xgmi.slot_bytes
 
     @property
     def enabled(self) -> bool:
@@ -40,7 +55,9 @@ class TPGroup:
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1 and not self.simulate:
-            if self.rccl is not None and t.is_cuda:
+            if t.dtype == torch.bfloat16 and t.is_contiguous() and self._xgmi_ok(t):
+                self.xgmi.all_reduce_bf16(t.data_ptr(), t.data_ptr(), t.numel() * 2, -1)
+            elif self.rccl is not None and t.is_cuda:
                 self.rccl.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], 0, -1)
             elif self.backend == "gloo" and t.dtype == torch.bfloat16:
                 f = t.float()
@@ -58,7 +75,9 @@ class TPGroup:
             return t.unsqueeze(0).expand(self.world, *t.shape).contiguous()
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         t = t.contiguous()
-        if self.rccl is not None and t.is_cuda:
+        if self._xgmi_ok(t):
+            self.xgmi.all_gather(t.data_ptr(), out.data_ptr(), t.numel() * t.element_size(), -1)
+        elif self.rccl is not None and t.is_cuda:
             self.rccl.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], -1)
         elif self.backend == "gloo":
             dist.all_gather(list(out.unbind(0)), t.contiguous(), group=self.group)
@@ -97,28 +116,46 @@ def make_control_channel(tp: TPGroup) -> Optional[ControlChannel]:
     return ControlChannel(tp.rank, grp)
 
 
-def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600) -> TPGroup:
+def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backend: Optional[str] = None,
+                  comm: Optional[str] = None) -> TPGroup:
     """Initialise torch.distributed from torchrun env (RANK/WORLD_SIZE/MASTER_*).  Single
-    process when WORLD_SIZE is unset or 1."""
+    process when WORLD_SIZE is unset or 1.
+
+    ``backend``: process-group backend (default ``nccl`` = RCCL on GPU, ``gloo`` on CPU; env
+    ``K8S_TP_BACKEND``).  ``comm`` (env ``K8S_TP_COMM``): ``auto`` = RCCL plus the xGMI one-shot
+    collectives when they are faster, ``rccl`` = RCCL only, ``xgmi`` = xGMI for every message that
+    fits (no RCCL communicator at all under a gloo process group, e.g. several ranks sharing one GPU
+    in tests).  Rank r uses GPU ``LOCAL_RANK % device_count``."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world <= 1:
         return TPGroup()
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
-    backend = "nccl" if device_type == "cuda" else "gloo"
+    backend = backend or os.environ.get("K8S_TP_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
+    comm = comm or os.environ.get("K8S_TP_COMM", "auto")
+    if comm not in ("auto", "rccl", "xgmi"):
+        raise ValueError(f"K8S_TP_COMM must be auto, rccl or xgmi (got {comm!r})")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if not dist.is_initialized():
         kw = {}
-        if backend == "nccl":
-            local = int(os.environ.get("LOCAL_RANK", rank))
+        if device_type == "cuda":
+            local = int(os.environ.get("LOCAL_RANK", rank)) % max(1, torch.cuda.device_count())
             torch.cuda.set_device(local)
-            kw["device_id"] = torch.device("cuda", local)
+            if backend == "nccl":
+                kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     tp = TPGroup(rank, world, dist.group.WORLD, backend)
-    if backend == "nccl" and os.environ.get("K8S_TP_COMM", "rccl") == "rccl":
-        tp.rccl = make_rccl_comm(tp)
+    if device_type == "cuda":
+        if backend == "nccl" and comm in ("auto", "rccl"):
+            tp.rccl = make_rccl_comm(tp)
+        if comm in ("auto", "xgmi"):
+            tp.xgmi = make_xgmi_comm(tp)
+        if comm == "auto" and tp.xgmi is not None and tp.rccl is not None:
+            autotune_comm(tp)
+        tp.comm_info["selected"] = "xgmi+rccl" if tp.xgmi is not None and tp.rccl is not None else \
+            ("xgmi" if tp.xgmi is not None else ("rccl" if tp.rccl is not None else backend))
     return tp
 
 
@@ -140,3 +177,117 @@ def make_rccl_comm(tp: TPGroup):
     if float(probe[0]) != float(tp.world):
         raise RuntimeError(f"RCCL communicator self-test failed: {float(probe[0])} != {tp.world}")
     return comm
+
+
+def _agree(tp: TPGroup, ok: bool) -> bool:
+    """True iff ``ok`` on every rank (every rank must call this)."""
+    flags = [None] * tp.world
+    dist.all_gather_object(flags, bool(ok), group=tp.group)
+    return all(flags)
+
+
+def make_xgmi_comm(tp: TPGroup, slot_bytes: Optional[int] = None, blocks: Optional[int] = None,
+                   timeout_s: float = 60.0):
+    """Map every rank's IPC region into every process and self-test the one-shot collectives.
+    Returns None (on every rank alike) when any rank cannot take part."""
+    from .. import ops
+
+    slot_bytes = int(slot_bytes or os.environ.get("K8S_XGMI_MAX_BYTES", 512 * 1024))
+    slot_bytes = (slot_bytes + 4095) // 4096 * 4096
+    blocks = int(blocks or os.environ.get("K8S_XGMI_BLOCKS", 16))
+    dev = torch.cuda.current_device()
+    comm, handle, err = None, b"", ""
+    try:
+        if tp.world > 8:
+            raise RuntimeError("more than 8 ranks")
+        comm = ops.native().XgmiComm(tp.world, tp.rank, slot_bytes, blocks, timeout_s)
+        handle = comm.handle()
+    except Exception as e:  # noqa: BLE001 -- every rank must still join the exchange below
+        err = str(e)
+    info = [None] * tp.world
+    dist.all_gather_object(info, (socket.gethostname(), dev, handle, err), group=tp.group)
+    ok = all(h == info[0][0] and hd and not er for h, _, hd, er in info)
+    if ok:
+        try:
+            for _, d, _, _ in info:
+                if d != dev and not torch.cuda.can_device_access_peer(dev, d):
+                    raise RuntimeError(f"GPU {dev} cannot access GPU {d}")
+            comm.open([x[2] for x in info])
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, str(e)
+    if not _agree(tp, ok):
+        reasons = sorted({x[3] for x in info if x[3]} | ({err} if err else set()))
+        log.warning(f" xGMI peer-memory collectives disabled: {'; '.join(reasons) or 'a peer could not map memory'}")
+        return None
+    ok = _xgmi_selftest(tp, comm, dev)
+    if not _agree(tp, ok):
+        log.warning(" xGMI peer-memory collectives disabled: self-test failed")
+        return None
+    return comm
+
+
+def _xgmi_selftest(tp: TPGroup, comm, dev) -> bool:
+    try:
+        n = min(comm.slot_bytes // 2, 64 * 1024)
+        for it in range(3):  # both slots, then the first again
+            x = (torch.arange(n, device=dev, dtype=torch.float32) % 61 + tp.rank * 3 + it).to(torch.bfloat16)
+            want = sum((torch.arange(n, device=dev, dtype=torch.float32) % 61 + r * 3 + it) for r in range(tp.world))
+            comm.all_reduce_bf16(x.data_ptr(), x.data_ptr(), n * 2, -1)
+            g_in = torch.full((1024,), float(tp.rank + it), device=dev)
+            g_out = torch.empty((tp.world, 1024), device=dev)
+            comm.all_gather(g_in.data_ptr(), g_out.data_ptr(), 4096, -1)
+            torch.cuda.synchronize(dev)
+            if comm.error() != 0:
+                return False
+            if not torch.equal(x.float(), want.to(torch.bfloat16).float()):
+                return False
+            if not torch.equal(g_out[:, 0].cpu(), torch.arange(tp.world, dtype=torch.float32) + it):
+                return False
+        return True
+    except Exception as e:  # noqa: BLE001
+        log.warning(f" xGMI self-test raised: {e}")
+        return False
+
+
+def _graph_time_us(fn, iters: int = 32, reps: int = 5) -> float:
+    """Per-call time of ``fn`` (a collective) captured ``iters`` times into one hipGraph."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        g.replay()
+        torch.cuda.synchronize()
+        best = min(best, (time.perf_counter() - t0) / iters * 1e6)
+    return best
+
+
+def autotune_comm(tp: TPGroup, nbytes: int = 16384) -> None:
+    """Graph-time the decode all-reduce (B=1 x 8192 bf16) on both paths, max over ranks; keep
+    xGMI only if it is faster.  Results land in ``tp.comm_info`` (bench.py reports them)."""
+    dev = torch.cuda.current_device()
+    x = torch.ones(nbytes // 2, dtype=torch.bfloat16, device=dev)
+    xg, rc = tp.xgmi, tp.rccl
+    dist.barrier(group=tp.group)
+    t_x = _graph_time_us(lambda: xg.all_reduce_bf16(x.data_ptr(), x.data_ptr(), nbytes, -1))
+    dist.barrier(group=tp.group)
+    t_r = _graph_time_us(lambda: rc.all_reduce(x.data_ptr(), x.data_ptr(), nbytes // 2, 0, 0, -1))
+    ts = torch.tensor([t_x, t_r], dtype=torch.float64, device=dev)
+    dist.all_reduce(ts, op=dist.ReduceOp.MAX, group=tp.group)
+    t_x, t_r = float(ts[0]), float(ts[1])
+    ok = xg.error() == 0
+    tp.comm_info.update({"allreduce_bytes": nbytes, "xgmi_allreduce_us": round(t_x, 2),
+                         "rccl_allreduce_us": round(t_r, 2)})
+    if not _agree(tp, ok) or t_x >= t_r:
+        tp.xgmi = None
+    log.info(f" TP all-reduce {nbytes} B: xGMI one-shot {t_x:.1f} us, RCCL {t_r:.1f} us -> "
+             f"{'xGMI' if tp.xgmi is not None else 'RCCL'}")
