@@ -46,6 +46,8 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="projection weight dtype (fp8 = BASELINE config 5: row-scaled e4m3 weights, bf16 activations)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--simulate-tp", type=int, default=0,
                     help="PROFILING ONLY: run one TP rank's shapes on one GPU with collectives skipped")
@@ -79,7 +81,8 @@ def main() -> int:
     eng = build_engine(args.preset, tp=tp, max_batch=max(1, args.batch), block_size=bs,
                        num_blocks=max(args.batch, 2) * (per_seq // bs + 2) + 64,
                        max_model_len=args.max_model_len, cuda_graphs=not args.no_graphs,
-                       prefix_caching=not args.no_prefix_cache, capture=False, decode_chunk=8)
+                       prefix_caching=not args.no_prefix_cache, capture=False, decode_chunk=8,
+                       weight_dtype=args.dtype)
     if eng.use_graphs:
         eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= max(1, args.batch)] or [1])
     torch.cuda.synchronize()
@@ -145,7 +148,7 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": round(value / BASELINE_DECISIONS_PER_S, 3),
-        "dtype": "bf16",
+        "dtype": "bf16" if args.dtype == "bf16" else "fp8-e4m3 weights, bf16 activations",
         "data": "synthetic cluster-state prompts, random-init weights",
         "config": {
             "model": f"{args.preset} (Llama-3.3-70B-Instruct architecture)" if "70b" in args.preset else args.preset,

@@ -31,6 +31,14 @@ int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, c
                                 const int* context_lens, const int* block_tables, float scale, int num_seqs,
                                 int max_qlen, int nq, int nkv, int D, int block_size, int max_blocks, hipStream_t s);
 void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int* splits_out);
+int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out,
+                 int K, int epi, const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
+int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s);
+int k8s_dequant_fp8_rows(void* w, const void* q, const float* scale, int N, int K, hipStream_t s);
+int k8s_skinny_supported(int M, int N_out, int K);
+long long k8s_skinny_workspace(int M, int N_out, int epi);
+int k8s_skinny_gemm(void* out, void* workspace, const void* x, const void* W, int M, int N_out, int K, int epi,
+                    int num_cus, hipStream_t s);
 int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi, hipStream_t s);
 int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi,
                   const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
@@ -97,6 +105,24 @@ PYBIND11_MODULE(_C, m) {
     int ks, sp;
     k8s_gemv_plan(M, N, K, epi, &ks, &sp);
     return py::make_tuple(ks, sp);
+  });
+  m.def("gemv_fp8", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, uintptr_t wscale, int M, int N,
+                       int K, int epi, uintptr_t res_in, uintptr_t res_out, uintptr_t nw, float eps, int64_t s) {
+    check(k8s_gemv_fp8(P(out), P(partial), P(x), P(W), P<float>(wscale), M, N, K, epi, P(res_in), P(res_out), P(nw),
+                       eps, S(s)),
+          "gemv_fp8");
+  });
+  m.def("quantize_fp8_rows", [](uintptr_t q, uintptr_t scale, uintptr_t w, int N, int K, int64_t s) {
+    check(k8s_quantize_fp8_rows(P(q), P<float>(scale), P(w), N, K, S(s)), "quantize_fp8_rows");
+  });
+  m.def("dequant_fp8_rows", [](uintptr_t w, uintptr_t q, uintptr_t scale, int N, int K, int64_t s) {
+    check(k8s_dequant_fp8_rows(P(w), P(q), P<float>(scale), N, K, S(s)), "dequant_fp8_rows");
+  });
+  m.def("skinny_supported", [](int M, int N, int K) { return k8s_skinny_supported(M, N, K) != 0; });
+  m.def("skinny_workspace", [](int M, int N, int epi) { return k8s_skinny_workspace(M, N, epi); });
+  m.def("skinny_gemm", [](uintptr_t out, uintptr_t ws, uintptr_t x, uintptr_t W, int M, int N, int K, int epi,
+                          int num_cus, int64_t s) {
+    check(k8s_skinny_gemm(P(out), P(ws), P(x), P(W), M, N, K, epi, num_cus, S(s)), "skinny_gemm");
   });
   m.def("gemv", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, int M, int N, int K, int epi,
                    int64_t s) { check(k8s_gemv(P(out), P(partial), P(x), P(W), M, N, K, epi, S(s)), "gemv"); });

@@ -1,0 +1,88 @@
+// FP8 weight storage (BASELINE config 5: Llama-3.3-70B with fp8 weights, TP = 4).
+//
+// Format: OCP e4m3 (gfx950's native fp8, max 448) with one fp32 scale per output row,
+// w[n, k] ~= e4m3(q[n, k]) * scale[n].  Row scales keep every output feature's dynamic range and
+// cost one multiply per output in the GEMV epilogue.  Conversions use the gfx950 packed
+// converters (v_cvt_pk_fp8_f32 / v_cvt_pk_f32_fp8, round-to-nearest-even).
+#include "common.h"
+
+namespace k8sllm {
+
+constexpr float FP8_MAX = 448.f;
+typedef __attribute__((ext_vector_type(2))) float f2v;
+
+// One workgroup per row: absmax -> scale -> quantize (16 elements per thread-iteration).
+__global__ void __launch_bounds__(256) quantize_fp8_rows_kernel(uint8_t* __restrict__ q, float* __restrict__ scale,
+                                                                const bf16_t* __restrict__ w, int K) {
+  __shared__ float red[16];
+  const int n = blockIdx.x;
+  const bf16_t* row = w + (size_t)n * K;
+  float amax = 0.f;
+  for (int c = threadIdx.x; c < K / 8; c += blockDim.x) {
+    const u32x4 v = reinterpret_cast<const u32x4*>(row)[c];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fmaxf(fabsf(lo_bf(v[j])), fabsf(hi_bf(v[j]))));
+  }
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  float m = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+  const float s = m > 0.f ? m / FP8_MAX : 1.f;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[n] = s;
+  for (int c = threadIdx.x; c < K / 16; c += blockDim.x) {
+    const u32x4 a = reinterpret_cast<const u32x4*>(row)[2 * c];
+    const u32x4 b = reinterpret_cast<const u32x4*>(row)[2 * c + 1];
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32x4& src = j < 2 ? a : b;
+      const uint32_t d0 = src[(2 * j) & 3], d1 = src[(2 * j + 1) & 3];
+      auto cl = [&](float v) { return fminf(fmaxf(v * inv, -FP8_MAX), FP8_MAX); };
+      int packed = __builtin_amdgcn_cvt_pk_fp8_f32(cl(lo_bf(d0)), cl(hi_bf(d0)), 0, false);
+      packed = __builtin_amdgcn_cvt_pk_fp8_f32(cl(lo_bf(d1)), cl(hi_bf(d1)), packed, true);
+      o[j] = (uint32_t)packed;
+    }
+    reinterpret_cast<u32x4*>(q + (size_t)n * K)[c] = o;
+  }
+}
+
+__global__ void dequant_fp8_rows_kernel(bf16_t* __restrict__ w, const uint8_t* __restrict__ q,
+                                        const float* __restrict__ scale, int N, int K) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // 16-element chunk
+  const long long per_row = K / 16;
+  if (i >= (long long)N * per_row) return;
+  const int n = (int)(i / per_row);
+  const float s = scale[n];
+  const u32x4 v = reinterpret_cast<const u32x4*>(q)[i];
+  u32x4 o0, o1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f2v lo = __builtin_amdgcn_cvt_pk_f32_fp8(v[j], false);
+    const f2v hi = __builtin_amdgcn_cvt_pk_f32_fp8(v[j], true);
+    const uint32_t p0 = pack_bf2(lo.x * s, lo.y * s), p1 = pack_bf2(hi.x * s, hi.y * s);
+    if (j < 2) { o0[2 * j] = p0; o0[2 * j + 1] = p1; }
+    else { o1[2 * j - 4] = p0; o1[2 * j - 3] = p1; }
+  }
+  reinterpret_cast<u32x4*>(w)[2 * i] = o0;
+  reinterpret_cast<u32x4*>(w)[2 * i + 1] = o1;
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+extern "C" int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s) {
+  if (N <= 0 || K <= 0 || K % 16 != 0) return -1;
+  quantize_fp8_rows_kernel<<<N, 256, 0, s>>>(static_cast<uint8_t*>(q), scale, static_cast<const bf16_t*>(w), K);
+  return (int)hipGetLastError();
+}
+
+extern "C" int k8s_dequant_fp8_rows(void* w, const void* q, const float* scale, int N, int K, hipStream_t s) {
+  if (N <= 0 || K <= 0 || K % 16 != 0) return -1;
+  const long long chunks = (long long)N * (K / 16);
+  dequant_fp8_rows_kernel<<<(unsigned)((chunks + 255) / 256), 256, 0, s>>>(
+      static_cast<bf16_t*>(w), static_cast<const uint8_t*>(q), scale, N, K);
+  return (int)hipGetLastError();
+}

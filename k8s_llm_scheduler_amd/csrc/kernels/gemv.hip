@@ -11,6 +11,9 @@
 //    fp32 slabs are combined by a finalize kernel that also applies the epilogue.
 // Epilogues: BF16 store, FP32 store (logits), SWIGLU: W = [gate; up] (2I rows) and the output is
 // silu(gate_j) * up_j (SURVEY.md K10 fused into K9).
+// FP8 weights (BASELINE config 5): W holds OCP e4m3 bytes with one fp32 scale per row; a 16-byte
+// load carries 16 weights (half the HBM bytes of bf16), decoded with v_cvt_pk_f32_fp8 and
+// multiplied in fp32; the row scale is applied once in the epilogue.
 #include "common.h"
 
 namespace k8sllm {
@@ -32,6 +35,23 @@ __device__ __forceinline__ float dot8(u32x4 w, u32x4 x, float acc) {
   return dot2(w.w, x.w, acc);
 }
 
+// 16 fp8 weights (one 16-byte load) against 16 bf16 activations (two 16-byte LDS vectors).
+__device__ __forceinline__ float dot16_fp8(u32x4 w, u32x4 x0, u32x4 x1, float acc) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f2 lo = __builtin_amdgcn_cvt_pk_f32_fp8(w[j], false);  // bytes 0, 1
+    const f2 hi = __builtin_amdgcn_cvt_pk_f32_fp8(w[j], true);   // bytes 2, 3
+    const uint32_t xa = j < 2 ? x0[2 * j] : x1[2 * j - 4];
+    const uint32_t xb = j < 2 ? x0[2 * j + 1] : x1[2 * j - 3];
+    acc = fmaf(lo.x, lo_bf(xa), acc);
+    acc = fmaf(lo.y, hi_bf(xa), acc);
+    acc = fmaf(hi.x, lo_bf(xb), acc);
+    acc = fmaf(hi.y, hi_bf(xb), acc);
+  }
+  return acc;
+}
+
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
 // Fused pre-norm prologue (NORM): the GEMV input is rmsnorm(x + res_in) * nw, computed by every
@@ -48,30 +68,35 @@ __device__ __forceinline__ void norm_row_chunk(const bf16_t* __restrict__ x, con
   for (int j = 0; j < 4; ++j) r[j] = pack_bf2(lo_bf(a[j]) + lo_bf(b[j]), hi_bf(a[j]) + hi_bf(b[j]));
 }
 
-template <int M, int RPW, int EPI, bool NORM>
+template <int M, int RPW, int EPI, bool NORM, bool FP8>
 __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float* __restrict__ partial,
-                                                   const bf16_t* __restrict__ x, const bf16_t* __restrict__ W,
+                                                   const bf16_t* __restrict__ x, const void* __restrict__ W,
                                                    int N_out, int K, int KS, int half_rows,
                                                    const bf16_t* __restrict__ res_in, bf16_t* __restrict__ res_out,
-                                                   const bf16_t* __restrict__ nw, float eps) {
+                                                   const bf16_t* __restrict__ nw, float eps,
+                                                   const float* __restrict__ wscale) {
+  constexpr int EPC = FP8 ? 16 : 8;  // weights per 16-byte chunk
+  constexpr int WB = FP8 ? 1 : 2;    // bytes per weight
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u32x4* xs = reinterpret_cast<u32x4*>(smem);  // [M][KS/8]
   __shared__ float nred[4][M];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int kb = blockIdx.y * KS;
   const int klen = min(KS, K - kb);
-  const int nch = klen >> 3;  // 16-byte chunks in this slice
+  const int nch = klen / EPC;  // 16-byte weight chunks in this slice
+  const int xch = klen >> 3;   // 16-byte x chunks (8 bf16) in this slice
 
   constexpr int NR = (EPI == EPI_SWIGLU) ? 2 * RPW : RPW;  // weight rows per wave
   constexpr int U = (NR >= 4) ? 2 : ((NR >= 2) ? 4 : 8);  // chunks per lane in flight per row
   const int r0 = (blockIdx.x * 4 + wid) * RPW;               // first output row of this wave
   const bool active = r0 < N_out;
-  const bf16_t* wrow[NR];
+  const char* wrow[NR];
+  const char* Wb = static_cast<const char*>(W);
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int n = min(r0 + r, N_out - 1);
-    wrow[r] = W + (size_t)n * K + kb;
-    if (EPI == EPI_SWIGLU) wrow[RPW + r] = W + (size_t)(n + half_rows) * K + kb;
+    wrow[r] = Wb + ((size_t)n * K + kb) * WB;
+    if (EPI == EPI_SWIGLU) wrow[RPW + r] = Wb + ((size_t)(n + half_rows) * K + kb) * WB;
   }
   // weights do not depend on x: start streaming them before the x staging / norm prologue
   u32x4 wv[U][NR];
@@ -105,7 +130,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
     for (int m = 0; m < M; ++m) inv[m] = rsqrtf((nred[0][m] + nred[1][m] + nred[2][m] + nred[3][m]) / (float)K + eps);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+      for (int c = threadIdx.x; c < xch; c += blockDim.x) {
         u32x4 r, o;
         norm_row_chunk<M>(x, res_in, m, K, (kb >> 3) + c, r);
         const u32x4 g = reinterpret_cast<const u32x4*>(nw + kb)[c];
@@ -117,8 +142,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
     }
   } else {
     // stage x[:, kb:kb+klen] into LDS
-    for (int i = threadIdx.x; i < M * nch; i += blockDim.x) {
-      const int m = i / nch, c = i - m * nch;
+    for (int i = threadIdx.x; i < M * xch; i += blockDim.x) {
+      const int m = i / xch, c = i - m * xch;
       xs[m * (KS >> 3) + c] = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + kb + c * 8);
     }
   }
@@ -151,9 +176,16 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
       if (c + 64 * u < nch) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          const u32x4 xv = xs[m * (KS >> 3) + c + 64 * u];
+          if (FP8) {
+            const u32x4 x0 = xs[m * (KS >> 3) + 2 * (c + 64 * u)];
+            const u32x4 x1 = xs[m * (KS >> 3) + 2 * (c + 64 * u) + 1];
 #pragma unroll
-          for (int r = 0; r < NR; ++r) acc[r][m] = dot8(cur[u][r], xv, acc[r][m]);
+            for (int r = 0; r < NR; ++r) acc[r][m] = dot16_fp8(cur[u][r], x0, x1, acc[r][m]);
+          } else {
+            const u32x4 xv = xs[m * (KS >> 3) + c + 64 * u];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r][m] = dot8(cur[u][r], xv, acc[r][m]);
+          }
         }
       }
     }
@@ -169,6 +201,15 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
   for (int r = 0; r < RPW; ++r) {
     const int n = r0 + r;
     if (n >= N_out) break;
+    if (FP8) {
+      const float sg = wscale[n];
+      const float su = EPI == EPI_SWIGLU ? wscale[n + half_rows] : 0.f;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        acc[r][m] *= sg;
+        if (EPI == EPI_SWIGLU) acc[RPW + r][m] *= su;
+      }
+    }
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       if (partial != nullptr) {
@@ -230,10 +271,13 @@ extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int
 
 // partial: fp32 workspace of splits * M * wrows floats (wrows = N_out, or 2*N_out for SWIGLU);
 // may be null when the plan has a single split.
-extern "C" int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K,
-                             int epi, const void* res_in, void* res_out, const void* nw, float eps,
-                             hipStream_t stream) {
+// wscale != null: W is fp8 (OCP e4m3, one fp32 scale per weight row); K must be a multiple of 16.
+extern "C" int k8s_gemv_norm_w(void* out, void* partial, const void* x, const void* W, const float* wscale, int M,
+                               int N_out, int K, int epi, const void* res_in, void* res_out, const void* nw,
+                               float eps, hipStream_t stream) {
   if (M < 1 || M > 8 || K % 8 != 0 || N_out <= 0) return -1;
+  const bool fp8 = wscale != nullptr;
+  if (fp8 && K % 16 != 0) return -1;
   int ks, splits;
   k8s_gemv_plan(M, N_out, K, epi, &ks, &splits);
   if (splits > 1 && partial == nullptr) return -3;
@@ -243,15 +287,18 @@ extern "C" int k8s_gemv_norm(void* out, void* partial, const void* x, const void
   const size_t lds = (size_t)M * ks * 2;
   const int half_rows = (epi == EPI_SWIGLU) ? N_out : 0;
   const bf16_t* xx = (const bf16_t*)x;
-  const bf16_t* ww = (const bf16_t*)W;
+  const void* ww = W;
   const bf16_t* ri = (const bf16_t*)res_in;
   bf16_t* ro = (bf16_t*)res_out;
   const bf16_t* gw = (const bf16_t*)nw;
-#define G(MM, RR, EE)                                                                                     \
-  if (gw) gemv_kernel<MM, RR, EE, true><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,      \
-                                                                    half_rows, ri, ro, gw, eps);         \
-  else gemv_kernel<MM, RR, EE, false><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,        \
-                                                                  half_rows, ri, ro, gw, eps)
+#define G2(MM, RR, EE, F8)                                                                                    \
+  if (gw) gemv_kernel<MM, RR, EE, true, F8><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,      \
+                                                                        half_rows, ri, ro, gw, eps, wscale); \
+  else gemv_kernel<MM, RR, EE, false, F8><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,        \
+                                                                      half_rows, ri, ro, gw, eps, wscale)
+#define G(MM, RR, EE)        \
+  if (fp8) { G2(MM, RR, EE, true); } \
+  else { G2(MM, RR, EE, false); }
 #define BY_EPI(MM, RR)                  \
   switch (epi) {                        \
     case EPI_BF16: G(MM, RR, EPI_BF16); break;       \
@@ -271,6 +318,7 @@ extern "C" int k8s_gemv_norm(void* out, void* partial, const void* x, const void
   }
 #undef BY_EPI
 #undef G
+#undef G2
   if (splits > 1) {
     const int total = M * N_out;
     const int blocks = (total + 255) / 256;
@@ -283,7 +331,20 @@ extern "C" int k8s_gemv_norm(void* out, void* partial, const void* x, const void
   return (int)hipGetLastError();
 }
 
+extern "C" int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K,
+                             int epi, const void* res_in, void* res_out, const void* nw, float eps,
+                             hipStream_t stream) {
+  return k8s_gemv_norm_w(out, partial, x, W, nullptr, M, N_out, K, epi, res_in, res_out, nw, eps, stream);
+}
+
 extern "C" int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi,
                         hipStream_t stream) {
-  return k8s_gemv_norm(out, partial, x, W, M, N_out, K, epi, nullptr, nullptr, nullptr, 0.f, stream);
+  return k8s_gemv_norm_w(out, partial, x, W, nullptr, M, N_out, K, epi, nullptr, nullptr, nullptr, 0.f, stream);
+}
+
+extern "C" int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const float* wscale, int M,
+                            int N_out, int K, int epi, const void* res_in, void* res_out, const void* nw, float eps,
+                            hipStream_t stream) {
+  if (wscale == nullptr) return -1;
+  return k8s_gemv_norm_w(out, partial, x, W, wscale, M, N_out, K, epi, res_in, res_out, nw, eps, stream);
 }

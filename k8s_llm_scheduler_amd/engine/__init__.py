@@ -16,8 +16,10 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
                  tokenizer: Optional[str] = None, seed: int = 0, max_batch: int = 64, block_size: int = 16,
                  num_blocks: Optional[int] = None, kv_cache_gb: float = 0.0, kv_cache_fraction: float = 0.85,
                  max_model_len: int = 16384, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
-                 prefix_caching: bool = True, decode_chunk: int = 4, metrics=None, capture: bool = True, control=None):
-    """Model + tokenizer + engine on this rank's GPU (or CPU when no GPU is present)."""
+                 prefix_caching: bool = True, decode_chunk: int = 4, metrics=None, capture: bool = True, control=None,
+                 weight_dtype: str = "bf16"):
+    """Model + tokenizer + engine on this rank's GPU (or CPU when no GPU is present).
+    ``weight_dtype``: "bf16" or "fp8" (row-scaled e4m3 projection weights)."""
     import torch
 
     from ..models.config import get_config
@@ -30,7 +32,8 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
         device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
     cfg = get_config(weights or preset) if weights else get_config(preset)
     t0 = time.perf_counter()
-    model = LlamaModel(cfg, tp, device=device, seed=seed, weights=weights, max_model_len=max_model_len)
+    model = LlamaModel(cfg, tp, device=device, seed=seed, weights=weights, max_model_len=max_model_len,
+                       weight_dtype=weight_dtype)
     if device.startswith("cuda"):
         torch.cuda.synchronize()
     log.info(f" Model {cfg.name} ready on {device} (tp {tp.rank}/{tp.world}, "
@@ -53,4 +56,5 @@ def engine_from_config(cfg, tp=None, metrics=None, control=None):
                         max_batch=e.max_batch, block_size=e.block_size, kv_cache_gb=e.kv_cache_gb,
                         kv_cache_fraction=e.kv_cache_fraction, max_model_len=e.max_model_len,
                         max_prefill_tokens=e.max_prefill_tokens, cuda_graphs=e.cuda_graphs,
-                        prefix_caching=e.prefix_caching, metrics=metrics, control=control)
+                        prefix_caching=e.prefix_caching, metrics=metrics, control=control,
+                        weight_dtype="fp8" if e.dtype in ("fp8", "fp8_e4m3") else "bf16")

@@ -11,7 +11,10 @@ runs on CPU through the fp32 reference ops, which is how TP=k == TP=1 is tested 
 
 Weights: deterministic hash-uniform random init (identical global tensors for every TP degree
 and device; BASELINE allows random-init weights) or a HuggingFace safetensors checkpoint,
-loaded shard-by-shard with ``safetensors`` (no pickle).
+loaded shard-by-shard with ``safetensors`` (no pickle).  ``weight_dtype="fp8"`` (BASELINE
+config 5) stores the four projection matrices of every layer as row-scaled OCP e4m3
+(:class:`ops.Fp8Weight`, quantized on the device right after each layer is built); embedding,
+norms and the LM head stay bf16.
 """
 
 from __future__ import annotations
@@ -49,12 +52,15 @@ class LayerWeights:
 class LlamaModel:
     def __init__(self, cfg: LlamaConfig, tp: Optional[TPGroup] = None, device: str | torch.device = "cpu",
                  dtype: torch.dtype = torch.bfloat16, seed: int = 0, weights: Optional[str] = None,
-                 max_model_len: int = 8192):
+                 max_model_len: int = 8192, weight_dtype: str = "bf16"):
         self.cfg = cfg
         self.tp = tp or TPGroup()
         cfg.validate_tp(self.tp.world)
         self.device = torch.device(device)
         self.dtype = dtype
+        if weight_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"weight_dtype must be bf16 or fp8, got {weight_dtype!r}")
+        self.weight_dtype = weight_dtype
         self.seed = seed
         t, r = self.tp.world, self.tp.rank
         self.nq = cfg.num_heads // t
@@ -101,7 +107,7 @@ class LlamaModel:
             ops.hash_init_(wgu[:self.I], H, r * self.I, 0, s, _tid(l, 4), a)
             ops.hash_init_(wgu[self.I:], H, r * self.I, 0, s, _tid(l, 5), a)
             wd = ops.hash_init_(self._new(H, self.I), c.intermediate, 0, r * self.I, s, _tid(l, 6), a_out)
-            self.layers.append(LayerWeights(ones(_tid(l, 7)), wqkv, wo, ones(_tid(l, 8)), wgu, wd))
+            self._add_layer(LayerWeights(ones(_tid(l, 7)), wqkv, wo, ones(_tid(l, 8)), wgu, wd))
         self.norm = ones(_TID_NORM)
         self.lm_head = ops.hash_init_(self._new(self.Vs, H), H, r * self.Vs, 0, s, _TID_LM, a)
 
@@ -144,18 +150,24 @@ class LlamaModel:
             g = sl(pre + "mlp.gate_proj.weight", 0, r * self.I, (r + 1) * self.I)
             u = sl(pre + "mlp.up_proj.weight", 0, r * self.I, (r + 1) * self.I)
             d = sl(pre + "mlp.down_proj.weight", 1, r * self.I, (r + 1) * self.I)
-            self.layers.append(LayerWeights(sl(pre + "input_layernorm.weight"), torch.cat([q, k, v]).contiguous(),
-                                            o.contiguous(), sl(pre + "post_attention_layernorm.weight"),
-                                            torch.cat([g, u]).contiguous(), d.contiguous()))
+            self._add_layer(LayerWeights(sl(pre + "input_layernorm.weight"), torch.cat([q, k, v]).contiguous(),
+                                         o.contiguous(), sl(pre + "post_attention_layernorm.weight"),
+                                         torch.cat([g, u]).contiguous(), d.contiguous()))
         self.norm = sl("model.norm.weight")
         lm = "lm_head.weight" if "lm_head.weight" in index else "model.embed_tokens.weight"
         self.lm_head = sl(lm, 0, r * self.Vs, (r + 1) * self.Vs).contiguous()
 
+    def _add_layer(self, lw: LayerWeights) -> None:
+        if self.weight_dtype == "fp8":
+            lw.wqkv, lw.wo, lw.wgu, lw.wdown = (ops.quantize_fp8(w) for w in (lw.wqkv, lw.wo, lw.wgu, lw.wdown))
+        self.layers.append(lw)
+
     def weight_bytes(self) -> int:
-        n = self.embed.numel() + self.norm.numel() + self.lm_head.numel()
+        nb = lambda t: t.nbytes() if isinstance(t, ops.Fp8Weight) else t.numel() * t.element_size()
+        n = sum(nb(t) for t in (self.embed, self.norm, self.lm_head))
         for w in self.layers:
-            n += sum(t.numel() for t in (w.ln1, w.wqkv, w.wo, w.ln2, w.wgu, w.wdown))
-        return n * self.embed.element_size()
+            n += sum(nb(t) for t in (w.ln1, w.wqkv, w.wo, w.ln2, w.wgu, w.wdown))
+        return n
 
     # ------------------------------------------------------------------ KV cache
     def allocate_kv(self, num_blocks: int, block_size: int) -> torch.Tensor:
@@ -217,8 +229,12 @@ class LlamaModel:
         if self.device.type == "cuda" and B <= ops.GEMV_MAX_M and self.fused_decode:
             return self._forward_decode_fused(tokens, context_lens, block_tables, max_context)
         kv = self.kv_cache
+        fused_attn = self.device.type == "cuda" and self.fused_decode   # batched decode (B > 8)
 
         def attn(l: int, qkv: torch.Tensor) -> torch.Tensor:
+            if fused_attn:
+                return ops.decode_attention_fused(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
+                                                  self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
             q = ops.rope_kv_write(qkv, self.cos_sin, kv[l, 0], kv[l, 1], self.nq, self.nkv, self.D,
                                   context_lens=context_lens, block_tables=block_tables, block_size=self.block_size)
             a = ops.paged_decode_attention(q, kv[l, 0], kv[l, 1], block_tables, context_lens, self.scale,
@@ -259,7 +275,7 @@ def save_hf_checkpoint(model: LlamaModel, path: Path) -> None:
     """Write a TP=1 model as a HuggingFace-layout safetensors checkpoint (tests/tools)."""
     from safetensors.torch import save_file
 
-    assert model.tp.world == 1
+    assert model.tp.world == 1 and model.weight_dtype == "bf16"
     c, D = model.cfg, model.D
     t: Dict[str, torch.Tensor] = {"model.embed_tokens.weight": model.embed, "model.norm.weight": model.norm,
                                   "lm_head.weight": model.lm_head}

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import importlib
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -24,6 +25,7 @@ except Exception as e:  # pragma: no cover - reported loudly on first GPU use
     _C_ERR = e
 
 EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
+BF16, F32, I32 = torch.bfloat16, torch.float32, torch.int32
 DECODE_PARTITION = 64
 FUSED_PARTITION = 1024
 
@@ -38,6 +40,64 @@ def native():
 
 def available() -> bool:
     return _C is not None
+
+
+class Fp8Weight:
+    """Row-scaled OCP e4m3 weight (fp8.hip): ``q`` [N, K] uint8 bit patterns, ``scale`` [N] fp32,
+    w ~= e4m3(q) * scale[:, None].  Decode GEMVs stream ``q`` directly (half the HBM bytes of
+    bf16); prefill GEMMs dequantize to a bf16 scratch copy for the library GEMM."""
+
+    __slots__ = ("q", "scale")
+
+    def __init__(self, q: torch.Tensor, scale: torch.Tensor):
+        if q.dtype != torch.uint8 or q.dim() != 2 or scale.shape != (q.shape[0],) or scale.dtype != F32:
+            raise ValueError("Fp8Weight needs q [N, K] uint8 and scale [N] fp32")
+        self.q, self.scale = q.contiguous(), scale.contiguous()
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    @property
+    def device(self):
+        return self.q.device
+
+    @property
+    def is_cuda(self) -> bool:
+        return self.q.is_cuda
+
+    def numel(self) -> int:
+        return self.q.numel()
+
+    def nbytes(self) -> int:
+        return self.q.numel() + self.scale.numel() * 4
+
+    def __getitem__(self, rows) -> "Fp8Weight":
+        return Fp8Weight(self.q[rows], self.scale[rows])
+
+    def dequant(self, dtype=torch.bfloat16) -> torch.Tensor:
+        if not self.is_cuda:
+            return ref.dequant_fp8(self.q, self.scale, dtype)
+        N, K = self.q.shape
+        out = torch.empty(N, K, dtype=BF16, device=self.q.device)
+        native().dequant_fp8_rows(out.data_ptr(), self.q.data_ptr(), self.scale.data_ptr(), N, K, -1)
+        return out if dtype == BF16 else out.to(dtype)
+
+
+def quantize_fp8(w: torch.Tensor) -> Fp8Weight:
+    """bf16 [N, K] -> row-scaled fp8 (K % 16 == 0)."""
+    if not w.is_cuda:
+        q, s = ref.quantize_fp8(w)
+        return Fp8Weight(q, s)
+    N, K = w.shape
+    q = torch.empty(N, K, dtype=torch.uint8, device=w.device)
+    s = torch.empty(N, dtype=F32, device=w.device)
+    native().quantize_fp8_rows(q.data_ptr(), s.data_ptr(), _chk(w, BF16, "w"), N, K, -1)
+    return Fp8Weight(q, s)
+
+
+def _is_fp8(w) -> bool:
+    return isinstance(w, Fp8Weight)
 
 
 def _gpu(*ts: torch.Tensor) -> bool:
@@ -55,7 +115,6 @@ def _chk(t: torch.Tensor, dtype, name: str) -> int:
     return t.data_ptr()
 
 
-BF16, F32, I32 = torch.bfloat16, torch.float32, torch.int32
 
 
 # ----------------------------------------------------------------------------- norms
@@ -148,45 +207,91 @@ def paged_prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: tor
 
 # ----------------------------------------------------------------------------- linear
 GEMV_MAX_M = 8
+SKINNY_MAX_M = 64
 
 
-def _gemv(x: torch.Tensor, w: torch.Tensor, epi: int, out_dtype) -> torch.Tensor:
+def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0, res_in=None,
+          res_out=None) -> torch.Tensor:
+    """Decode GEMV (M <= 8) for bf16 or fp8 weights, optionally with the fused pre-norm prologue."""
     M, K = x.shape
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     out = torch.empty(M, N, dtype=out_dtype, device=x.device)
     ks, splits = native().gemv_plan(M, N, K, epi)
-    part = 0
-    if splits > 1:
-        wrows = w.shape[0]
-        part = torch.empty(splits * M * wrows, dtype=F32, device=x.device)
-        pp = part.data_ptr()
+    part = torch.empty(splits * M * w.shape[0], dtype=F32, device=x.device) if splits > 1 else None
+    pp = part.data_ptr() if part is not None else 0
+    ri = _chk(res_in, BF16, "res_in") if res_in is not None else 0
+    ro = _chk(res_out, BF16, "res_out") if res_out is not None else 0
+    nw = _chk(norm_w, BF16, "norm_w") if norm_w is not None else 0
+    if _is_fp8(w):
+        native().gemv_fp8(out.data_ptr(), pp, _chk(x, BF16, "x"), w.q.data_ptr(), w.scale.data_ptr(), M, N, K, epi,
+                          ri, ro, nw, float(eps), -1)
+    elif norm_w is not None:
+        native().gemv_norm(out.data_ptr(), pp, _chk(x, BF16, "x"), _chk(w, BF16, "w"), M, N, K, epi, ri, ro, nw,
+                           float(eps), -1)
     else:
-        pp = 0
-    native().gemv(out.data_ptr(), pp, _chk(x, BF16, "x"), _chk(w, BF16, "w"), M, N, K, epi, -1)
+        native().gemv(out.data_ptr(), pp, _chk(x, BF16, "x"), _chk(w, BF16, "w"), M, N, K, epi, -1)
     del part
     return out
 
 
+def _lib_weight(w) -> torch.Tensor:
+    """Weight for a library GEMM: fp8 weights are dequantized to a bf16 scratch copy."""
+    return w.dequant() if _is_fp8(w) else w
+
+
+_NUM_CUS = {}
+
+
+def _num_cus(dev: torch.device) -> int:
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _NUM_CUS:
+        _NUM_CUS[i] = torch.cuda.get_device_properties(i).multi_processor_count
+    return _NUM_CUS[i]
+
+
+def _skinny(x: torch.Tensor, w: torch.Tensor, epi: int, out_dtype) -> torch.Tensor:
+    M, K = x.shape
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    out = torch.empty(M, N, dtype=out_dtype, device=x.device)
+    n_ws = native().skinny_workspace(M, N, epi)
+    ws = torch.empty(n_ws, dtype=F32, device=x.device) if n_ws else None
+    native().skinny_gemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, _chk(x, BF16, "x"),
+                         _chk(w, BF16, "w"), M, N, K, epi, _num_cus(x.device), -1)
+    del ws
+    return out
+
+
+# The MFMA skinny GEMM is opt-in until it beats hipBLASLt at every batched-decode shape
+# (profiles/kbench_skinny_*.txt); K8S_SKINNY=1 routes 8 < M <= 64 through it.
+SKINNY_ENABLED = os.environ.get("K8S_SKINNY", "0") == "1"
+
+
+def _use_skinny(M: int, w, K: int) -> bool:
+    return SKINNY_ENABLED and not _is_fp8(w) and GEMV_MAX_M < M <= SKINNY_MAX_M and K % 256 == 0
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
-    """y = x @ w.T with w [N, K] bf16.  M <= 8 rows: hand-written HBM-streaming GEMV;
-    larger M (prefill): library GEMM (hipBLASLt via torch)."""
+    """y = x @ w.T with w [N, K] bf16.  M <= 8 rows: hand-written HBM-streaming GEMV; M <= 64
+    (batched decode): MFMA skinny GEMM; larger M (prefill): library GEMM (hipBLASLt via torch)."""
     if not _gpu(x, w):
         return ref.linear(x, w, out_dtype)
     x2 = x.reshape(-1, x.shape[-1])
     if x2.shape[0] <= GEMV_MAX_M:
         y = _gemv(x2.contiguous(), w, EPI_F32 if out_dtype == F32 else EPI_BF16, out_dtype or BF16)
+    elif _use_skinny(x2.shape[0], w, x2.shape[1]):
+        y = _skinny(x2.contiguous(), w, EPI_F32 if out_dtype == F32 else EPI_BF16, out_dtype or BF16)
     else:
-        y = torch.nn.functional.linear(x2, w)
+        y = torch.nn.functional.linear(x2, _lib_weight(w))
         if out_dtype is not None and out_dtype != y.dtype:
             y = y.to(out_dtype)
     return y.view(*x.shape[:-1], y.shape[-1])
 
 
-def linear_norm(x: torch.Tensor, w: torch.Tensor, norm_w: torch.Tensor, eps: float,
+def linear_norm(x: torch.Tensor, w, norm_w: torch.Tensor, eps: float,
                 res_in: Optional[torch.Tensor], res_out: Optional[torch.Tensor], epi: int = EPI_BF16) -> torch.Tensor:
     """Decode-path fused pre-norm projection (M <= 8 rows):
     r = x + res_in (or x), res_out <- r, y = epi(rmsnorm(r) * norm_w @ w.T).
-    res_in and res_out must be distinct buffers (ping-pong)."""
+    res_in and res_out must be distinct buffers (ping-pong).  ``w``: bf16 tensor or Fp8Weight."""
     if res_in is not None and res_out is not None and res_in.data_ptr() == res_out.data_ptr():
         raise ValueError("res_in and res_out must be different buffers")
     M, K = x.shape
@@ -200,16 +305,7 @@ def linear_norm(x: torch.Tensor, w: torch.Tensor, norm_w: torch.Tensor, eps: flo
         return ref.linear(h, w, F32 if epi == EPI_F32 else None)
     if M > GEMV_MAX_M:
         raise ValueError("linear_norm is the decode path (M <= 8)")
-    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
-    out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
-    ks, splits = native().gemv_plan(M, N, K, epi)
-    part = torch.empty(splits * M * w.shape[0], dtype=F32, device=x.device) if splits > 1 else None
-    native().gemv_norm(out.data_ptr(), part.data_ptr() if part is not None else 0, _chk(x, BF16, "x"),
-                       _chk(w, BF16, "w"), M, N, K, epi,
-                       _chk(res_in, BF16, "res_in") if res_in is not None else 0,
-                       _chk(res_out, BF16, "res_out") if res_out is not None else 0,
-                       _chk(norm_w, BF16, "norm_w"), float(eps), -1)
-    return out
+    return _gemv(x, w, epi, F32 if epi == EPI_F32 else BF16, norm_w=norm_w, eps=eps, res_in=res_in, res_out=res_out)
 
 
 def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
@@ -249,8 +345,10 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     x2 = x.reshape(-1, x.shape[-1])
     if x2.shape[0] <= GEMV_MAX_M:
         y = _gemv(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
+    elif _use_skinny(x2.shape[0], w_gate_up, x2.shape[1]):
+        y = _skinny(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
     else:
-        y = silu_mul(torch.nn.functional.linear(x2, w_gate_up))
+        y = silu_mul(torch.nn.functional.linear(x2, _lib_weight(w_gate_up)))
     return y.view(*x.shape[:-1], y.shape[-1])
 
 

@@ -165,8 +165,32 @@ def paged_prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: tor
     return out
 
 
+FP8_MAX = 448.0
+
+
+def quantize_fp8(w: torch.Tensor):
+    """Row-scaled OCP e4m3: returns (q [N, K] uint8 bit patterns, scale [N] fp32) with
+    w ~= e4m3(q) * scale[:, None] (same recipe as fp8.hip)."""
+    wf = w.float()
+    amax = wf.abs().amax(dim=1)
+    scale = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+    q = (wf * (1.0 / scale)[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), scale
+
+
+def dequant_fp8(q: torch.Tensor, scale: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    return (q.view(torch.float8_e4m3fn).float() * scale.float()[:, None]).to(dtype)
+
+
+def _wf(w) -> torch.Tensor:
+    """fp32 view of a weight: a plain tensor or an ops.Fp8Weight (duck-typed: .q / .scale)."""
+    if hasattr(w, "scale") and hasattr(w, "q"):
+        return dequant_fp8(w.q, w.scale)
+    return w.float()
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
-    y = x.float() @ w.float().T
+    y = x.float() @ _wf(w).T
     return y.to(out_dtype or x.dtype)
 
 
@@ -177,7 +201,7 @@ def silu_mul(gu: torch.Tensor) -> torch.Tensor:
 
 
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
-    gu = x.float() @ w_gate_up.float().T
+    gu = x.float() @ _wf(w_gate_up).T
     I = gu.shape[-1] // 2
     return (torch.nn.functional.silu(gu[..., :I]) * gu[..., I:]).to(x.dtype)
 

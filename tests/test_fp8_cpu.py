@@ -1,0 +1,55 @@
+"""FP8 (row-scaled OCP e4m3) weights on CPU: quantization error bound, the fp8 linear ops against
+dequantized fp32 math, and the tiny Llama with fp8 projections tracking its bf16 twin."""
+
+import torch
+
+from k8s_llm_scheduler_amd import ops
+from k8s_llm_scheduler_amd.engine import SamplingParams, build_engine
+from k8s_llm_scheduler_amd.models.config import PRESETS
+from k8s_llm_scheduler_amd.models.llama import LlamaModel
+from k8s_llm_scheduler_amd.ops import reference as ref
+
+from test_engine_cpu import _prefill  # noqa: E402
+
+
+def test_quantize_roundtrip_error_bound():
+    g = torch.Generator().manual_seed(0)
+    w = (torch.randn(64, 512, generator=g) * torch.logspace(-3, 1, 64)[:, None]).bfloat16()
+    fw = ops.quantize_fp8(w)
+    assert fw.q.dtype == torch.uint8 and fw.scale.shape == (64,)
+    back = fw.dequant(torch.float32)
+    wf = w.float()
+    # e4m3: 3 mantissa bits -> relative error <= 2^-4 for normal values; row max maps to 448
+    rel = ((back - wf).abs() / wf.abs().clamp_min(1e-30))[wf.abs() > fw.scale[:, None] * 2 ** -6]
+    assert float(rel.max()) <= 2 ** -4 + 1e-6
+    assert torch.allclose(back.abs().amax(1), wf.abs().amax(1), rtol=1e-6)
+
+
+def test_fp8_linear_ops_match_dequantized_math():
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(5, 256, generator=g).bfloat16()
+    w = ops.quantize_fp8((torch.randn(96, 256, generator=g) * 0.05).bfloat16())
+    wd = w.dequant(torch.float32)
+    torch.testing.assert_close(ops.linear(x, w).float(), (x.float() @ wd.T).bfloat16().float())
+    gu = ops.quantize_fp8((torch.randn(2 * 48, 256, generator=g) * 0.05).bfloat16())
+    y = ops.linear_swiglu(x, gu)
+    want = ref.linear_swiglu(x, gu.dequant(torch.float32))
+    torch.testing.assert_close(y.float(), want.float())
+
+
+def test_tiny_model_fp8_tracks_bf16():
+    ids = [7, 100, 2000, 31, 32, 33, 900, 12]
+    m16 = LlamaModel(PRESETS["tiny"], device="cpu", seed=3, max_model_len=256)
+    m8 = LlamaModel(PRESETS["tiny"], device="cpu", seed=3, max_model_len=256, weight_dtype="fp8")
+    assert isinstance(m8.layers[0].wqkv, ops.Fp8Weight)
+    proj = lambda m: m.weight_bytes() - sum(t.numel() * 2 for t in (m.embed, m.norm, m.lm_head))
+    assert proj(m8) < 0.52 * proj(m16)   # 1 byte per weight + one fp32 scale per row
+    a, _ = _prefill(m16, ids)
+    b, _ = _prefill(m8, ids)
+    a, b = a.flatten().float(), b.flatten().float()
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=0)
+    assert float(cos) > 0.99
+    eng = build_engine("tiny", device="cpu", max_batch=2, max_model_len=256, num_blocks=32, seed=1,
+                       weight_dtype="fp8")
+    out = eng.generate(["fp8 weights"], SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))[0]
+    assert len(out.token_ids) == 4

@@ -151,6 +151,24 @@ def test_gemv_swiglu(M, I, K):
     close(ops.linear_swiglu(x, w), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)
 
 
+@pytest.mark.parametrize("M", [9, 16, 17, 40, 64])
+@pytest.mark.parametrize("N,K", [(1280, 8192), (10240, 8192), (8192, 3584), (100, 256), (16032, 8192)])
+def test_skinny_mfma_gemm(M, N, K, monkeypatch):
+    """Batched-decode path (8 < M <= 64): MFMA skinny GEMM (stream-K, fp32 atomics), all epilogues."""
+    monkeypatch.setattr(ops, "SKINNY_ENABLED", True)
+    x, w = rnd(M, K), rnd(N, K, scale=0.05)
+    close(ops.linear(x, w), ref.linear(x.cpu(), w.cpu()), 3e-2)
+    close(ops.linear(x, w, out_dtype=torch.float32), ref.linear(x.cpu(), w.cpu(), torch.float32), 1e-2, 1e-3)
+
+
+@pytest.mark.parametrize("M", [12, 64])
+@pytest.mark.parametrize("I,K", [(3584, 8192), (128, 512), (28672, 8192)])
+def test_skinny_mfma_swiglu(M, I, K, monkeypatch):
+    monkeypatch.setattr(ops, "SKINNY_ENABLED", True)
+    x, w = rnd(M, K), rnd(2 * I, K, scale=0.05)
+    close(ops.linear_swiglu(x, w), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)
+
+
 def test_prefill_linear_and_silu_mul():
     x, w = rnd(300, 1024), rnd(2 * 512, 1024, scale=0.05)
     close(ops.linear_swiglu(x, w), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)
@@ -268,3 +286,56 @@ def test_decode_attention_fused(nq, nkv, ctxs):
         close(got, want, 2e-2)
         close(kc2, kr, 2e-2)
         close(vc2, vr, 0, 0)
+
+
+def test_fp8_decode_matches_torch_e4m3():
+    """v_cvt_pk_f32_fp8 on gfx950 decodes OCP e4m3 (torch.float8_e4m3fn) for every finite byte."""
+    codes = torch.tensor([c if c not in (0x7F, 0xFF) else 0 for c in range(256)], dtype=torch.uint8)
+    q = codes.repeat(16, 1).contiguous()  # 16 rows x 256
+    w = ops.Fp8Weight(q.to(DEV), torch.ones(16, device=DEV))
+    got = w.dequant(torch.float32).cpu()
+    want = q.view(torch.float8_e4m3fn).float().bfloat16().float()
+    assert torch.equal(got, want)
+
+
+def test_fp8_quantize_matches_reference():
+    w = rnd(256, 1024, scale=0.03)
+    fw = ops.quantize_fp8(w)
+    q_ref, s_ref = ref.quantize_fp8(w.cpu())
+    torch.testing.assert_close(fw.scale.cpu(), s_ref, rtol=1e-6, atol=0)
+    a = fw.q.cpu().view(torch.float8_e4m3fn).float()
+    b = q_ref.view(torch.float8_e4m3fn).float()
+    # w * (1/s) vs w / s may round differently at a tie: at most one e4m3 step, on a tiny fraction
+    diff = (a - b).abs()
+    assert float((diff > 0).float().mean()) < 1e-3
+    assert float((diff / b.abs().clamp_min(2 ** -6)).max()) <= 0.125 + 1e-6
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("N,K", [(1280, 8192), (8192, 1024), (8192, 3584), (96, 512)])
+def test_gemv_fp8(M, N, K):
+    x = rnd(M, K)
+    w = ops.quantize_fp8(rnd(N, K, scale=0.05))
+    want = x.float().cpu() @ w.dequant(torch.float32).cpu().T
+    close(ops.linear(x, w), want.bfloat16(), 3e-2)
+    close(ops.linear(x, w, out_dtype=torch.float32), want, 1e-2, 1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 4])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_linear_norm_fp8(M, epi):
+    K, N = 4096, 1024
+    x, res = rnd(M, K), rnd(M, K)
+    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    w = ops.quantize_fp8(rnd(2 * N if epi == 2 else N, K, scale=0.05))
+    ro = torch.empty_like(x)
+    got = ops.linear_norm(x, w, nw, 1e-5, res, ro, epi=epi)
+    r = (x.float() + res.float()).bfloat16()
+    h, _ = ref.rmsnorm(r.cpu(), nw.cpu(), 1e-5)
+    wd = w.dequant(torch.float32).cpu()
+    if epi == 2:
+        want = ref.linear_swiglu(h, wd)
+    else:
+        want = ref.linear(h, wd, torch.float32 if epi == 1 else None)
+    close(got, want, 3e-2)
+    close(ro, r, 1e-2)

@@ -70,3 +70,42 @@ def test_engine_gpu_generate_and_graph():
     eng.use_graphs = False
     eager = eng.generate(prompts[:1], p)[0]
     assert eager.token_ids == single[0].token_ids
+
+
+def test_batched_decode_matches_cpu_reference(models):
+    """B = 24 > 8: the batched path (MFMA skinny GEMMs + fused RoPE/KV/attention) vs the CPU model."""
+    g, c = models
+    B, bs, per = 24, 16, 24
+    lens = [5 + 13 * i for i in range(B)]
+    outs = {}
+    for m in (g, c):
+        dev = m.device
+        m.allocate_kv(B * per + 8, bs)
+        bt = torch.zeros(B, 32, dtype=torch.int32)
+        t = lambda x: torch.tensor(x, dtype=torch.int32, device=dev)
+        for i, T in enumerate(lens):
+            blocks = list(range(i * per, (i + 1) * per))
+            bt[i, :per] = torch.tensor(blocks)
+            ids = [(37 * i + 11 * p) % 16000 for p in range(T)]
+            slots = [blocks[p // bs] * bs + p % bs for p in range(T)]
+            m.forward_prefill(t(ids), t(list(range(T))), t(slots), t([0, T]), t([T]), bt[i:i + 1].to(dev), T,
+                              t([T - 1]))
+        ctx = t([T + 1 for T in lens])
+        outs[dev.type] = m.forward_decode(t([(7 * i) % 16000 for i in range(B)]), ctx, bt.to(dev), 2048)
+    torch.testing.assert_close(outs["cuda"].cpu(), outs["cpu"], atol=6e-2, rtol=5e-2)
+
+
+def test_fp8_model_gpu_matches_cpu_reference():
+    """fp8 projections: GPU (fp8 GEMVs, dequantized prefill GEMMs) vs the CPU model with the
+    same fp8 weights; both quantize the same bf16 init, so only rounding ties may differ."""
+    g = LlamaModel(CFG, device="cuda", seed=5, max_model_len=2048, weight_dtype="fp8")
+    c = LlamaModel(CFG, device="cpu", seed=5, max_model_len=2048, weight_dtype="fp8")
+    ids = list(range(90, 400, 9))
+    lg_g, bt_g = _prefill(g, ids)
+    lg_c, bt_c = _prefill(c, ids)
+    torch.testing.assert_close(lg_g.cpu(), lg_c, atol=8e-2, rtol=5e-2)
+    ctx = torch.tensor([len(ids) + 1], dtype=torch.int32)
+    tok = torch.tensor([321], dtype=torch.int32)
+    dec_g = g.forward_decode(tok.cuda(), ctx.cuda(), bt_g, 2048)
+    dec_c = c.forward_decode(tok, ctx, bt_c, 2048)
+    torch.testing.assert_close(dec_g.cpu(), dec_c, atol=8e-2, rtol=5e-2)

@@ -3,7 +3,7 @@
 
     python tools/kbench.py [--tp 8] [--ctx 564] [--iters 200]
 
-Reports us/call and effective HBM bandwidth for the decode-path kernels at the per-GPU shapes
+Reports us/call and effective HBM bandwidth (weight bytes / time) for the decode-path kernels at the per-GPU shapes
 of Llama-3.3-70B at a given TP degree.
 """
 
@@ -51,6 +51,7 @@ def main():
     dev = "cuda"
     H, I, V, nq, nkv, D = 8192, 28672 // a.tp, 128256 // a.tp, 64 // a.tp, max(1, 8 // a.tp), 128
     M = a.M
+    ops.SKINNY_ENABLED = True  # compare the MFMA skinny GEMM against hipBLASLt at M > 8
     bf = torch.bfloat16
     res = []
 
@@ -59,6 +60,8 @@ def main():
         w = (torch.randn(N * (2 if epi == 2 else 1), K, device=dev) * 0.02).to(bf)
         nw = torch.ones(K, device=dev, dtype=bf)
         ri, ro = torch.randn(M, K, device=dev).to(bf), torch.empty(M, K, device=dev, dtype=bf)
+        if norm and M > ops.GEMV_MAX_M:
+            return
         if norm:
             fn = lambda: ops.linear_norm(x, w, nw, 1e-5, ri, ro, epi=epi)
         elif epi == 2:
@@ -67,6 +70,11 @@ def main():
             fn = lambda: ops.linear(x, w, out_dtype=torch.float32 if epi == 1 else None)
         us = timeit(fn, a.iters)
         res.append((name, us, w.numel() * 2 / us / 1e6))
+        if M > ops.GEMV_MAX_M:  # library GEMM (hipBLASLt) at the same shape, for comparison
+            lib = (lambda: ops.silu_mul(torch.nn.functional.linear(x, w))) if epi == 2 else \
+                (lambda: torch.nn.functional.linear(x, w))
+            us = timeit(lib, a.iters)
+            res.append((name + " [hipBLASLt]", us, w.numel() * 2 / us / 1e6))
 
     gemv_case("qkv (norm)", (nq + 2 * nkv) * D, H, norm=True)
     gemv_case("qkv", (nq + 2 * nkv) * D, H)
@@ -111,7 +119,7 @@ def main():
     res.append(("trivial torch kernel (launch floor)", timeit(lambda: empty.add_(1), a.iters), 0))
     print(f"# tp={a.tp} M={M} ctx={ctx}")
     for name, us, gbs in res:
-        print(f"{name:45s} {us:8.2f} us  {gbs:8.1f} GB/s")
+        print(f"{name:45s} {us:8.2f} us  {gbs:8.2f} TB/s")
 
 
 if __name__ == "__main__":
