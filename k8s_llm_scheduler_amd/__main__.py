@@ -41,15 +41,19 @@ def build_backend(cfg: Config, metrics=None):
 
     if not cfg.engine.enabled or cfg.engine.backend == "fallback":
         return None, None, None
+    from .control.backends import FaultInjectingBackend
+
     if cfg.engine.backend == "scripted":
-        return ScriptedBackend(default=first_node_answer), None, None
+        return FaultInjectingBackend.from_spec(ScriptedBackend(default=first_node_answer),
+                                               cfg.engine.fault_injection, cfg.engine.seed), None, None
     from .engine import engine_from_config
     from .parallel import init_from_env, make_control_channel
 
     tp = init_from_env()
     control = make_control_channel(tp)
     engine = engine_from_config(cfg, tp, metrics, control=control)
-    return LocalEngineBackend(engine, ignore_eos=cfg.engine.ignore_eos), engine, tp
+    backend = LocalEngineBackend(engine, ignore_eos=cfg.engine.ignore_eos)
+    return FaultInjectingBackend.from_spec(backend, cfg.engine.fault_injection, cfg.engine.seed), engine, tp
 
 
 def build_scheduler(cfg: Config, api, backend, metrics=None):

@@ -110,6 +110,7 @@ class EngineSection:
     prefix_caching: bool = True
     ignore_eos: bool = False
     stop_on_json_close: bool = True
+    fault_injection: str = "none"      # chaos hook: none | raise:<rate> | hang:<rate> | garbage:<rate>
 
 
 @dataclass
@@ -165,6 +166,7 @@ ENV_OVERRIDES = {
     "ENGINE_BACKEND": ("engine", "backend", str),
     "ENGINE_WEIGHTS": ("engine", "weights", str),
     "ENGINE_TOKENIZER": ("engine", "tokenizer", str),
+    "K8S_FAULT_INJECTION": ("engine", "fault_injection", str),
     "SCHEDULER_MODE": ("scheduler", "mode", str),
 }
 

@@ -92,3 +92,47 @@ class LocalEngineBackend:
                                          ignore_eos=bool(self.ignore_eos)))
         outs = self.engine.generate(prompts, params, deadline=deadline)
         return [o.text for o in outs]
+
+
+class FaultInjectingBackend:
+    """Chaos hook around any backend (failure detection): with probability
+    ``rate`` an engine call raises, hangs past its deadline, or answers garbage, so the retry /
+    circuit-breaker / fallback machinery can be exercised against the real engine.
+
+    Spec string (``engine.fault_injection`` / ``K8S_FAULT_INJECTION``): ``none`` or
+    ``<mode>:<rate>`` with mode in raise | hang | garbage, e.g. ``raise:0.1``."""
+
+    MODES = ("raise", "hang", "garbage")
+
+    def __init__(self, inner, mode: str, rate: float, seed: int = 0, hang_s: float = 3600.0):
+        if mode not in self.MODES:
+            raise ValueError(f"fault mode must be one of {self.MODES}, got {mode!r}")
+        import random
+
+        self.inner, self.mode, self.rate, self.hang_s = inner, mode, float(rate), hang_s
+        self.name = f"{getattr(inner, 'name', 'backend')}+fault({mode}:{rate})"
+        self._rng = random.Random(seed)
+        self._lock = threading.Lock()
+        self.injected = 0
+
+    @classmethod
+    def from_spec(cls, inner, spec: Optional[str], seed: int = 0):
+        if not spec or spec.strip().lower() in ("none", "off", ""):
+            return inner
+        mode, _, rate = spec.partition(":")
+        return cls(inner, mode.strip().lower(), float(rate or 1.0), seed=seed)
+
+    def complete(self, requests: Sequence[GenerationRequest]) -> List[str]:
+        with self._lock:
+            hit = self._rng.random() < self.rate
+            if hit:
+                self.injected += 1
+        if not hit:
+            return self.inner.complete(requests)
+        if self.mode == "raise":
+            raise RuntimeError("injected engine fault")
+        if self.mode == "hang":
+            limit = min((r.deadline_s for r in requests if r.deadline_s), default=self.hang_s)
+            time.sleep(limit)
+            raise TimeoutError(f"injected engine hang ({limit}s)")
+        return ["\x00garbage{{" for _ in requests]

@@ -42,6 +42,7 @@ from ..control.jsonextract import json_object_closed
 from ..models.llama import LlamaModel
 from .sampling import SamplingParams
 from .tokenizer import Tokenizer
+from ..utils.tracing import trace
 
 log = logging.getLogger(__name__)
 
@@ -172,6 +173,10 @@ class LLMEngine:
         skip rows with context length 0, so warm-up and capture do not touch any state)."""
         if not self.use_graphs:
             return
+        with trace("engine.capture_graphs"):
+            self._capture_graphs(buckets)
+
+    def _capture_graphs(self, buckets: Optional[Sequence[int]]) -> None:
         assert not self.running and not self.prefilling, "capture needs an idle engine"
         buckets = buckets or [b for b in BUCKETS if b <= self.max_batch]
         stream = torch.cuda.Stream(self.device)
@@ -432,8 +437,11 @@ class LLMEngine:
                 raise StopIteration("engine stopped by rank 0")
             self._reap_aborted()
             self._admit()
-            self._prefill()
-            return self._decode()
+            if self.prefilling or self.waiting:
+                with trace("engine.prefill"):
+                    self._prefill()
+            with trace("engine.decode"):
+                return self._decode()
 
     def serve_worker(self) -> None:
         """Non-zero TP ranks: follow rank 0's schedule until it sends stop."""

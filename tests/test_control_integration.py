@@ -199,3 +199,29 @@ def test_batched_round_revalidates_capacity():
     assert out[0].selected_node == "small" and not out[0].fallback_needed
     assert all(d.selected_node == "big" and d.fallback_needed for d in out[1:])
     assert len(be.calls) == 1 and len(be.calls[0]) == 3     # one engine call for the batch
+
+
+def test_fault_injection_hook_drives_retries_breaker_and_fallback():
+    from k8s_llm_scheduler_amd.control.backends import FaultInjectingBackend
+
+    nodes = snapshot(cluster())
+    pod = pod_to_spec(make_pod("a"))
+    inner = ScriptedBackend(default=first_node_answer)
+    assert FaultInjectingBackend.from_spec(inner, "none") is inner
+    # every call raises: 3 retries, then the breaker opens and trips
+    fi = FaultInjectingBackend.from_spec(inner, "raise:1.0")
+    svc, sleeps = service(fi, circuit_breaker__failure_threshold=3)
+    d = svc.decide("VALID NODE NAMES: kind-worker\n", pod, nodes)
+    assert d.fallback_needed and sleeps == [1.0, 2.0] and fi.injected == 3
+    assert svc.decide("VALID NODE NAMES: kind-worker\n", pod, nodes).reasoning.endswith("Circuit breaker open")
+    # garbage answers: fallback "JSON parsing failed", not a breaker failure (reference quirk 6)
+    svc, _ = service(FaultInjectingBackend.from_spec(inner, "garbage:1"))
+    d = svc.decide("VALID NODE NAMES: kind-worker\n", pod, nodes)
+    assert d.reasoning.endswith("JSON parsing failed") and svc.circuit_breaker.failures == 0
+    # hang past the deadline -> engine failure per attempt
+    svc, _ = service(FaultInjectingBackend.from_spec(inner, "hang:1"), llm__timeout=0.01, llm__max_retries=1)
+    d = svc.decide("VALID NODE NAMES: kind-worker\n", pod, nodes)
+    assert d.fallback_needed and svc.get_stats()["failed_requests"] == 1
+    # rate 0: transparent
+    svc, _ = service(FaultInjectingBackend.from_spec(inner, "raise:0.0"))
+    assert svc.decide("VALID NODE NAMES: kind-worker\n", pod, nodes).selected_node == "kind-worker"
