@@ -75,9 +75,13 @@ class LocalEngineBackend:
 
     name = "local"
 
-    def __init__(self, engine, ignore_eos: Optional[bool] = None):
+    def __init__(self, engine, ignore_eos: Optional[bool] = None,
+                 forced_answer: Optional[Callable[[GenerationRequest], str]] = None):
+        """``forced_answer`` (tests / benchmarks of the LLM-success path): the engine still runs the
+        full prefill and decode, but reports the tokens of ``forced_answer(request)``."""
         self.engine = engine
         self.ignore_eos = ignore_eos
+        self.forced_answer = forced_answer
 
     def complete(self, requests: Sequence[GenerationRequest]) -> List[str]:
         from ..engine.sampling import SamplingParams
@@ -88,8 +92,12 @@ class LocalEngineBackend:
         prompts, params = [], []
         for r in requests:
             prompts.append(self.engine.render_chat(r.system, r.user))
+            forced = None
+            if self.forced_answer is not None:
+                forced = self.engine.tok.encode(self.forced_answer(r))
             params.append(SamplingParams(max_tokens=r.max_tokens, temperature=r.temperature, top_p=r.top_p,
-                                         ignore_eos=bool(self.ignore_eos)))
+                                         ignore_eos=bool(self.ignore_eos) and forced is None,
+                                         forced_output_ids=forced))
         outs = self.engine.generate(prompts, params, deadline=deadline)
         return [o.text for o in outs]
 

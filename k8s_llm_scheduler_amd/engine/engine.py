@@ -376,7 +376,11 @@ class LLMEngine:
             n = int(nsteps[slot])
             new = hist[slot, len(r.output_ids):n].tolist()
             self.stats["decode_tokens"] += len(new)
+            forced = r.params.forced_output_ids
             for tkn in new:
+                if forced is not None:  # scripted answer; past its end: EOS
+                    i = len(r.output_ids)
+                    tkn = forced[i] if i < len(forced) else next(iter(self.tok.eos_ids))
                 r.output_ids.append(tkn)
                 if self._stopped(r, tkn):
                     break

@@ -16,6 +16,10 @@ class SamplingParams:
     ignore_eos: bool = False
     stop_on_json_close: bool = True
     stop_token_ids: List[int] = field(default_factory=list)
+    # Forced decode: the engine runs the full prefill + decode but reports these
+    # tokens instead of the sampled ones (then stops), so the LLM-success path of the control
+    # plane can be driven through the real engine with random-init weights.
+    forced_output_ids: Optional[List[int]] = None
 
     def validate(self) -> "SamplingParams":
         if self.max_tokens < 1:

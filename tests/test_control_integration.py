@@ -225,3 +225,21 @@ def test_fault_injection_hook_drives_retries_breaker_and_fallback():
     # rate 0: transparent
     svc, _ = service(FaultInjectingBackend.from_spec(inner, "raise:0.0"))
     assert svc.decide("VALID NODE NAMES: kind-worker\n", pod, nodes).selected_node == "kind-worker"
+
+
+@pytest.mark.parametrize("mode", ["sequential", "batched"])
+def test_e2e_real_engine_forced_decode_llm_success_path(mode):
+    """The whole pipeline through the real (tiny, CPU) engine: chat template -> tokenize ->
+    prefill/decode -> detokenize -> JSON extraction -> validation -> bind.  Forced decode makes the
+    random-init model emit a valid answer, so every pod is an LLM decision, not a fallback."""
+    from k8s_llm_scheduler_amd.control.backends import LocalEngineBackend
+    from k8s_llm_scheduler_amd.engine import build_engine
+
+    eng = build_engine("tiny", device="cpu", max_batch=4, max_model_len=1024, num_blocks=256, seed=1)
+    api = cluster(run_bound_pods=True)
+    pods = ai_test_pods(api)
+    sched = run_scheduler(api, LocalEngineBackend(eng, forced_answer=first_node_answer), pods, mode=mode, timeout=60)
+    st = sched.get_stats()
+    assert st["total_scheduled"] == 3 and st["llm_decisions"] == 3 and st["fallback_decisions"] == 0
+    assert st["llm_client"]["successful_requests"] == 3
+    assert eng.stats["decode_tokens"] > 0 and eng.stats["prefill_tokens"] > 0

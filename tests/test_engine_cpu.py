@@ -181,3 +181,10 @@ def test_block_allocator_prefix_and_eviction():
         A.allocate([1], 4)
     with pytest.raises(Exception):
         A.release([c.blocks[0], c.blocks[0]])
+
+
+def test_forced_decode_emits_script_and_stops_on_json(engine):
+    ans = '{"selected_node": "kind-worker2", "confidence": 0.9, "reasoning": "r"}'
+    ids = engine.tok.encode(ans)
+    o = engine.generate(["pick a node"], SamplingParams(max_tokens=200, temperature=0.3, forced_output_ids=ids))[0]
+    assert o.text == ans and o.finish_reason == "json"
