@@ -8,12 +8,17 @@
 //  * weights are loaded with non-temporal hints (read once: keep them out of L2/MALL),
 //  * bf16 pairs are multiplied with v_dot2_f32_bf16 (fp32 accumulate),
 //  * when N alone gives too few workgroups to fill 256 CUs, K is split (grid.y) and partial
-//    fp32 slabs are combined by a finalize kernel that also applies the epilogue.
+//    fp32 slabs are combined by a finalize kernel that also applies the epilogue;
+//  * for small N (e.g. the TP = 8 QKV / gate-up slices) KW waves of a workgroup share one row
+//    set and split its K range (reduced through LDS), so every wave's share of the weight
+//    stream is in flight at once instead of taking several dependent rounds.
 // Epilogues: BF16 store, FP32 store (logits), SWIGLU: W = [gate; up] (2I rows) and the output is
 // silu(gate_j) * up_j (SURVEY.md K10 fused into K9).
 // FP8 weights (BASELINE config 5): W holds OCP e4m3 bytes with one fp32 scale per row; a 16-byte
 // load carries 16 weights (half the HBM bytes of bf16), decoded with v_cvt_pk_f32_fp8 and
 // multiplied in fp32; the row scale is applied once in the epilogue.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace k8sllm {
@@ -68,7 +73,7 @@ __device__ __forceinline__ void norm_row_chunk(const bf16_t* __restrict__ x, con
   for (int j = 0; j < 4; ++j) r[j] = pack_bf2(lo_bf(a[j]) + lo_bf(b[j]), hi_bf(a[j]) + hi_bf(b[j]));
 }
 
-template <int M, int RPW, int EPI, bool NORM, bool FP8>
+template <int M, int RPW, int EPI, bool NORM, bool FP8, int KW>
 __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float* __restrict__ partial,
                                                    const bf16_t* __restrict__ x, const void* __restrict__ W,
                                                    int N_out, int K, int KS, int half_rows,
@@ -88,8 +93,11 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
 
   constexpr int NR = (EPI == EPI_SWIGLU) ? 2 * RPW : RPW;  // weight rows per wave
   constexpr int U = (NR >= 4) ? 2 : ((NR >= 2) ? 4 : 8);  // chunks per lane in flight per row
-  const int r0 = (blockIdx.x * 4 + wid) * RPW;               // first output row of this wave
+  const int r0 = (blockIdx.x * (4 / KW) + wid / KW) * RPW;  // first output row of this wave
   const bool active = r0 < N_out;
+  const int kpart = wid % KW;                                // this wave's share of the K chunks
+  const int per = (nch + KW - 1) / KW;
+  const int cb = kpart * per, ce = min(nch, cb + per), clast = max(min(ce, nch) - 1, 0);
   const char* wrow[NR];
   const char* Wb = static_cast<const char*>(W);
 #pragma unroll
@@ -104,39 +112,73 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int r = 0; r < NR; ++r)
-      wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + min(lane + 64 * u, nch - 1));
+      wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + min(cb + lane + 64 * u, clast));
 
   if (NORM) {
+    // One global pass: r = x + res_in over the whole row (the sum of squares needs all of it),
+    // this slice of r parked in LDS, this thread's norm-weight chunks prefetched into registers;
+    // after the reduction the slice is normalised in place in LDS (no second global read).
     const bool writer = blockIdx.x == 0 && blockIdx.y == 0 && res_out != nullptr;
-    float inv[M];
+    const int kc0 = kb >> 3;
+    constexpr int GI = 4;  // norm-weight chunks per thread held in registers (xch <= 1024)
+    u32x4 g[GI];
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      float ss = 0.f;
-      for (int c = threadIdx.x; c < (K >> 3); c += blockDim.x) {
-        u32x4 r;
-        norm_row_chunk<M>(x, res_in, m, K, c, r);
-        if (writer) reinterpret_cast<u32x4*>(res_out + (size_t)m * K)[c] = r;
+    for (int i = 0; i < GI; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (c < xch) g[i] = reinterpret_cast<const u32x4*>(nw + kb)[c];
+    }
+    float ss[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ss[m] = 0.f;
+#pragma unroll 2
+    for (int c = threadIdx.x; c < (K >> 3); c += blockDim.x) {
+      u32x4 r[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) norm_row_chunk<M>(x, res_in, m, K, c, r[m]);
+      const int cs = c - kc0;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        if (writer) reinterpret_cast<u32x4*>(res_out + (size_t)m * K)[c] = r[m];
+        if (cs >= 0 && cs < xch) xs[m * (KS >> 3) + cs] = r[m];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float l = lo_bf(r[j]), h = hi_bf(r[j]);
-          ss += l * l + h * h;
+          const float l = lo_bf(r[m][j]), h = hi_bf(r[m][j]);
+          ss[m] += l * l + h * h;
         }
       }
-      ss = wave_sum(ss);
-      if (lane == 0) nred[wid][m] = ss;
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float t = wave_sum(ss[m]);
+      if (lane == 0) nred[wid][m] = t;
     }
     __syncthreads();
+    float inv[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) inv[m] = rsqrtf((nred[0][m] + nred[1][m] + nred[2][m] + nred[3][m]) / (float)K + eps);
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      for (int c = threadIdx.x; c < xch; c += blockDim.x) {
-        u32x4 r, o;
-        norm_row_chunk<M>(x, res_in, m, K, (kb >> 3) + c, r);
-        const u32x4 g = reinterpret_cast<const u32x4*>(nw + kb)[c];
+    for (int i = 0; i < GI; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (c >= xch) break;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const u32x4 r = xs[m * (KS >> 3) + c];
+        u32x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          o[j] = pack_bf2(lo_bf(r[j]) * inv[m] * lo_bf(g[j]), hi_bf(r[j]) * inv[m] * hi_bf(g[j]));
+          o[j] = pack_bf2(lo_bf(r[j]) * inv[m] * lo_bf(g[i][j]), hi_bf(r[j]) * inv[m] * hi_bf(g[i][j]));
+        xs[m * (KS >> 3) + c] = o;
+      }
+    }
+    for (int c = threadIdx.x + 256 * GI; c < xch; c += blockDim.x) {  // slices longer than 8192
+      const u32x4 gw = reinterpret_cast<const u32x4*>(nw + kb)[c];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const u32x4 r = xs[m * (KS >> 3) + c];
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = pack_bf2(lo_bf(r[j]) * inv[m] * lo_bf(gw[j]), hi_bf(r[j]) * inv[m] * hi_bf(gw[j]));
         xs[m * (KS >> 3) + c] = o;
       }
     }
@@ -156,24 +198,23 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
   for (int r = 0; r < NR; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
-  if (!active) return;
-  for (int c = lane; c < nch; c += 64 * U) {
+  for (int c = cb + lane; active && c < ce; c += 64 * U) {
     u32x4 cur[U][NR];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < NR; ++r) cur[u][r] = wv[u][r];
     const int cn = c + 64 * U;
-    if (cn < nch) {
+    if (cn < ce) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int r = 0; r < NR; ++r)
-          wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + min(cn + 64 * u, nch - 1));
+          wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + min(cn + 64 * u, clast));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (c + 64 * u < nch) {
+      if (c + 64 * u < ce) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           if (FP8) {
@@ -195,7 +236,25 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
 
-  if (lane != 0) return;
+  if (KW > 1) {  // combine the K parts of the waves sharing these rows
+    __shared__ float kred[4][NR][M];
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int m = 0; m < M; ++m) kred[wid][r][m] = acc[r][m];
+    }
+    __syncthreads();
+    if (kpart != 0 || lane != 0 || !active) return;
+#pragma unroll
+    for (int j = 1; j < KW; ++j)
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int m = 0; m < M; ++m) acc[r][m] += kred[wid + j][r][m];
+  } else if (lane != 0 || !active) {
+    return;
+  }
   const int wrows = (EPI == EPI_SWIGLU) ? 2 * half_rows : N_out;  // weight rows (slab width)
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
@@ -283,7 +342,21 @@ extern "C" int k8s_gemv_norm_w(void* out, void* partial, const void* x, const vo
   if (splits > 1 && partial == nullptr) return -3;
   float* part = splits > 1 ? (float*)partial : nullptr;
   const int rpw = (M >= 4) ? 2 : 1;
-  dim3 grid((N_out + 4 * rpw - 1) / (4 * rpw), splits);
+  // KW: waves per row set.  Split a row set's K over 2 or 4 waves while N alone leaves fewer
+  // than ~1024 workgroups and every wave keeps >= 2 chunks per lane (K8S_GEMV_KW overrides).
+  static const int kw_env = [] { const char* e = getenv("K8S_GEMV_KW"); return e ? atoi(e) : 0; }();
+  const int nch_split = ks / (fp8 ? 16 : 8);
+  int kw = 1;
+  if (kw_env == 1 || kw_env == 2 || kw_env == 4) {
+    kw = kw_env;
+  } else {
+    // measured (profiles/kbench_gemv_kw.txt): only the plain small-N GEMV gains; the norm
+    // variants pay one prologue per workgroup, so they keep one wave per row set
+    const int wg1 = (N_out + 4 * rpw - 1) / (4 * rpw) * splits;
+    if (nw == nullptr && wg1 < 512 && nch_split >= 256) kw = 2;
+  }
+  const int rows_per_wg = (4 / kw) * rpw;
+  dim3 grid((N_out + rows_per_wg - 1) / rows_per_wg, splits);
   const size_t lds = (size_t)M * ks * 2;
   const int half_rows = (epi == EPI_SWIGLU) ? N_out : 0;
   const bf16_t* xx = (const bf16_t*)x;
@@ -291,11 +364,15 @@ extern "C" int k8s_gemv_norm_w(void* out, void* partial, const void* x, const vo
   const bf16_t* ri = (const bf16_t*)res_in;
   bf16_t* ro = (bf16_t*)res_out;
   const bf16_t* gw = (const bf16_t*)nw;
-#define G2(MM, RR, EE, F8)                                                                                    \
-  if (gw) gemv_kernel<MM, RR, EE, true, F8><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,      \
-                                                                        half_rows, ri, ro, gw, eps, wscale); \
-  else gemv_kernel<MM, RR, EE, false, F8><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,        \
-                                                                      half_rows, ri, ro, gw, eps, wscale)
+#define G3(MM, RR, EE, F8, KK)                                                                                 \
+  if (gw) gemv_kernel<MM, RR, EE, true, F8, KK><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,   \
+                                                                            half_rows, ri, ro, gw, eps, wscale); \
+  else gemv_kernel<MM, RR, EE, false, F8, KK><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,     \
+                                                                          half_rows, ri, ro, gw, eps, wscale)
+#define G2(MM, RR, EE, F8)                      \
+  if (kw == 4) { G3(MM, RR, EE, F8, 4); }        \
+  else if (kw == 2) { G3(MM, RR, EE, F8, 2); }   \
+  else { G3(MM, RR, EE, F8, 1); }
 #define G(MM, RR, EE)        \
   if (fp8) { G2(MM, RR, EE, true); } \
   else { G2(MM, RR, EE, false); }
@@ -319,6 +396,7 @@ extern "C" int k8s_gemv_norm_w(void* out, void* partial, const void* x, const vo
 #undef BY_EPI
 #undef G
 #undef G2
+#undef G3
   if (splits > 1) {
     const int total = M * N_out;
     const int blocks = (total + 255) / 256;

@@ -405,8 +405,25 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
                     _chk(ctx_inc, I32, "ctx_inc") if ctx_inc is not None else 0,
                     _chk(hist, I32, "hist") if hist is not None else 0,
                     hist.shape[1] if hist is not None else 0,
-                    _chk(steps, I32, "steps") if steps is not None else 0, -1)
+                    _chk(steps, I32, "steps") if steps is not None else 0, _sample_scratch(logits.device, B), -1)
     return out
+
+
+_SCRATCH: dict = {}
+
+
+def _sample_scratch(dev: torch.device, B: int) -> int:
+    """Zeroed per-row (atomic key, arrival counter) scratch of the multi-workgroup sampler.  Every
+    launch leaves it zeroed again; buffers are never freed because captured graphs keep their
+    pointers (stream order serialises the launches that share one)."""
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    buf = _SCRATCH.get(i)
+    need = native().sample_scratch_bytes(B)
+    if buf is None or buf.numel() < need:
+        buf = torch.zeros(max(need, native().sample_scratch_bytes(256)), dtype=torch.uint8, device=dev)
+        _SCRATCH.setdefault(("keep", i), []).append(buf)
+        _SCRATCH[i] = buf
+    return buf.data_ptr()
 
 
 # ----------------------------------------------------------------------------- init

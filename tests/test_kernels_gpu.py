@@ -316,7 +316,7 @@ def test_fp8_quantize_matches_reference():
 def test_gemv_fp8(M, N, K):
     x = rnd(M, K)
     w = ops.quantize_fp8(rnd(N, K, scale=0.05))
-    want = x.float().cpu() @ w.dequant(torch.float32).cpu().T
+    want = x.float().cpu() @ ref.dequant_fp8(w.q.cpu(), w.scale.cpu()).T   # exact fp32 dequant
     close(ops.linear(x, w), want.bfloat16(), 3e-2)
     close(ops.linear(x, w, out_dtype=torch.float32), want, 1e-2, 1e-3)
 
@@ -332,7 +332,7 @@ def test_linear_norm_fp8(M, epi):
     got = ops.linear_norm(x, w, nw, 1e-5, res, ro, epi=epi)
     r = (x.float() + res.float()).bfloat16()
     h, _ = ref.rmsnorm(r.cpu(), nw.cpu(), 1e-5)
-    wd = w.dequant(torch.float32).cpu()
+    wd = ref.dequant_fp8(w.q.cpu(), w.scale.cpu())
     if epi == 2:
         want = ref.linear_swiglu(h, wd)
     else:
