@@ -46,6 +46,11 @@ int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const v
                                void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
                                float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax,
                                hipStream_t s);
+long long k8s_decode_split_workspace(int B, int nq, int nkv, int pmax);
+int k8s_decode_attention_split(void* out, void* part, uint32_t* counters, const void* qkv, const float* cos_sin,
+                               void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
+                               float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax,
+                               hipStream_t s);
 int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
                const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist,
                int hist_stride, int* steps, void* scratch, hipStream_t s);
@@ -138,6 +143,17 @@ PYBIND11_MODULE(_C, m) {
     check(k8s_decode_attention_fused(P(out), P(pacc), P(pml), P(qkv), P<float>(cos_sin), P(kc), P(vc), P<int>(bt),
                                      P<int>(ctx), scale, B, nq, nkv, D, bs, max_blocks, pmax, S(s)),
           "decode_attention_fused");
+  });
+  m.def("decode_split_workspace", [](int B, int nq, int nkv, int pmax) {
+    return k8s_decode_split_workspace(B, nq, nkv, pmax);
+  });
+  m.def("decode_attention_split", [](uintptr_t out, uintptr_t part, uintptr_t counters, uintptr_t qkv,
+                                     uintptr_t cos_sin, uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx,
+                                     float scale, int B, int nq, int nkv, int D, int bs, int max_blocks, int pmax,
+                                     int64_t s) {
+    check(k8s_decode_attention_split(P(out), P(part), P<uint32_t>(counters), P(qkv), P<float>(cos_sin), P(kc), P(vc),
+                                     P<int>(bt), P<int>(ctx), scale, B, nq, nkv, D, bs, max_blocks, pmax, S(s)),
+          "decode_attention_split");
   });
   m.def("sample", [](uintptr_t tokens, uintptr_t logits, int B, int Vs, int shards, uintptr_t temp, uintptr_t top_p,
                      uintptr_t seeds, uintptr_t counter, uintptr_t ctx_inc, uintptr_t hist, int hist_stride,

@@ -130,20 +130,32 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
     float ss[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = 0.f;
-#pragma unroll 2
-    for (int c = threadIdx.x; c < (K >> 3); c += blockDim.x) {
-      u32x4 r[M];
+    // NL row chunks per thread are loaded before any is consumed: at K = 8192 and M <= 2 the
+    // whole row is ONE round trip (the prologue sits on every workgroup's critical path)
+    constexpr int NL = M <= 2 ? 4 : (M <= 4 ? 2 : 1);
+    const int nkc = K >> 3;
+    for (int c0 = threadIdx.x; c0 < nkc; c0 += blockDim.x * NL) {
+      u32x4 r[NL][M];
 #pragma unroll
-      for (int m = 0; m < M; ++m) norm_row_chunk<M>(x, res_in, m, K, c, r[m]);
-      const int cs = c - kc0;
+      for (int u = 0; u < NL; ++u) {
+        const int c = min(c0 + u * (int)blockDim.x, nkc - 1);
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        if (writer) reinterpret_cast<u32x4*>(res_out + (size_t)m * K)[c] = r[m];
-        if (cs >= 0 && cs < xch) xs[m * (KS >> 3) + cs] = r[m];
+        for (int m = 0; m < M; ++m) norm_row_chunk<M>(x, res_in, m, K, c, r[u][m]);
+      }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float l = lo_bf(r[m][j]), h = hi_bf(r[m][j]);
-          ss[m] += l * l + h * h;
+      for (int u = 0; u < NL; ++u) {
+        const int c = c0 + u * (int)blockDim.x;
+        if (c >= nkc) break;
+        const int cs = c - kc0;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          if (writer) reinterpret_cast<u32x4*>(res_out + (size_t)m * K)[c] = r[u][m];
+          if (cs >= 0 && cs < xch) xs[m * (KS >> 3) + cs] = r[u][m];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float l = lo_bf(r[u][m][j]), h = hi_bf(r[u][m][j]);
+            ss[m] += l * l + h * h;
+          }
         }
       }
     }

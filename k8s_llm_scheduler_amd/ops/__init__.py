@@ -28,6 +28,11 @@ EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
 BF16, F32, I32 = torch.bfloat16, torch.float32, torch.int32
 DECODE_PARTITION = 64
 FUSED_PARTITION = 1024
+SPLIT_PARTITION = 64
+# Decode attention with at most this many (sequence, kv head) pairs uses the small-grid kernel
+# (attn_decode_split.hip: one wave per 64-token chunk, in-kernel merge); more pairs fill the chip
+# with the one-workgroup-per-pair kernel (attn_decode_fused.hip).  K8S_ATTN_SPLIT_PAIRS overrides.
+SPLIT_MAX_PAIRS = int(os.environ.get("K8S_ATTN_SPLIT_PAIRS", "64"))
 
 
 def native():
@@ -323,6 +328,9 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
                           block_tables=block_tables, block_size=block_size)
         return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, context_lens, scale,
                                           block_size).view(B, nq * D)
+    if B * nkv <= SPLIT_MAX_PAIRS and max_context <= 64 * SPLIT_PARTITION:
+        return _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
+                                       max_context, nq, nkv, D)
     pmax = max(1, math.ceil(max_context / FUSED_PARTITION))
     out = torch.empty(B, nq * D, dtype=BF16, device=qkv.device)
     if pmax > 1:
@@ -335,6 +343,24 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
                                     _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
                                     _chk(block_tables, I32, "block_tables"), _chk(context_lens, I32, "context_lens"),
                                     float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], pmax, -1)
+    return out
+
+
+def _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
+                            max_context, nq, nkv, D) -> torch.Tensor:
+    B = qkv.shape[0]
+    pmax = max(1, math.ceil(max_context / SPLIT_PARTITION))
+    out = torch.empty(B, nq * D, dtype=BF16, device=qkv.device)
+    part = None
+    if pmax > 1:
+        part = torch.empty(native().decode_split_workspace(B, nq, nkv, pmax), dtype=F32, device=qkv.device)
+    counters = _zeroed_scratch(qkv.device, "attn_split", B * nkv * 4)
+    native().decode_attention_split(out.data_ptr(), part.data_ptr() if part is not None else 0, counters,
+                                    _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"),
+                                    _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
+                                    _chk(block_tables, I32, "block_tables"), _chk(context_lens, I32, "context_lens"),
+                                    float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], pmax, -1)
+    del part
     return out
 
 
@@ -412,18 +438,22 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
 _SCRATCH: dict = {}
 
 
-def _sample_scratch(dev: torch.device, B: int) -> int:
-    """Zeroed per-row (atomic key, arrival counter) scratch of the multi-workgroup sampler.  Every
-    launch leaves it zeroed again; buffers are never freed because captured graphs keep their
-    pointers (stream order serialises the launches that share one)."""
+def _zeroed_scratch(dev: torch.device, kind: str, nbytes: int, min_bytes: int = 4096) -> int:
+    """Zeroed scratch of a kernel that leaves it zeroed again after every launch (arrival counters,
+    atomic keys).  Buffers are never freed because captured graphs keep their pointers; stream order
+    serialises the launches that share one."""
     i = dev.index if dev.index is not None else torch.cuda.current_device()
-    buf = _SCRATCH.get(i)
-    need = native().sample_scratch_bytes(B)
-    if buf is None or buf.numel() < need:
-        buf = torch.zeros(max(need, native().sample_scratch_bytes(256)), dtype=torch.uint8, device=dev)
+    buf = _SCRATCH.get((kind, i))
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.zeros(max(nbytes, min_bytes), dtype=torch.uint8, device=dev)
         _SCRATCH.setdefault(("keep", i), []).append(buf)
-        _SCRATCH[i] = buf
+        _SCRATCH[(kind, i)] = buf
     return buf.data_ptr()
+
+
+def _sample_scratch(dev: torch.device, B: int) -> int:
+    """Per-row (atomic key, arrival counter) scratch of the multi-workgroup sampler."""
+    return _zeroed_scratch(dev, "sample", native().sample_scratch_bytes(B), native().sample_scratch_bytes(256))
 
 
 # ----------------------------------------------------------------------------- init

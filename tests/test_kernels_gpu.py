@@ -262,9 +262,11 @@ def test_linear_norm_fused(M, epi, with_res):
     close(got, want, 3e-2 if epi != 1 else 2e-2)
 
 
-@pytest.mark.parametrize("nq,nkv", [(8, 1), (64, 8), (32, 8), (4, 2)])
-@pytest.mark.parametrize("ctxs", [[1, 37, 600], [1024, 1025], [3000]])
-def test_decode_attention_fused(nq, nkv, ctxs):
+@pytest.mark.parametrize("split_pairs", [0, 64], ids=["one-wg-per-pair", "small-grid-split"])
+@pytest.mark.parametrize("nq,nkv", [(8, 1), (64, 8), (32, 8), (4, 2), (16, 1)])
+@pytest.mark.parametrize("ctxs", [[1, 37, 600], [1024, 1025], [3000], [64, 65, 128]])
+def test_decode_attention_fused(nq, nkv, ctxs, split_pairs, monkeypatch):
+    monkeypatch.setattr(ops, "SPLIT_MAX_PAIRS", split_pairs)
     D, bs = 128, 16
     B = len(ctxs)
     maxb = (max(ctxs) + bs - 1) // bs
@@ -339,3 +341,34 @@ def test_linear_norm_fp8(M, epi):
         want = ref.linear(h, wd, torch.float32 if epi == 1 else None)
     close(got, want, 3e-2)
     close(ro, r, 1e-2)
+
+
+def test_decode_attention_split_graph_replay_rearms_counters(monkeypatch):
+    """The small-grid kernel's last-arriver merge must leave its arrival counters at zero: many
+    captured launches in a row (as in 80 decode layers) give the same answer every time."""
+    monkeypatch.setattr(ops, "SPLIT_MAX_PAIRS", 64)
+    nq, nkv, D, bs, B = 8, 1, 128, 16, 2
+    ctxs = [700, 129]
+    maxb = 64
+    kc, vc = _paged_cache(nkv, D, bs, B * maxb)
+    bt = torch.arange(B * maxb, device=DEV, dtype=torch.int32).view(B, maxb)
+    ctx = torch.tensor(ctxs, device=DEV, dtype=torch.int32)
+    qkv = rnd(B, (nq + 2 * nkv) * D)
+    cs = ref.rope_table(D, 4096, 500000.0, None).to(DEV)
+    want = ops.decode_attention_fused(qkv.cpu(), cs.cpu(), kc.cpu().clone(), vc.cpu().clone(), bt.cpu(), ctx.cpu(),
+                                      1 / math.sqrt(D), bs, 1024, nq, nkv, D)
+    outs = []
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.decode_attention_fused(qkv, cs, kc, vc, bt, ctx, 1 / math.sqrt(D), bs, 1024, nq, nkv, D)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(6):
+            outs.append(ops.decode_attention_fused(qkv, cs, kc, vc, bt, ctx, 1 / math.sqrt(D), bs, 1024, nq, nkv, D))
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    for o in outs:
+        close(o, want, 2e-2)

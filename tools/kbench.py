@@ -93,13 +93,18 @@ def main():
     cl = torch.full((M,), ctx, device=dev, dtype=torch.int32)
     qkv = torch.randn(M, (nq + 2 * nkv) * D, device=dev).to(bf)
     cs = ref.rope_table(D, 4096, 500000.0, None).to(dev)
-    for mc in (1024, 4096):
-        us = timeit(lambda: ops.decode_attention_fused(qkv, cs, kc, vc, bt, cl, 0.088, bs, mc, nq, nkv, D), a.iters)
-        res.append((f"decode_attn_fused ctx={ctx} maxctx={mc}", us, 2 * ctx * nkv * D * 2 * M / us / 1e6))
-    for c2 in (1, 16, 64, 128, 256, 1000):
-        cl2 = torch.full((M,), c2, device=dev, dtype=torch.int32)
-        us = timeit(lambda: ops.decode_attention_fused(qkv, cs, kc, vc, bt, cl2, 0.088, bs, 1024, nq, nkv, D), a.iters)
-        res.append((f"decode_attn_fused ctx={c2}", us, 0))
+    default_pairs = ops.SPLIT_MAX_PAIRS
+    for pairs, tag in ((0, "one-wg"), (default_pairs, "split")):
+        ops.SPLIT_MAX_PAIRS = pairs
+        for mc in (1024, 4096):
+            us = timeit(lambda: ops.decode_attention_fused(qkv, cs, kc, vc, bt, cl, 0.088, bs, mc, nq, nkv, D), a.iters)
+            res.append((f"decode_attn[{tag}] ctx={ctx} maxctx={mc}", us, 2 * ctx * nkv * D * 2 * M / us / 1e6))
+        for c2 in (1, 64, 256, 1000):
+            cl2 = torch.full((M,), c2, device=dev, dtype=torch.int32)
+            us = timeit(lambda: ops.decode_attention_fused(qkv, cs, kc, vc, bt, cl2, 0.088, bs, 1024, nq, nkv, D),
+                        a.iters)
+            res.append((f"decode_attn[{tag}] ctx={c2}", us, 0))
+    ops.SPLIT_MAX_PAIRS = default_pairs
     q = torch.randn(M, nq, D, device=dev).to(bf)
     us = timeit(lambda: ops.paged_decode_attention(q, kc, vc, bt, cl, 0.088, bs, 1024), a.iters)
     res.append((f"paged_decode_attention(split64) ctx={ctx}", us, 2 * ctx * nkv * D * 2 * M / us / 1e6))
