@@ -16,6 +16,10 @@ decision rate itself.  Scaling is "strong" (fixed work per decision, more GPUs).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--preset llama-3.3-70b] [--gen-tokens 64]
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+    torchrun --nproc-per-node 8 ... bench.py --gpus 8 --tp 4 --dtype fp8   # 2 half-node replicas (config 5)
+
+Default: one TP=N engine (strong scaling).  With --tp T < N, N/T replicas each decide their own
+pods (data parallelism, weak scaling) and the value is the sum over replicas.
 """
 
 from __future__ import annotations
@@ -48,6 +52,9 @@ def main() -> int:
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
                     help="projection weight dtype (fp8 = BASELINE config 5: row-scaled e4m3 weights, bf16 activations)")
+    ap.add_argument("--tp", type=int, default=0,
+                    help="TP degree of one engine replica (0 = all GPUs); WORLD_SIZE / tp replicas decide in "
+                         "parallel (data parallelism, e.g. --tp 4 on 8 GPUs = two half-node engines)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--simulate-tp", type=int, default=0,
                     help="PROFILING ONLY: run one TP rank's shapes on one GPU with collectives skipped")
@@ -69,11 +76,12 @@ def main() -> int:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-    tp = init_from_env("cuda")
+    tp = init_from_env("cuda", tp_size=args.tp)
     if args.simulate_tp > 1:
         from k8s_llm_scheduler_amd.parallel import TPGroup
         tp = TPGroup(0, args.simulate_tp, None, "none", simulate=True)
-    rank = tp.rank
+    rank = tp.global_rank
+    dp = tp.replicas
 
     t_init = time.perf_counter()
     bs = 16
@@ -109,8 +117,10 @@ def main() -> int:
 
     prompt_tokens = len(eng.render_chat(svc.system_message, make_items()[0][0]))
 
+    distributed = world > 1 and not tp.simulate
+
     def barrier():
-        if tp.world > 1 and not tp.simulate:
+        if distributed:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -128,12 +138,12 @@ def main() -> int:
         fallbacks += sum(d.fallback_needed for d in ds)
     barrier()
     elapsed = time.perf_counter() - t0
-    if tp.world > 1 and not tp.simulate:
+    if distributed:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    decisions = args.steps * args.batch
+    decisions = args.steps * args.batch * dp   # every replica decides its own pods
     value = decisions / elapsed
     st = eng.stats
     dec_tok_ms = 1000 * st["decode_time"] / max(1, st["decode_steps"])
@@ -141,23 +151,23 @@ def main() -> int:
         "metric": "scheduling_decisions_per_sec",
         "value": round(value, 4),
         "unit": "decisions/s",
-        "n_gpus": tp.world,
+        "n_gpus": tp.world * dp if not tp.simulate else tp.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000 * elapsed / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if dp > 1 else "strong",
         "vs_baseline": round(value / BASELINE_DECISIONS_PER_S, 3),
         "dtype": "bf16" if args.dtype == "bf16" else "fp8-e4m3 weights, bf16 activations",
         "data": "synthetic cluster-state prompts, random-init weights",
         "config": {
             "model": f"{args.preset} (Llama-3.3-70B-Instruct architecture)" if "70b" in args.preset else args.preset,
-            "global_batch": args.batch,
+            "global_batch": args.batch * dp,
             "seq_len": prompt_tokens + args.gen_tokens,
             "prompt_tokens": prompt_tokens,
             "gen_tokens": args.gen_tokens,
             "cluster_nodes": args.nodes,
-            "parallelism": f"tp{tp.world}" + ("-SIMULATED-no-comm" if tp.simulate else ""),
+            "parallelism": (f"dp{dp}-" if dp > 1 else "") + f"tp{tp.world}" + ("-SIMULATED-no-comm" if tp.simulate else ""),
             "cuda_graphs": eng.use_graphs,
             "prefix_cache": not args.no_prefix_cache,
         },
@@ -165,8 +175,8 @@ def main() -> int:
         "p99_decision_latency_ms": round(1000 * sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))], 2),
         "decode_ms_per_step": round(dec_tok_ms, 3),
         "prefill_ms_per_decision": round(1000 * st["prefill_time"] / max(1, args.steps), 2),
-        "prefill_tokens_per_decision": round(st["prefill_tokens"] / max(1, decisions), 1),
-        "fallback_rate": round(fallbacks / decisions, 3),
+        "prefill_tokens_per_decision": round(st["prefill_tokens"] / max(1, args.steps * args.batch), 1),
+        "fallback_rate": round(fallbacks / (args.steps * args.batch), 3),
         "init_s": round(init_s, 1),
         "tp_comm": tp.comm_info,
         "baseline_note": "BASELINE.md publishes no numbers; vs_baseline uses the implied 0.3 decisions/s of test_e2e.py",
@@ -177,7 +187,7 @@ def main() -> int:
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    if tp.world > 1 and not tp.simulate:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
     return 0

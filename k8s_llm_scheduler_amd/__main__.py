@@ -35,25 +35,62 @@ def _fake_cluster(n: int):
     return FakeKubeAPI([make_node(nm, cpu="8", memory="16281924Ki") for nm in names], run_bound_pods=True)
 
 
-def build_backend(cfg: Config, metrics=None):
-    """Returns (backend, engine, tp) for this process."""
+class Runtime:
+    """What build_backend made for this process: the decision backend (rank 0), the engine, the
+    parallel layout and the links to the other engine replicas (data parallelism)."""
+
+    def __init__(self, backend=None, engine=None, tp=None, links=(), local=None):
+        self.backend, self.engine, self.tp, self.links, self.local = backend, engine, tp, list(links), local
+
+    @property
+    def is_control_rank(self) -> bool:
+        return self.tp is None or self.tp.global_rank == 0
+
+    def serve(self) -> None:
+        """Non-control ranks: a remote replica's leader answers rank 0's batches, every other
+        rank follows its replica leader's engine schedule."""
+        from .parallel.replicas import serve_replica
+
+        if self.tp.rank == 0 and self.links:
+            serve_replica(self.local, self.links[0], self.engine)
+        else:
+            self.engine.serve_worker()
+
+    def shutdown(self) -> None:
+        if self.is_control_rank:
+            if hasattr(self.router, "shutdown"):
+                self.router.shutdown()
+            if self.engine is not None:
+                self.engine.shutdown_workers()
+
+    router = None
+
+
+def build_backend(cfg: Config, metrics=None) -> Runtime:
     from .control.backends import LocalEngineBackend, ScriptedBackend, first_node_answer
 
     if not cfg.engine.enabled or cfg.engine.backend == "fallback":
-        return None, None, None
+        return Runtime()
     from .control.backends import FaultInjectingBackend
 
     if cfg.engine.backend == "scripted":
-        return FaultInjectingBackend.from_spec(ScriptedBackend(default=first_node_answer),
-                                               cfg.engine.fault_injection, cfg.engine.seed), None, None
+        return Runtime(FaultInjectingBackend.from_spec(ScriptedBackend(default=first_node_answer),
+                                                       cfg.engine.fault_injection, cfg.engine.seed))
     from .engine import engine_from_config
     from .parallel import init_from_env, make_control_channel
+    from .parallel.replicas import ReplicaRouterBackend, make_replica_links
 
-    tp = init_from_env()
+    tp = init_from_env(tp_size=cfg.engine.tp)
     control = make_control_channel(tp)
+    links = make_replica_links(tp)
     engine = engine_from_config(cfg, tp, metrics, control=control)
-    backend = LocalEngineBackend(engine, ignore_eos=cfg.engine.ignore_eos)
-    return FaultInjectingBackend.from_spec(backend, cfg.engine.fault_injection, cfg.engine.seed), engine, tp
+    local = LocalEngineBackend(engine, ignore_eos=cfg.engine.ignore_eos)
+    rt = Runtime(None, engine, tp, links, local)
+    backend = local
+    if tp.global_rank == 0 and links:
+        backend = rt.router = ReplicaRouterBackend(local, links)
+    rt.backend = FaultInjectingBackend.from_spec(backend, cfg.engine.fault_injection, cfg.engine.seed)
+    return rt
 
 
 def build_scheduler(cfg: Config, api, backend, metrics=None):
@@ -88,15 +125,17 @@ def cmd_run(args, cfg: Config) -> int:
     from .control.metrics import SchedulerMetrics
 
     metrics = SchedulerMetrics(cfg.metrics.enabled, cfg.metrics.port)
-    backend, engine, tp = build_backend(cfg, metrics)
-    if tp is not None and tp.rank != 0:
-        engine.serve_worker()   # follow rank 0 until it shuts down
+    rt = build_backend(cfg, metrics)
+    backend, engine, tp = rt.backend, rt.engine, rt.tp
+    if not rt.is_control_rank:
+        rt.serve()   # follow rank 0 until it shuts down
         return 0
     metrics.start()
     print(f" AI-Powered Kubernetes Scheduler with {cfg.llm.model.split('/')[-1]}")
     print("=" * 60)
     if engine is not None:
-        print(f"Local decision engine: {cfg.engine.preset} on MI355X, TP={tp.world if tp else 1}")
+        print(f"Local decision engine: {cfg.engine.preset} on MI355X, TP={tp.world if tp else 1}"
+              + (f" x {tp.replicas} replicas" if tp is not None and tp.replicas > 1 else ""))
     else:
         print(f"Decision backend: {cfg.engine.backend if cfg.engine.enabled else 'disabled (fallback only)'}")
     print(f"Model: {cfg.llm.model}")
@@ -128,8 +167,7 @@ def cmd_run(args, cfg: Config) -> int:
         print("\n\n⏹  Scheduler stopped by user")
     finally:
         sched.stop()
-        if engine is not None:
-            engine.shutdown_workers()
+        rt.shutdown()
         print_final_stats(sched.get_stats())
     return 0
 
@@ -190,8 +228,7 @@ def cmd_smoke(args, cfg: Config) -> int:
     pods = [it for d in docs for it in (d.get("items", []) if d.get("kind") == "List" else [d])]
     if args.fake_cluster:
         api = _fake_cluster(args.fake_cluster)
-        backend, engine, _ = build_backend(cfg) if cfg.engine.backend != "local" or args.with_engine else \
-            (None, None, None)
+        backend = build_backend(cfg).backend if cfg.engine.backend != "local" or args.with_engine else None
         sched = build_scheduler(cfg, api, backend)
 
         async def run():

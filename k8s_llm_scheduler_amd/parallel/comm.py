@@ -44,6 +44,15 @@ class TPGroup:
     simulate: bool = False          # shapes of a TP rank, collectives skipped (profiling only)
     xgmi: Optional[object] = None   # native XgmiComm: one-shot peer-memory collectives (small messages)
     comm_info: dict = field(default_factory=dict)
+    # Data parallelism over engine replicas (WORLD_SIZE = replicas x world): this rank is TP rank
+    # ``rank`` of replica ``replica``, whose TP rank 0 is global rank ``leader``.
+    replica: int = 0
+    replicas: int = 1
+    leader: int = 0
+
+    @property
+    def global_rank(self) -> int:
+        return self.leader + self.rank
 
     def _xgmi_ok(self, t: torch.Tensor) -> bool:
         n = t.numel() * t.element_size()
@@ -87,7 +96,7 @@ class TPGroup:
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world > 1:
-            dist.broadcast(t, src=src, group=self.group)
+            dist.broadcast(t, src=self.leader + src, group=self.group)
         return t
 
     def barrier(self) -> None:
@@ -96,30 +105,47 @@ class TPGroup:
 
 
 class ControlChannel:
-    """Rank 0 -> all ranks object broadcast on a CPU (gloo) group: the serving control plane runs
-    on rank 0 and every other TP rank follows its engine schedule (engine.LLMEngine._sync)."""
+    """TP-rank-0 -> replica object broadcast on a CPU (gloo) group: the replica's leader (global
+    rank 0 runs the serving control plane) announces new requests, every other TP rank of the
+    replica follows its engine schedule (engine.LLMEngine._sync)."""
 
-    def __init__(self, rank: int, group=None):
-        self.rank = rank
+    def __init__(self, rank: int, group=None, src: int = 0):
+        self.rank = rank      # TP rank within the replica
         self.group = group
+        self.src = src        # global rank of the replica's leader
 
     def exchange(self, payload):
         obj = [payload]
-        dist.broadcast_object_list(obj, src=0, group=self.group)
+        dist.broadcast_object_list(obj, src=self.src, group=self.group)
         return obj[0]
 
 
+def replica_ranks(tp: TPGroup, replica: int) -> list:
+    return list(range(replica * tp.world, (replica + 1) * tp.world))
+
+
 def make_control_channel(tp: TPGroup) -> Optional[ControlChannel]:
+    """Every rank must call this (torch.distributed.new_group is collective over the world)."""
     if tp.world <= 1 or tp.simulate:
         return None
-    grp = dist.new_group(backend="gloo", timeout=datetime.timedelta(days=7))
-    return ControlChannel(tp.rank, grp)
+    mine = None
+    for r in range(tp.replicas):
+        ranks = replica_ranks(tp, r) if tp.replicas > 1 else None
+        g = dist.new_group(ranks=ranks, backend="gloo", timeout=datetime.timedelta(days=7))
+        if r == tp.replica:
+            mine = g
+    return ControlChannel(tp.rank, mine, src=tp.leader)
 
 
 def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backend: Optional[str] = None,
-                  comm: Optional[str] = None) -> TPGroup:
+                  comm: Optional[str] = None, tp_size: int = 0) -> TPGroup:
     """Initialise torch.distributed from torchrun env (RANK/WORLD_SIZE/MASTER_*).  Single
     process when WORLD_SIZE is unset or 1.
+
+    ``tp_size`` (env ``K8S_TP``; 0 = WORLD_SIZE): tensor-parallel degree of one engine replica.
+    WORLD_SIZE / tp_size replicas of ranks [r*tp, (r+1)*tp) each hold a full model copy (data
+    parallelism over decisions, e.g. two TP=4 half-node engines on 8 GPUs); each replica gets its
+    own process group, RCCL communicator and xGMI peer regions.
 
     ``backend``: process-group backend (default ``nccl`` = RCCL on GPU, ``gloo`` on CPU; env
     ``K8S_TP_BACKEND``).  ``comm`` (env ``K8S_TP_COMM``): ``auto`` = RCCL plus the xGMI one-shot
@@ -130,6 +156,10 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backe
     rank = int(os.environ.get("RANK", "0"))
     if world <= 1:
         return TPGroup()
+    tp_size = int(tp_size or os.environ.get("K8S_TP", "0") or 0) or world
+    if tp_size < 1 or world % tp_size:
+        raise ValueError(f"WORLD_SIZE {world} is not a multiple of the TP degree {tp_size}")
+    replicas = world // tp_size
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     backend = backend or os.environ.get("K8S_TP_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
@@ -146,7 +176,17 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backe
                 kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    tp = TPGroup(rank, world, dist.group.WORLD, backend)
+    replica = rank // tp_size
+    group = dist.group.WORLD
+    if replicas > 1:   # collective: every rank creates every replica's group, in order
+        for r in range(replicas):
+            g = dist.new_group(ranks=list(range(r * tp_size, (r + 1) * tp_size)))
+            if r == replica:
+                group = g
+    tp = TPGroup(rank % tp_size, tp_size, group, backend, replica=replica, replicas=replicas,
+                 leader=replica * tp_size)
+    if tp_size == 1:
+        return tp   # pure data parallelism: no collectives inside the model
     if device_type == "cuda":
         if backend == "nccl" and comm in ("auto", "rccl"):
             tp.rccl = make_rccl_comm(tp)
@@ -168,7 +208,7 @@ def make_rccl_comm(tp: TPGroup):
     uid = torch.zeros(128, dtype=torch.uint8, device=dev)
     if tp.rank == 0:
         uid.copy_(torch.frombuffer(bytearray(_C.RcclComm.unique_id()), dtype=torch.uint8))
-    dist.broadcast(uid, src=0, group=tp.group)
+    dist.broadcast(uid, src=tp.leader, group=tp.group)
     comm = _C.RcclComm(tp.world, tp.rank, bytes(uid.cpu().tolist()))
     # one eager collective so lazy RCCL setup happens outside any graph capture
     probe = torch.ones(16, dtype=torch.float32, device=dev)

@@ -1,0 +1,105 @@
+"""Data parallelism over engine replicas on CPU (gloo): WORLD_SIZE = 4 as 2 replicas x TP=2.
+
+Rank 0 runs the router backend (the control plane's view), global rank 2 leads replica 1 and
+answers rank 0's share over its link, ranks 1 and 3 follow their leaders' engine schedules.  The
+texts must equal those of one TP=1 engine given the same requests (greedy decoding), in request
+order, and both replicas must have received work."""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from k8s_llm_scheduler_amd.control.backends import LocalEngineBackend
+from k8s_llm_scheduler_amd.control.decision import GenerationRequest
+from k8s_llm_scheduler_amd.engine import build_engine
+
+SYSTEM = "You are an intelligent Kubernetes scheduler. Respond only with valid JSON."
+USERS = [f"pod-{i} needs {i * 100}m cpu; nodes: kind-worker, kind-worker2" for i in range(5)]
+
+
+def _requests():
+    return [GenerationRequest(SYSTEM, u, max_tokens=6, temperature=0.0) for u in USERS]
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, tp_size, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from k8s_llm_scheduler_amd.parallel import init_from_env, make_control_channel
+    from k8s_llm_scheduler_amd.parallel.replicas import ReplicaRouterBackend, make_replica_links, serve_replica
+
+    try:
+        tp = init_from_env("cpu", backend="gloo", tp_size=tp_size)
+        control = make_control_channel(tp)
+        links = make_replica_links(tp)
+        eng = build_engine("tiny", tp=tp, device="cpu", max_batch=4, max_model_len=512, num_blocks=128, seed=1,
+                           control=control)
+        local = LocalEngineBackend(eng, ignore_eos=True)
+        if tp.global_rank == 0:
+            router = ReplicaRouterBackend(local, links)
+            texts = router.complete(_requests())
+            again = router.complete(_requests()[:1])      # a lone request stays on replica 0
+            router.shutdown()
+            eng.shutdown_workers()
+            q.put(("router", texts, again, list(router.dispatched), (tp.replica, tp.replicas, tp.world)))
+        elif tp.rank == 0:
+            serve_replica(local, links[0], eng)
+            q.put(("leader", tp.replica, tp.global_rank))
+        else:
+            eng.serve_worker()
+            q.put(("follower", tp.replica, tp.global_rank))
+    except BaseException as e:  # noqa: BLE001
+        import traceback
+
+        q.put(("error", rank, traceback.format_exc()))
+        raise
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_two_replicas_of_tp2_match_single_engine():
+    eng = build_engine("tiny", device="cpu", max_batch=4, max_model_len=512, num_blocks=128, seed=1)
+    want = LocalEngineBackend(eng, ignore_eos=True).complete(_requests())
+
+    world, tp_size = 4, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, tp_size, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    errors = [g for g in got if g[0] == "error"]
+    assert not errors, errors[0][2]
+    assert all(p.exitcode == 0 for p in procs)
+    router = next(g for g in got if g[0] == "router")
+    _, texts, again, dispatched, layout = router
+    assert layout == (0, 2, 2)
+    assert texts == want
+    assert again == want[:1]
+    assert dispatched == [3 + 1, 2]          # round-robin deal: requests 0,2,4 local, 1,3 remote
+    assert sorted(g[0] for g in got) == ["follower", "follower", "leader", "router"]
+
+
+def test_world_not_multiple_of_tp_is_rejected(monkeypatch):
+    from k8s_llm_scheduler_amd.parallel import init_from_env
+
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("RANK", "0")
+    with pytest.raises(ValueError):
+        init_from_env("cpu", backend="gloo", tp_size=3)
