@@ -34,6 +34,7 @@ void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int* splits_ou
 int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out,
                  int K, int epi, const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
 int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s);
+int k8s_quantize_act_fp8(void* q, float* scale, const void* x, int T, int K, hipStream_t s);
 int k8s_dequant_fp8_rows(void* w, const void* q, const float* scale, int N, int K, hipStream_t s);
 int k8s_skinny_supported(int M, int N_out, int K);
 long long k8s_skinny_workspace(int M, int N_out, int epi);
@@ -120,6 +121,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("quantize_fp8_rows", [](uintptr_t q, uintptr_t scale, uintptr_t w, int N, int K, int64_t s) {
     check(k8s_quantize_fp8_rows(P(q), P<float>(scale), P(w), N, K, S(s)), "quantize_fp8_rows");
+  });
+  m.def("quantize_act_fp8", [](uintptr_t q, uintptr_t scale, uintptr_t x, int T, int K, int64_t s) {
+    check(k8s_quantize_act_fp8(P(q), P<float>(scale), P(x), T, K, S(s)), "quantize_act_fp8");
   });
   m.def("dequant_fp8_rows", [](uintptr_t w, uintptr_t q, uintptr_t scale, int N, int K, int64_t s) {
     check(k8s_dequant_fp8_rows(P(w), P(q), P<float>(scale), N, K, S(s)), "dequant_fp8_rows");

@@ -69,9 +69,72 @@ __global__ void dequant_fp8_rows_kernel(bf16_t* __restrict__ w, const uint8_t* _
   reinterpret_cast<u32x4*>(w)[2 * i + 1] = o1;
 }
 
+// K16: per-token activation quantization for the fp8 prefill GEMMs (hipBLASLt fp8 MFMA with
+// row-wise scales): one workgroup per row, the row kept in registers between the absmax and the
+// conversion (one read of x).  sx[t] = max|x[t]| / 448, xq[t, k] = e4m3(x[t, k] / sx[t]).
+template <int VPT>
+__global__ void __launch_bounds__(256) quantize_act_fp8_kernel(uint8_t* __restrict__ q, float* __restrict__ scale,
+                                                               const bf16_t* __restrict__ x, int K) {
+  __shared__ float red[16];
+  const int t = blockIdx.x;
+  const u32x4* row = reinterpret_cast<const u32x4*>(x + (size_t)t * K);
+  const int nvec = K / 16;  // 16 elements per thread-item
+  u32x4 va[VPT], vb[VPT];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * 256;
+    if (c < nvec) {
+      va[i] = row[2 * c];
+      vb[i] = row[2 * c + 1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        amax = fmaxf(amax, fmaxf(fabsf(lo_bf(va[i][j])), fabsf(hi_bf(va[i][j]))));
+        amax = fmaxf(amax, fmaxf(fabsf(lo_bf(vb[i][j])), fabsf(hi_bf(vb[i][j]))));
+      }
+    }
+  }
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float s = m > 0.f ? m / FP8_MAX : 1.f;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[t] = s;
+  auto cl = [&](float v) { return fminf(fmaxf(v * inv, -FP8_MAX), FP8_MAX); };
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * 256;
+    if (c < nvec) {
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const u32x4& src = j < 2 ? va[i] : vb[i];
+        const uint32_t d0 = src[(2 * j) & 3], d1 = src[(2 * j + 1) & 3];
+        int packed = __builtin_amdgcn_cvt_pk_fp8_f32(cl(lo_bf(d0)), cl(hi_bf(d0)), 0, false);
+        packed = __builtin_amdgcn_cvt_pk_fp8_f32(cl(lo_bf(d1)), cl(hi_bf(d1)), packed, true);
+        o[j] = (uint32_t)packed;
+      }
+      reinterpret_cast<u32x4*>(q + (size_t)t * K)[c] = o;
+    }
+  }
+}
+
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+extern "C" int k8s_quantize_act_fp8(void* q, float* scale, const void* x, int T, int K, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (K <= 0 || K % 16 != 0 || K > 16 * 256 * 8) return -1;
+  const int vpt = (K / 16 + 255) / 256;
+  auto* qq = static_cast<uint8_t*>(q);
+  auto* xx = static_cast<const bf16_t*>(x);
+  if (vpt <= 2) quantize_act_fp8_kernel<2><<<T, 256, 0, s>>>(qq, scale, xx, K);
+  else if (vpt <= 4) quantize_act_fp8_kernel<4><<<T, 256, 0, s>>>(qq, scale, xx, K);
+  else quantize_act_fp8_kernel<8><<<T, 256, 0, s>>>(qq, scale, xx, K);
+  return (int)hipGetLastError();
+}
 
 extern "C" int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s) {
   if (N <= 0 || K <= 0 || K % 16 != 0) return -1;

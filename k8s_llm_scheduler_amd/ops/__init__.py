@@ -50,7 +50,7 @@ def available() -> bool:
 class Fp8Weight:
     """Row-scaled OCP e4m3 weight (fp8.hip): ``q`` [N, K] uint8 bit patterns, ``scale`` [N] fp32,
     w ~= e4m3(q) * scale[:, None].  Decode GEMVs stream ``q`` directly (half the HBM bytes of
-    bf16); prefill GEMMs dequantize to a bf16 scratch copy for the library GEMM."""
+    bf16); prefill GEMMs quantize the activations per token and run the row-scaled fp8 GEMM."""
 
     __slots__ = ("q", "scale")
 
@@ -99,6 +99,27 @@ def quantize_fp8(w: torch.Tensor) -> Fp8Weight:
     s = torch.empty(N, dtype=F32, device=w.device)
     native().quantize_fp8_rows(q.data_ptr(), s.data_ptr(), _chk(w, BF16, "w"), N, K, -1)
     return Fp8Weight(q, s)
+
+
+def quantize_act_fp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-token (row) activation quantization: bf16 [T, K] -> (e4m3 bytes [T, K], scale [T] f32)."""
+    if not x.is_cuda:
+        return ref.quantize_fp8(x)
+    T, K = x.shape
+    q = torch.empty(T, K, dtype=torch.uint8, device=x.device)
+    s = torch.empty(T, dtype=F32, device=x.device)
+    native().quantize_act_fp8(q.data_ptr(), s.data_ptr(), _chk(x, BF16, "x"), T, K, -1)
+    return q, s
+
+
+def _fp8_gemm(x: torch.Tensor, w: "Fp8Weight", out_dtype=None) -> torch.Tensor:
+    """Prefill / batched-decode projection with fp8 weights: per-token e4m3 activations (hand-written
+    quantization kernel) x row-scaled e4m3 weights on the fp8 MFMA path of hipBLASLt (row-wise
+    scaled GEMM), bf16 out.  Reads 1 byte per weight instead of dequantizing to a bf16 copy."""
+    xq, sx = quantize_act_fp8(x.contiguous())
+    f8 = torch.float8_e4m3fn
+    return torch._scaled_mm(xq.view(f8), w.q.view(f8).t(), scale_a=sx.view(-1, 1), scale_b=w.scale.view(1, -1),
+                            out_dtype=out_dtype or BF16)
 
 
 def _is_fp8(w) -> bool:
@@ -239,11 +260,6 @@ def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0
     return out
 
 
-def _lib_weight(w) -> torch.Tensor:
-    """Weight for a library GEMM: fp8 weights are dequantized to a bf16 scratch copy."""
-    return w.dequant() if _is_fp8(w) else w
-
-
 _NUM_CUS = {}
 
 
@@ -285,8 +301,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
         y = _gemv(x2.contiguous(), w, EPI_F32 if out_dtype == F32 else EPI_BF16, out_dtype or BF16)
     elif _use_skinny(x2.shape[0], w, x2.shape[1]):
         y = _skinny(x2.contiguous(), w, EPI_F32 if out_dtype == F32 else EPI_BF16, out_dtype or BF16)
+    elif _is_fp8(w):
+        y = _fp8_gemm(x2, w, out_dtype)
     else:
-        y = torch.nn.functional.linear(x2, _lib_weight(w))
+        y = torch.nn.functional.linear(x2, w)
         if out_dtype is not None and out_dtype != y.dtype:
             y = y.to(out_dtype)
     return y.view(*x.shape[:-1], y.shape[-1])
@@ -373,8 +391,10 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
         y = _gemv(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
     elif _use_skinny(x2.shape[0], w_gate_up, x2.shape[1]):
         y = _skinny(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
+    elif _is_fp8(w_gate_up):
+        y = silu_mul(_fp8_gemm(x2, w_gate_up))
     else:
-        y = silu_mul(torch.nn.functional.linear(x2, _lib_weight(w_gate_up)))
+        y = silu_mul(torch.nn.functional.linear(x2, w_gate_up))
     return y.view(*x.shape[:-1], y.shape[-1])
 
 

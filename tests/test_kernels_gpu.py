@@ -372,3 +372,34 @@ def test_decode_attention_split_graph_replay_rearms_counters(monkeypatch):
     torch.cuda.synchronize()
     for o in outs:
         close(o, want, 2e-2)
+
+
+@pytest.mark.parametrize("T,K", [(1, 8192), (300, 1024), (37, 3584), (5, 28672)])
+def test_quantize_act_fp8_matches_reference(T, K):
+    x = rnd(T, K, scale=2.0)
+    q, s = ops.quantize_act_fp8(x)
+    q_ref, s_ref = ref.quantize_fp8(x.cpu())
+    torch.testing.assert_close(s.cpu(), s_ref, rtol=1e-6, atol=0)
+    a = q.cpu().view(torch.float8_e4m3fn).float()
+    b = q_ref.view(torch.float8_e4m3fn).float()
+    diff = (a - b).abs()
+    assert float((diff > 0).float().mean()) < 1e-3          # rounding ties only
+    assert float((diff / b.abs().clamp_min(2 ** -6)).max()) <= 0.125 + 1e-6
+
+
+@pytest.mark.parametrize("M", [9, 64, 300])
+@pytest.mark.parametrize("N,K", [(2560, 8192), (8192, 2048), (96, 512)])
+def test_fp8_prefill_gemm(M, N, K):
+    """Prefill / batched decode with fp8 weights: per-token e4m3 activations x row-scaled e4m3
+    weights (fp8 MFMA GEMM) against the fp32 product of the dequantized weights."""
+    x = rnd(M, K)
+    w = ops.quantize_fp8(rnd(N, K, scale=0.05))
+    want = x.float().cpu() @ ref.dequant_fp8(w.q.cpu(), w.scale.cpu()).T
+    got = ops.linear(x, w)
+    rel = float((got.float().cpu() - want).abs().max() / want.abs().max())
+    assert rel < 0.06, rel                                   # e4m3 activations: ~2^-4 relative
+    gu = ops.quantize_fp8(rnd(2 * N, K, scale=0.05))
+    want_gu = ref.linear_swiglu(x.cpu().float(), ref.dequant_fp8(gu.q.cpu(), gu.scale.cpu()))
+    got_gu = ops.linear_swiglu(x, gu)
+    rel = float((got_gu.float().cpu() - want_gu.float()).abs().max() / want_gu.float().abs().max())
+    assert rel < 0.08, rel
