@@ -222,7 +222,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rank", &XgmiComm::rank)
       .def_property_readonly("slot_bytes", &XgmiComm::slot_bytes)
       .def_property_readonly("blocks", &XgmiComm::blocks)
-      .def_property_readonly("is_open", &XgmiComm::is_open);
+      .def_property_readonly("is_open", &XgmiComm::is_open)
+      .def_property("ll_max_bytes", &XgmiComm::ll_max_bytes, &XgmiComm::set_ll_max_bytes);
 
   using k8sllm::BlockAllocator;
   py::class_<BlockAllocator::Allocation>(m, "Allocation")

@@ -127,6 +127,67 @@ __global__ __launch_bounds__(XG_THREADS) void xg_allreduce_bf16_kernel(XgArgs a)
   }
 }
 
+// LL ("low-latency") all-reduce for decode-size messages: the flag travels WITH the data.  Every
+// 4-byte word (two bf16) is pushed as one 8-byte store {word, epoch} into row `rank` of slot (e & 1)
+// at every peer; a reader polls each peer's 8-byte word until its high half equals e, so there is
+// no separate flag store, no workgroup barrier and no second fabric crossing between the data and
+// its readiness.  8-byte stores arrive untorn (MI355X_MICROARCH.md visibility notes).  The rows
+// hold 2x the payload bytes.  Slot reuse is safe for the same reason as in the flagged kernel.
+template <int W>
+__global__ __launch_bounds__(XG_THREADS) void xg_allreduce_ll_kernel(XgArgs a) {
+  typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+  const uint32_t e = xg_epoch(a);
+  const long long nwords = a.bytes >> 2;
+  const long long my_row = XG_FLAG_BYTES + ((long long)(e & 1) * W + a.rank) * a.slot_bytes;
+  const long long slot0 = XG_FLAG_BYTES + (long long)(e & 1) * W * a.slot_bytes;
+  const uint32_t* in = reinterpret_cast<const uint32_t*>(a.in);
+  uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
+  const long long stride = (long long)gridDim.x * XG_THREADS;
+  for (long long v = (long long)blockIdx.x * XG_THREADS + threadIdx.x; v < nwords; v += stride) {
+    const uint32_t mine = in[v];
+    const u32x2 word = u32x2{mine, e};
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      if (p == a.rank) continue;
+      __builtin_amdgcn_raw_buffer_store_b64(word, xg_rsrc(a.base[p] + my_row, a.slot_bytes), (int)(v << 3), 0, XG_SYS);
+    }
+  }
+  for (long long v = (long long)blockIdx.x * XG_THREADS + threadIdx.x; v < nwords; v += stride) {
+    uint32_t d[W];
+    u32x2 w[W];
+#pragma unroll
+    for (int t = 0; t < W; ++t)
+      if (t != a.rank)
+        w[t] = __builtin_amdgcn_raw_buffer_load_b64(xg_rsrc(a.base[a.rank] + slot0 + t * a.slot_bytes, a.slot_bytes),
+                                                    (int)(v << 3), 0, XG_SYS);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (int t = 0; t < W; ++t) {
+      if (t == a.rank) {
+        d[t] = in[v];
+        continue;
+      }
+      while (w[t].y != e) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+          __hip_atomic_fetch_or(a.err, 1u << t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        w[t] = __builtin_amdgcn_raw_buffer_load_b64(xg_rsrc(a.base[a.rank] + slot0 + t * a.slot_bytes, a.slot_bytes),
+                                                    (int)(v << 3), 0, XG_SYS);
+      }
+      d[t] = w[t].x;
+    }
+    float lo = 0.f, hi = 0.f;
+#pragma unroll
+    for (int t = 0; t < W; ++t) {  // fixed rank order: bit-identical on every rank
+      lo += lo_bf(d[t]);
+      hi += hi_bf(d[t]);
+    }
+    out[v] = pack_bf2(lo, hi);
+  }
+}
+
 // out[t * bytes ...] = contribution of rank t (shard-major), any dtype.
 __global__ __launch_bounds__(XG_THREADS) void xg_allgather_kernel(XgArgs a) {
   const uint32_t e = xg_epoch(a);
@@ -177,6 +238,26 @@ extern "C" int k8s_xgmi_allreduce_bf16(void* const* bases, uint32_t* counters, u
     case 5: xg_allreduce_bf16_kernel<5><<<blocks, XG_THREADS, 0, s>>>(a); break;
     case 6: xg_allreduce_bf16_kernel<6><<<blocks, XG_THREADS, 0, s>>>(a); break;
     case 7: xg_allreduce_bf16_kernel<7><<<blocks, XG_THREADS, 0, s>>>(a); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int k8s_xgmi_allreduce_ll_bf16(void* const* bases, uint32_t* counters, uint32_t* err, const void* in,
+                                          void* out, long long bytes, long long slot_bytes, int rank, int world,
+                                          int blocks, long long timeout_ticks, hipStream_t s) {
+  XgArgs a;
+  if (2 * bytes > slot_bytes) return -2;  // LL rows carry a flag word per data word
+  if (int rc = xg_fill(a, bases, counters, err, in, out, bytes, slot_bytes, rank, world, timeout_ticks)) return rc;
+  if (blocks < 1 || blocks > XG_MAX_BLOCKS) return -4;
+  switch (world) {
+    case 2: xg_allreduce_ll_kernel<2><<<blocks, XG_THREADS, 0, s>>>(a); break;
+    case 4: xg_allreduce_ll_kernel<4><<<blocks, XG_THREADS, 0, s>>>(a); break;
+    case 8: xg_allreduce_ll_kernel<8><<<blocks, XG_THREADS, 0, s>>>(a); break;
+    case 3: xg_allreduce_ll_kernel<3><<<blocks, XG_THREADS, 0, s>>>(a); break;
+    case 5: xg_allreduce_ll_kernel<5><<<blocks, XG_THREADS, 0, s>>>(a); break;
+    case 6: xg_allreduce_ll_kernel<6><<<blocks, XG_THREADS, 0, s>>>(a); break;
+    case 7: xg_allreduce_ll_kernel<7><<<blocks, XG_THREADS, 0, s>>>(a); break;
     default: return -1;
   }
   return (int)hipGetLastError();

@@ -29,6 +29,9 @@ class XgmiComm {
   long long slot_bytes() const { return slot_bytes_; }
   int blocks() const { return blocks_; }
   bool is_open() const { return opened_; }
+  // Messages up to this size use the LL protocol (flag in every 8-byte word); 0 disables it.
+  long long ll_max_bytes() const { return ll_max_bytes_; }
+  void set_ll_max_bytes(long long b) { ll_max_bytes_ = b; }
 
  private:
   int world_, rank_, blocks_;
@@ -39,6 +42,7 @@ class XgmiComm {
   std::vector<void*> bases_;    // every rank's region in this address space
   std::vector<bool> mapped_;    // true where bases_[i] came from hipIpcOpenMemHandle
   bool opened_ = false;
+  long long ll_max_bytes_ = 64 * 1024;
 };
 
 }  // namespace k8sllm

@@ -241,6 +241,7 @@ def make_xgmi_comm(tp: TPGroup, slot_bytes: Optional[int] = None, blocks: Option
         if tp.world > 8:
             raise RuntimeError("more than 8 ranks")
         comm = ops.native().XgmiComm(tp.world, tp.rank, slot_bytes, blocks, timeout_s)
+        comm.ll_max_bytes = int(os.environ.get("K8S_XGMI_LL_MAX", 64 * 1024))
         handle = comm.handle()
     except Exception as e:  # noqa: BLE001 -- every rank must still join the exchange below
         err = str(e)
@@ -268,8 +269,11 @@ def make_xgmi_comm(tp: TPGroup, slot_bytes: Optional[int] = None, blocks: Option
 
 def _xgmi_selftest(tp: TPGroup, comm, dev) -> bool:
     try:
-        n = min(comm.slot_bytes // 2, 64 * 1024)
-        for it in range(3):  # both slots, then the first again
+        sizes = [min(comm.slot_bytes // 2, 64 * 1024)]               # flagged one-shot path
+        if comm.ll_max_bytes >= 2:
+            sizes.append(min(comm.ll_max_bytes, comm.slot_bytes // 2) // 2)  # LL path (flag in every word)
+        for it in range(3 * len(sizes)):  # both slots, then the first again, for every path
+            n = sizes[it % len(sizes)]
             x = (torch.arange(n, device=dev, dtype=torch.float32) % 61 + tp.rank * 3 + it).to(torch.bfloat16)
             want = sum((torch.arange(n, device=dev, dtype=torch.float32) % 61 + r * 3 + it) for r in range(tp.world))
             comm.all_reduce_bf16(x.data_ptr(), x.data_ptr(), n * 2, -1)

@@ -61,6 +61,18 @@ def _worker(rank, world, port, q):
             torch.cuda.synchronize()
             assert torch.equal(y.cpu(), want), f"all_reduce n={n}"
             assert torch.equal(x.cpu(), want), f"in-place all_reduce n={n}"
+        # the same sizes with the LL protocol off (flagged one-shot kernel for every size)
+        ll = xg.ll_max_bytes
+        xg.ll_max_bytes = 0
+        for seed, n in enumerate([8, 520, 8192]):
+            x = _data(rank, n, seed).cuda()
+            want = sum(_data(r, n, seed).float() for r in range(world)).to(torch.bfloat16)
+            tp.all_reduce_(x)
+            torch.cuda.synchronize()
+            assert torch.equal(x.cpu(), want), f"flagged all_reduce n={n}"
+        res["graph_us_16k_flagged"] = _graph_time_us(
+            lambda: xg.all_reduce_bf16(x.data_ptr(), x.data_ptr(), 16384, -1)) if x.numel() * 2 >= 16384 else 0.0
+        xg.ll_max_bytes = ll
         # all-gather (fp32 logits layout, shard-major)
         for n in (4, 4096, 16032 * 4):
             src = torch.arange(n, dtype=torch.float32, device="cuda") + 1e6 * rank
@@ -153,7 +165,8 @@ def test_xgmi_two_ranks_one_gpu():
     assert not fails, "\n".join(f"rank {r}:\n{tb}" for r, tb in fails.items())
     assert len(got) == WORLD, f"ranks finished: {sorted(got)}, exit codes {[p.exitcode for p in procs]}"
     r0, r1 = got[0][1], got[1][1]
-    print(f"xgmi all-reduce 16 KiB (2 ranks sharing one GPU): {r0['graph_us_16k']:.1f} us; "
+    print(f"xgmi all-reduce 16 KiB (2 ranks sharing one GPU): LL {r0['graph_us_16k']:.1f} us, "
+          f"flagged {r0['graph_us_16k_flagged']:.1f} us; "
           f"TP2 vs TP1 max |d logit| prefill {r0['prefill_err']:.3g} decode {r0['decode_err']:.3g} "
           f"(scale {r0['logit_scale']:.3g})")
     assert r0["err"] == 0 and r1["err"] == 0
