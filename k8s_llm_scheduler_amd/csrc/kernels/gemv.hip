@@ -106,6 +106,27 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
     wrow[r] = Wb + ((size_t)n * K + kb) * WB;
     if (EPI == EPI_SWIGLU) wrow[RPW + r] = Wb + ((size_t)(n + half_rows) * K + kb) * WB;
   }
+  // NORM: the norm weights and the first NL row chunks of x (+ res_in) per thread are loaded BEFORE
+  // the weight stream: vmcnt retires in order, so the prologue's waits then do not sit behind the
+  // weights' HBM latency and the reduction overlaps the first weight round trip
+  constexpr int NL = M <= 2 ? 4 : (M <= 4 ? 2 : 1);
+  constexpr int GI = 4;  // norm-weight chunks per thread held in registers (xch <= 1024)
+  const int nkc = K >> 3;
+  u32x4 g[GI];
+  u32x4 pre[NL][M];
+  if (NORM) {
+#pragma unroll
+    for (int i = 0; i < GI; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (c < xch) g[i] = reinterpret_cast<const u32x4*>(nw + kb)[c];
+    }
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int c = min((int)threadIdx.x + u * (int)blockDim.x, nkc - 1);
+#pragma unroll
+      for (int m = 0; m < M; ++m) norm_row_chunk<M>(x, res_in, m, K, c, pre[u][m]);
+    }
+  }
   // weights do not depend on x: start streaming them before the x staging / norm prologue
   u32x4 wv[U][NR];
 #pragma unroll
@@ -120,27 +141,25 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
     // after the reduction the slice is normalised in place in LDS (no second global read).
     const bool writer = blockIdx.x == 0 && blockIdx.y == 0 && res_out != nullptr;
     const int kc0 = kb >> 3;
-    constexpr int GI = 4;  // norm-weight chunks per thread held in registers (xch <= 1024)
-    u32x4 g[GI];
-#pragma unroll
-    for (int i = 0; i < GI; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      if (c < xch) g[i] = reinterpret_cast<const u32x4*>(nw + kb)[c];
-    }
     float ss[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = 0.f;
-    // NL row chunks per thread are loaded before any is consumed: at K = 8192 and M <= 2 the
-    // whole row is ONE round trip (the prologue sits on every workgroup's critical path)
-    constexpr int NL = M <= 2 ? 4 : (M <= 4 ? 2 : 1);
-    const int nkc = K >> 3;
+    // NL row chunks per thread per pass, all loaded before any is consumed (the first pass was
+    // issued before the weight stream): at K = 8192 and M <= 2 the whole row is ONE pass
     for (int c0 = threadIdx.x; c0 < nkc; c0 += blockDim.x * NL) {
       u32x4 r[NL][M];
+      if (c0 == (int)threadIdx.x) {
 #pragma unroll
-      for (int u = 0; u < NL; ++u) {
-        const int c = min(c0 + u * (int)blockDim.x, nkc - 1);
+        for (int u = 0; u < NL; ++u)
 #pragma unroll
-        for (int m = 0; m < M; ++m) norm_row_chunk<M>(x, res_in, m, K, c, r[u][m]);
+          for (int m = 0; m < M; ++m) r[u][m] = pre[u][m];
+      } else {
+#pragma unroll
+        for (int u = 0; u < NL; ++u) {
+          const int c = min(c0 + u * (int)blockDim.x, nkc - 1);
+#pragma unroll
+          for (int m = 0; m < M; ++m) norm_row_chunk<M>(x, res_in, m, K, c, r[u][m]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < NL; ++u) {
