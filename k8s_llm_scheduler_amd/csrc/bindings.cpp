@@ -41,6 +41,8 @@ long long k8s_skinny_workspace(int M, int N_out, int epi);
 int k8s_skinny_gemm(void* out, void* workspace, const void* x, const void* W, int M, int N_out, int K, int epi,
                     int num_cus, hipStream_t s);
 int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi, hipStream_t s);
+int k8s_gemv_rms(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out, int K,
+                 int epi, const void* res_in, void* res_out, float eps, hipStream_t s);
 int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi,
                   const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
 int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const void* qkv, const float* cos_sin,
@@ -140,6 +142,11 @@ PYBIND11_MODULE(_C, m) {
                         uintptr_t res_in, uintptr_t res_out, uintptr_t nw, float eps, int64_t s) {
     check(k8s_gemv_norm(P(out), P(partial), P(x), P(W), M, N, K, epi, P(res_in), P(res_out), P(nw), eps, S(s)),
           "gemv_norm");
+  });
+  m.def("gemv_rms", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, uintptr_t wscale, int M, int N,
+                       int K, int epi, uintptr_t res_in, uintptr_t res_out, float eps, int64_t s) {
+    check(k8s_gemv_rms(P(out), P(partial), P(x), P(W), P<float>(wscale), M, N, K, epi, P(res_in), P(res_out), eps, S(s)),
+          "gemv_rms");
   });
   m.def("decode_attention_fused", [](uintptr_t out, uintptr_t pacc, uintptr_t pml, uintptr_t qkv, uintptr_t cos_sin,
                                      uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx, float scale, int B, int nq,

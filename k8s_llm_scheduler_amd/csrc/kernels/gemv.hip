@@ -73,8 +73,12 @@ __device__ __forceinline__ void norm_row_chunk(const bf16_t* __restrict__ x, con
   for (int j = 0; j < 4; ++j) r[j] = pack_bf2(lo_bf(a[j]) + lo_bf(b[j]), hi_bf(a[j]) + hi_bf(b[j]));
 }
 
-template <int M, int RPW, int EPI, bool NORM, bool FP8, int KW>
-__global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float* __restrict__ partial,
+// NORM: 0 = plain input x; 1 = rmsnorm(x + res_in) * nw applied in the prologue; 2 = the norm weight is
+// folded into W (W' = W * nw, done once at model load): the prologue only stages r = x + res_in and
+// its sum of squares, and the per-row 1/rms scales the accumulator in the epilogue -- no
+// normalisation pass and no barrier between the row statistics and the weight stream.
+template <int M, int RPW, int EPI, int NORM, bool FP8, int KW, int NT = 256>
+__global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float* __restrict__ partial,
                                                    const bf16_t* __restrict__ x, const void* __restrict__ W,
                                                    int N_out, int K, int KS, int half_rows,
                                                    const bf16_t* __restrict__ res_in, bf16_t* __restrict__ res_out,
@@ -84,7 +88,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
   constexpr int WB = FP8 ? 1 : 2;    // bytes per weight
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u32x4* xs = reinterpret_cast<u32x4*>(smem);  // [M][KS/8]
-  __shared__ float nred[4][M];
+  constexpr int NWV = NT / 64;  // waves per workgroup; NWV / KW row sets
+  __shared__ float nred[NWV][M];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int kb = blockIdx.y * KS;
   const int klen = min(KS, K - kb);
@@ -93,7 +98,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
 
   constexpr int NR = (EPI == EPI_SWIGLU) ? 2 * RPW : RPW;  // weight rows per wave
   constexpr int U = (NR >= 4) ? 2 : ((NR >= 2) ? 4 : 8);  // chunks per lane in flight per row
-  const int r0 = (blockIdx.x * (4 / KW) + wid / KW) * RPW;  // first output row of this wave
+  const int r0 = (blockIdx.x * (NWV / KW) + wid / KW) * RPW;  // first output row of this wave
   const bool active = r0 < N_out;
   const int kpart = wid % KW;                                // this wave's share of the K chunks
   const int per = (nch + KW - 1) / KW;
@@ -110,14 +115,15 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
   // the weight stream: vmcnt retires in order, so the prologue's waits then do not sit behind the
   // weights' HBM latency and the reduction overlaps the first weight round trip
   constexpr int NL = M <= 2 ? 4 : (M <= 4 ? 2 : 1);
-  constexpr int GI = 4;  // norm-weight chunks per thread held in registers (xch <= 1024)
+  constexpr int GI = (1024 + NT - 1) / NT;  // norm-weight chunks per thread held in registers (xch <= 1024)
   const int nkc = K >> 3;
   u32x4 g[GI];
   u32x4 pre[NL][M];
-  if (NORM) {
+  if (NORM != 0) {
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
-      const int c = threadIdx.x + 256 * i;
+      if (NORM != 1) break;
+      const int c = threadIdx.x + NT * i;
       if (c < xch) g[i] = reinterpret_cast<const u32x4*>(nw + kb)[c];
     }
 #pragma unroll
@@ -135,7 +141,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
     for (int r = 0; r < NR; ++r)
       wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + min(cb + lane + 64 * u, clast));
 
-  if (NORM) {
+  float inv[M];
+  if (NORM != 0) {
     // One global pass: r = x + res_in over the whole row (the sum of squares needs all of it),
     // this slice of r parked in LDS, this thread's norm-weight chunks prefetched into registers;
     // after the reduction the slice is normalised in place in LDS (no second global read).
@@ -183,13 +190,19 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
       const float t = wave_sum(ss[m]);
       if (lane == 0) nred[wid][m] = t;
     }
+  }
+  if (NORM == 1) {
     __syncthreads();
-    float inv[M];
 #pragma unroll
-    for (int m = 0; m < M; ++m) inv[m] = rsqrtf((nred[0][m] + nred[1][m] + nred[2][m] + nred[3][m]) / (float)K + eps);
+    for (int m = 0; m < M; ++m) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) t += nred[w][m];
+      inv[m] = rsqrtf(t / (float)K + eps);
+    }
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
-      const int c = threadIdx.x + 256 * i;
+      const int c = threadIdx.x + NT * i;
       if (c >= xch) break;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
@@ -201,7 +214,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
         xs[m * (KS >> 3) + c] = o;
       }
     }
-    for (int c = threadIdx.x + 256 * GI; c < xch; c += blockDim.x) {  // slices longer than 8192
+    for (int c = threadIdx.x + NT * GI; c < xch; c += blockDim.x) {  // slices longer than 8192
       const u32x4 gw = reinterpret_cast<const u32x4*>(nw + kb)[c];
 #pragma unroll
       for (int m = 0; m < M; ++m) {
@@ -213,7 +226,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
         xs[m * (KS >> 3) + c] = o;
       }
     }
-  } else {
+  } else if (NORM == 0) {
     // stage x[:, kb:kb+klen] into LDS
     for (int i = threadIdx.x; i < M * xch; i += blockDim.x) {
       const int m = i / xch, c = i - m * xch;
@@ -268,7 +281,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
     for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
 
   if (KW > 1) {  // combine the K parts of the waves sharing these rows
-    __shared__ float kred[4][NR][M];
+    __shared__ float kred[NWV][NR][M];
     if (lane == 0) {
 #pragma unroll
       for (int r = 0; r < NR; ++r)
@@ -287,6 +300,19 @@ __global__ void __launch_bounds__(256) gemv_kernel(void* __restrict__ out, float
     return;
   }
   const int wrows = (EPI == EPI_SWIGLU) ? 2 * half_rows : N_out;  // weight rows (slab width)
+  if (NORM == 2) {  // 1/rms of each input row (the statistics are in LDS since the pre-loop barrier)
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) t += nred[w][m];
+      inv[m] = rsqrtf(t / (float)K + eps);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int m = 0; m < M; ++m) acc[r][m] *= inv[m];
+  }
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int n = r0 + r;
@@ -362,9 +388,10 @@ extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int
 // partial: fp32 workspace of splits * M * wrows floats (wrows = N_out, or 2*N_out for SWIGLU);
 // may be null when the plan has a single split.
 // wscale != null: W is fp8 (OCP e4m3, one fp32 scale per weight row); K must be a multiple of 16.
-extern "C" int k8s_gemv_norm_w(void* out, void* partial, const void* x, const void* W, const float* wscale, int M,
-                               int N_out, int K, int epi, const void* res_in, void* res_out, const void* nw,
-                               float eps, hipStream_t stream) {
+// mode: 0 plain, 1 norm weight nw applied in the prologue, 2 norm weight folded into W (nw unused)
+static int gemv_launch(int mode, void* out, void* partial, const void* x, const void* W, const float* wscale, int M,
+                       int N_out, int K, int epi, const void* res_in, void* res_out, const void* nw, float eps,
+                       hipStream_t stream) {
   if (M < 1 || M > 8 || K % 8 != 0 || N_out <= 0) return -1;
   const bool fp8 = wscale != nullptr;
   if (fp8 && K % 16 != 0) return -1;
@@ -381,12 +408,15 @@ extern "C" int k8s_gemv_norm_w(void* out, void* partial, const void* x, const vo
   if (kw_env == 1 || kw_env == 2 || kw_env == 4) {
     kw = kw_env;
   } else {
-    // measured (profiles/kbench_gemv_kw.txt): only the plain small-N GEMV gains; the norm
-    // variants pay one prologue per workgroup, so they keep one wave per row set
+    // small N: two waves per row set (one weight round trip per wave); the norm variants then
+    // run 8-wave workgroups so the prologue is not repeated per extra workgroup
     const int wg1 = (N_out + 4 * rpw - 1) / (4 * rpw) * splits;
-    if (nw == nullptr && wg1 < 512 && nch_split >= 256) kw = 2;
+    if (wg1 < 512 && nch_split >= 256 && (mode == 0 || M <= 4)) kw = 2;
   }
-  const int rows_per_wg = (4 / kw) * rpw;
+  // The norm variants keep 4 row sets per workgroup when they split K (8 waves, 512 threads):
+  // the per-workgroup norm prologue is then shared by twice the waves instead of being repeated.
+  const int nt = (mode != 0 && kw == 2 && M <= 4) ? 512 : 256;
+  const int rows_per_wg = (nt / 64 / kw) * rpw;
   dim3 grid((N_out + rows_per_wg - 1) / rows_per_wg, splits);
   const size_t lds = (size_t)M * ks * 2;
   const int half_rows = (epi == EPI_SWIGLU) ? N_out : 0;
@@ -395,11 +425,19 @@ extern "C" int k8s_gemv_norm_w(void* out, void* partial, const void* x, const vo
   const bf16_t* ri = (const bf16_t*)res_in;
   bf16_t* ro = (bf16_t*)res_out;
   const bf16_t* gw = (const bf16_t*)nw;
-#define G3(MM, RR, EE, F8, KK)                                                                                 \
-  if (gw) gemv_kernel<MM, RR, EE, true, F8, KK><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,   \
-                                                                            half_rows, ri, ro, gw, eps, wscale); \
-  else gemv_kernel<MM, RR, EE, false, F8, KK><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,     \
-                                                                          half_rows, ri, ro, gw, eps, wscale)
+#define G4(MM, RR, EE, F8, KK, NTT)                                                                            \
+  if (mode == 1) gemv_kernel<MM, RR, EE, 1, F8, KK, NTT><<<grid, NTT, lds, stream>>>(                          \
+      out, part, xx, ww, N_out, K, ks, half_rows, ri, ro, gw, eps, wscale);                                      \
+  else if (mode == 2) gemv_kernel<MM, RR, EE, 2, F8, KK, NTT><<<grid, NTT, lds, stream>>>(                     \
+      out, part, xx, ww, N_out, K, ks, half_rows, ri, ro, gw, eps, wscale);                                      \
+  else gemv_kernel<MM, RR, EE, 0, F8, KK><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,          \
+                                                                       half_rows, ri, ro, gw, eps, wscale)
+#define G3(MM, RR, EE, F8, KK)                  \
+  if constexpr (KK == 2 && MM <= 4) {           \
+    G4(MM, RR, EE, F8, KK, 512);                \
+  } else {                                      \
+    G4(MM, RR, EE, F8, KK, 256);                \
+  }
 #define G2(MM, RR, EE, F8)                      \
   if (kw == 4) { G3(MM, RR, EE, F8, 4); }        \
   else if (kw == 2) { G3(MM, RR, EE, F8, 2); }   \
@@ -438,6 +476,20 @@ extern "C" int k8s_gemv_norm_w(void* out, void* partial, const void* x, const vo
     }
   }
   return (int)hipGetLastError();
+}
+
+extern "C" int k8s_gemv_norm_w(void* out, void* partial, const void* x, const void* W, const float* wscale, int M,
+                               int N_out, int K, int epi, const void* res_in, void* res_out, const void* nw,
+                               float eps, hipStream_t stream) {
+  return gemv_launch(nw != nullptr ? 1 : 0, out, partial, x, W, wscale, M, N_out, K, epi, res_in, res_out, nw, eps,
+                     stream);
+}
+
+// Pre-norm projection with the norm weight folded into W: y = epi((W' . (x + res_in)) / rms(x + res_in)).
+extern "C" int k8s_gemv_rms(void* out, void* partial, const void* x, const void* W, const float* wscale, int M,
+                            int N_out, int K, int epi, const void* res_in, void* res_out, float eps,
+                            hipStream_t stream) {
+  return gemv_launch(2, out, partial, x, W, wscale, M, N_out, K, epi, res_in, res_out, nullptr, eps, stream);
 }
 
 extern "C" int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K,

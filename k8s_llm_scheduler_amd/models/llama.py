@@ -52,8 +52,12 @@ class LayerWeights:
 class LlamaModel:
     def __init__(self, cfg: LlamaConfig, tp: Optional[TPGroup] = None, device: str | torch.device = "cpu",
                  dtype: torch.dtype = torch.bfloat16, seed: int = 0, weights: Optional[str] = None,
-                 max_model_len: int = 8192, weight_dtype: str = "bf16"):
+                 max_model_len: int = 8192, weight_dtype: str = "bf16", fold_norm: bool = True):
         self.cfg = cfg
+        # RMSNorm weights are folded into the projection that follows them (W' = W * gamma, one
+        # elementwise pass at load time): the decode GEMVs then apply only 1/rms, in their epilogue
+        # (gemv.hip NORM == 2), and prefill normalises with gamma = 1.  Mathematically identical.
+        self.norm_folded = fold_norm
         self.tp = tp or TPGroup()
         cfg.validate_tp(self.tp.world)
         self.device = torch.device(device)
@@ -81,6 +85,9 @@ class LlamaModel:
             self._load_safetensors(Path(weights))
         else:
             self._random_init()
+        if self.norm_folded:
+            self.lm_head = self._fold(self.lm_head, self.norm)
+            self.norm = self._ones()
         self.kv_cache: Optional[torch.Tensor] = None
         self.block_size = 16
 
@@ -157,7 +164,20 @@ class LlamaModel:
         lm = "lm_head.weight" if "lm_head.weight" in index else "model.embed_tokens.weight"
         self.lm_head = sl(lm, 0, r * self.Vs, (r + 1) * self.Vs).contiguous()
 
+    def _ones(self) -> torch.Tensor:
+        if getattr(self, "_ones_t", None) is None:
+            self._ones_t = torch.ones(self.cfg.hidden, dtype=self.dtype, device=self.device)
+        return self._ones_t
+
+    @staticmethod
+    def _fold(w: torch.Tensor, gamma: torch.Tensor) -> torch.Tensor:
+        """W[n, k] * gamma[k] (bf16 result), in place."""
+        return w.mul_(gamma.view(1, -1).to(w.dtype))
+
     def _add_layer(self, lw: LayerWeights) -> None:
+        if self.norm_folded:
+            lw.wqkv, lw.wgu = self._fold(lw.wqkv, lw.ln1), self._fold(lw.wgu, lw.ln2)
+            lw.ln1 = lw.ln2 = self._ones()
         if self.weight_dtype == "fp8":
             lw.wqkv, lw.wo, lw.wgu, lw.wdown = (ops.quantize_fp8(w) for w in (lw.wqkv, lw.wo, lw.wgu, lw.wdown))
         self.layers.append(lw)
@@ -258,16 +278,18 @@ class LlamaModel:
         res_b = torch.empty_like(h)
         res_in = None
         for w_l, w in enumerate(self.layers):
-            qkv = ops.linear_norm(h, w.wqkv, w.ln1, c.rms_eps, res_in, res_b)
+            qkv = ops.linear_norm(h, w.wqkv, None if self.norm_folded else w.ln1, c.rms_eps, res_in, res_b)
             a = ops.decode_attention_fused(qkv, self.cos_sin, kv[w_l, 0], kv[w_l, 1], block_tables, context_lens,
                                            self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
             o = ops.linear(a, w.wo)
             self.tp.all_reduce_(o)
-            g = ops.linear_norm(o, w.wgu, w.ln2, c.rms_eps, res_b, res_a, epi=ops.EPI_SWIGLU)
+            g = ops.linear_norm(o, w.wgu, None if self.norm_folded else w.ln2, c.rms_eps, res_b, res_a,
+                                epi=ops.EPI_SWIGLU)
             h = ops.linear(g, w.wdown)
             self.tp.all_reduce_(h)
             res_in = res_a
-        logits = ops.linear_norm(h, self.lm_head, self.norm, c.rms_eps, res_in, None, epi=ops.EPI_F32)
+        logits = ops.linear_norm(h, self.lm_head, None if self.norm_folded else self.norm, c.rms_eps, res_in, None,
+                                 epi=ops.EPI_F32)
         return self.tp.all_gather_shards(logits)
 
 
@@ -292,7 +314,7 @@ def save_hf_checkpoint(model: LlamaModel, path: Path) -> None:
         t[p + "input_layernorm.weight"] = w.ln1
         t[p + "post_attention_layernorm.weight"] = w.ln2
     path.mkdir(parents=True, exist_ok=True)
-    save_file({k: v.contiguous().cpu() for k, v in t.items()}, str(path / "model.safetensors"))
+    save_file({k: v.detach().cpu().clone().contiguous() for k, v in t.items()}, str(path / "model.safetensors"))
     (path / "config.json").write_text(json.dumps({
         "hidden_size": c.hidden, "num_attention_heads": c.num_heads, "num_key_value_heads": c.num_kv_heads,
         "head_dim": c.head_dim, "intermediate_size": c.intermediate, "vocab_size": c.vocab,

@@ -122,6 +122,18 @@ def _fp8_gemm(x: torch.Tensor, w: "Fp8Weight", out_dtype=None) -> torch.Tensor:
                             out_dtype=out_dtype or BF16)
 
 
+def _ref_act_quant(x: torch.Tensor, w) -> torch.Tensor:
+    """CPU oracle of the GPU dispatch: with fp8 weights, more than GEMV_MAX_M rows go through
+    per-token e4m3 activations (_fp8_gemm), so the reference rounds its activations the same way."""
+    if not isinstance(w, Fp8Weight):
+        return x
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.shape[0] <= GEMV_MAX_M:
+        return x
+    q, s = ref.quantize_fp8(x2)
+    return ref.dequant_fp8(q, s, torch.float32).to(x.dtype).view(x.shape)
+
+
 def _is_fp8(w) -> bool:
     return isinstance(w, Fp8Weight)
 
@@ -237,8 +249,9 @@ SKINNY_MAX_M = 64
 
 
 def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0, res_in=None,
-          res_out=None) -> torch.Tensor:
-    """Decode GEMV (M <= 8) for bf16 or fp8 weights, optionally with the fused pre-norm prologue."""
+          res_out=None, folded: bool = False) -> torch.Tensor:
+    """Decode GEMV (M <= 8) for bf16 or fp8 weights, optionally with the fused pre-norm prologue
+    (``folded``: the norm weight is already multiplied into ``w``; only 1/rms is applied)."""
     M, K = x.shape
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     out = torch.empty(M, N, dtype=out_dtype, device=x.device)
@@ -248,7 +261,10 @@ def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0
     ri = _chk(res_in, BF16, "res_in") if res_in is not None else 0
     ro = _chk(res_out, BF16, "res_out") if res_out is not None else 0
     nw = _chk(norm_w, BF16, "norm_w") if norm_w is not None else 0
-    if _is_fp8(w):
+    if folded:
+        native().gemv_rms(out.data_ptr(), pp, _chk(x, BF16, "x"), w.q.data_ptr() if _is_fp8(w) else _chk(w, BF16, "w"),
+                          w.scale.data_ptr() if _is_fp8(w) else 0, M, N, K, epi, ri, ro, float(eps), -1)
+    elif _is_fp8(w):
         native().gemv_fp8(out.data_ptr(), pp, _chk(x, BF16, "x"), w.q.data_ptr(), w.scale.data_ptr(), M, N, K, epi,
                           ri, ro, nw, float(eps), -1)
     elif norm_w is not None:
@@ -295,7 +311,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
     """y = x @ w.T with w [N, K] bf16.  M <= 8 rows: hand-written HBM-streaming GEMV; M <= 64
     (batched decode): MFMA skinny GEMM; larger M (prefill): library GEMM (hipBLASLt via torch)."""
     if not _gpu(x, w):
-        return ref.linear(x, w, out_dtype)
+        return ref.linear(_ref_act_quant(x, w), w, out_dtype)
     x2 = x.reshape(-1, x.shape[-1])
     if x2.shape[0] <= GEMV_MAX_M:
         y = _gemv(x2.contiguous(), w, EPI_F32 if out_dtype == F32 else EPI_BF16, out_dtype or BF16)
@@ -310,10 +326,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
     return y.view(*x.shape[:-1], y.shape[-1])
 
 
-def linear_norm(x: torch.Tensor, w, norm_w: torch.Tensor, eps: float,
+def linear_norm(x: torch.Tensor, w, norm_w: Optional[torch.Tensor], eps: float,
                 res_in: Optional[torch.Tensor], res_out: Optional[torch.Tensor], epi: int = EPI_BF16) -> torch.Tensor:
     """Decode-path fused pre-norm projection (M <= 8 rows):
     r = x + res_in (or x), res_out <- r, y = epi(rmsnorm(r) * norm_w @ w.T).
+    ``norm_w=None``: the norm weight has been folded into ``w`` (LlamaModel does this at load time),
+    so y = epi((r @ w.T) / rms(r)) and the kernel skips the normalisation pass.
     res_in and res_out must be distinct buffers (ping-pong).  ``w``: bf16 tensor or Fp8Weight."""
     if res_in is not None and res_out is not None and res_in.data_ptr() == res_out.data_ptr():
         raise ValueError("res_in and res_out must be different buffers")
@@ -322,13 +340,14 @@ def linear_norm(x: torch.Tensor, w, norm_w: torch.Tensor, eps: float,
         r = x if res_in is None else (x.float() + res_in.float()).to(x.dtype)
         if res_out is not None:
             res_out.copy_(r)
-        h, _ = ref.rmsnorm(r, norm_w, eps)
+        h, _ = ref.rmsnorm(r, norm_w if norm_w is not None else torch.ones(K, dtype=r.dtype), eps)
         if epi == EPI_SWIGLU:
             return ref.linear_swiglu(h, w)
         return ref.linear(h, w, F32 if epi == EPI_F32 else None)
     if M > GEMV_MAX_M:
         raise ValueError("linear_norm is the decode path (M <= 8)")
-    return _gemv(x, w, epi, F32 if epi == EPI_F32 else BF16, norm_w=norm_w, eps=eps, res_in=res_in, res_out=res_out)
+    return _gemv(x, w, epi, F32 if epi == EPI_F32 else BF16, norm_w=norm_w, eps=eps, res_in=res_in, res_out=res_out,
+                 folded=norm_w is None)
 
 
 def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
@@ -385,7 +404,7 @@ def _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, contex
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     """silu(x @ Wg.T) * (x @ Wu.T) with w_gate_up = [Wg; Wu] ([2I, K])."""
     if not _gpu(x, w_gate_up):
-        return ref.linear_swiglu(x, w_gate_up)
+        return ref.linear_swiglu(_ref_act_quant(x, w_gate_up), w_gate_up)
     x2 = x.reshape(-1, x.shape[-1])
     if x2.shape[0] <= GEMV_MAX_M:
         y = _gemv(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)

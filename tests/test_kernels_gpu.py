@@ -403,3 +403,37 @@ def test_fp8_prefill_gemm(M, N, K):
     got_gu = ops.linear_swiglu(x, gu)
     rel = float((got_gu.float().cpu() - want_gu.float()).abs().max() / want_gu.float().abs().max())
     assert rel < 0.08, rel
+
+
+@pytest.mark.parametrize("M", [1, 3, 4, 8])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("N", [1280, 96])
+def test_linear_norm_folded(M, epi, N):
+    """Decode pre-norm projection with the norm weight folded into W (the model's layout):
+    y = epi((r @ (W * g).T) / rms(r)), bf16 and fp8 weights, against exact fp32 products (the
+    kernel never rounds the normalised activations), and loosely against the unfolded layer."""
+    K = 8192
+    x, res = rnd(M, K), rnd(M, K)
+    g = rnd(K, scale=0.1) + 1
+    w = rnd(2 * N if epi == 2 else N, K, scale=0.05)
+    wf = (w.float() * g.float()).bfloat16()
+    ro = torch.zeros(M, K, dtype=torch.bfloat16, device=DEV)
+    got = ops.linear_norm(x, wf, None, 1e-5, res, ro, epi=epi)
+    r = (x.float() + res.float()).bfloat16()
+    rf = r.cpu().float()
+    h32 = rf * torch.rsqrt(rf.pow(2).mean(-1, keepdim=True) + 1e-5)
+
+    def exact(wt):
+        y32 = h32 @ wt.float().T
+        return torch.nn.functional.silu(y32[:, :N]) * y32[:, N:] if epi == 2 else y32
+
+    close(ro, r, 0, 0)
+    close(got, exact(wf.cpu()), 3e-2)
+    # the unfolded layer it stands for: that reference rounds the normalised activations to bf16,
+    # which SwiGLU's gate x up product amplifies to ~0.2 absolute at these output magnitudes
+    h, _ = ref.rmsnorm(r.cpu(), g.cpu(), 1e-5)
+    unf = ref.linear_swiglu(h, w.cpu()) if epi == 2 else ref.linear(h, w.cpu(), torch.float32 if epi == 1 else None)
+    close(got, unf, 4e-1 if epi == 2 else 6e-2, 4e-2)
+    wq = ops.quantize_fp8(wf)          # fp8 weights, folded the same way
+    got8 = ops.linear_norm(x, wq, None, 1e-5, res, ro, epi=epi)
+    close(got8, exact(ref.dequant_fp8(wq.q.cpu(), wq.scale.cpu())), 3e-2)

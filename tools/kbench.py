@@ -62,8 +62,8 @@ def main():
         ri, ro = torch.randn(M, K, device=dev).to(bf), torch.empty(M, K, device=dev, dtype=bf)
         if norm and M > ops.GEMV_MAX_M:
             return
-        if norm:
-            fn = lambda: ops.linear_norm(x, w, nw, 1e-5, ri, ro, epi=epi)
+        if norm:  # the model's layout: norm weight folded into W, 1/rms in the epilogue
+            fn = lambda: ops.linear_norm(x, w, None, 1e-5, ri, ro, epi=epi)
         elif epi == 2:
             fn = lambda: ops.linear_swiglu(x, w)
         else:
