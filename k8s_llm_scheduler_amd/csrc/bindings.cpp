@@ -30,7 +30,7 @@ int k8s_paged_decode_attention(void* out, void* part_acc, void* part_ml, const v
 int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, const void* v_cache, const int* cu_q,
                                 const int* context_lens, const int* block_tables, float scale, int num_seqs,
                                 int max_qlen, int nq, int nkv, int D, int block_size, int max_blocks, hipStream_t s);
-void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int* splits_out);
+void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* ks_out, int* splits_out);
 int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out,
                  int K, int epi, const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
 int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s);
@@ -110,9 +110,9 @@ PYBIND11_MODULE(_C, m) {
                                       max_qlen, nq, nkv, D, bs, max_blocks, S(s)),
           "paged_prefill_attention");
   });
-  m.def("gemv_plan", [](int M, int N, int K, int epi) {
+  m.def("gemv_plan", [](int M, int N, int K, int epi, int mode) {
     int ks, sp;
-    k8s_gemv_plan(M, N, K, epi, &ks, &sp);
+    k8s_gemv_plan(M, N, K, epi, mode, &ks, &sp);
     return py::make_tuple(ks, sp);
   });
   m.def("gemv_fp8", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, uintptr_t wscale, int M, int N,

@@ -366,8 +366,19 @@ __global__ void gemv_finalize_kernel(void* __restrict__ out, const float* __rest
 using namespace k8sllm;
 
 // Plan the launch: returns the K-slice length (multiple of 512) and the split count.
-extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int* ks_out, int* splits_out) {
-  const int rpw = (M >= 4) ? 2 : 1;
+// Rows per wave: 2 from M = 4 on.  Below, the plain (no norm prologue, no SwiGLU) projections with
+// N >= 8192 outputs (o_proj, down at every TP degree) also take 2: half as many workgroups, twice the
+// weight loads in flight per lane (measured TP = 8: o_proj 4.8 -> 3.6 us, down 10.8 -> 9.9 us; it
+// loses on the small-N QKV and on gate/up, profiles/kbench_*).  K8S_GEMV_RPW1 = 1 / 2 forces M < 4.
+static int gemv_rpw(int M, int N_out = 0, int epi = 0, int mode = 0) {
+  static const int env = [] { const char* e = getenv("K8S_GEMV_RPW1"); return e ? atoi(e) : 0; }();
+  if (M >= 4) return 2;
+  if (env == 1 || env == 2) return env;
+  return (mode == 0 && epi != EPI_SWIGLU && N_out >= 8192) ? 2 : 1;
+}
+
+extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* ks_out, int* splits_out) {
+  const int rpw = gemv_rpw(M, N_out, epi, mode);
   const int rows_per_wg = 4 * rpw;
   const int n_wg = (N_out + rows_per_wg - 1) / rows_per_wg;
   const int lds_cap_elems = 65536 / (2 * M);  // <= 64 KiB of x per workgroup (M=1: K up to 32768 unsplit)
@@ -396,10 +407,10 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
   const bool fp8 = wscale != nullptr;
   if (fp8 && K % 16 != 0) return -1;
   int ks, splits;
-  k8s_gemv_plan(M, N_out, K, epi, &ks, &splits);
+  k8s_gemv_plan(M, N_out, K, epi, mode, &ks, &splits);
   if (splits > 1 && partial == nullptr) return -3;
   float* part = splits > 1 ? (float*)partial : nullptr;
-  const int rpw = (M >= 4) ? 2 : 1;
+  const int rpw = gemv_rpw(M, N_out, epi, mode);
   // KW: waves per row set.  Split a row set's K over 2 or 4 waves while N alone leaves fewer
   // than ~1024 workgroups and every wave keeps >= 2 chunks per lane (K8S_GEMV_KW overrides).
   static const int kw_env = [] { const char* e = getenv("K8S_GEMV_KW"); return e ? atoi(e) : 0; }();
@@ -453,9 +464,9 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
     default: return -2;                 \
   }
   switch (M) {
-    case 1: BY_EPI(1, 1) break;
-    case 2: BY_EPI(2, 1) break;
-    case 3: BY_EPI(3, 1) break;
+    case 1: if (rpw == 2) { BY_EPI(1, 2) } else { BY_EPI(1, 1) } break;
+    case 2: if (rpw == 2) { BY_EPI(2, 2) } else { BY_EPI(2, 1) } break;
+    case 3: if (rpw == 2) { BY_EPI(3, 2) } else { BY_EPI(3, 1) } break;
     case 4: BY_EPI(4, 2) break;
     case 5: BY_EPI(5, 2) break;
     case 6: BY_EPI(6, 2) break;

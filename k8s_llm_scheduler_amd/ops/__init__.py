@@ -255,7 +255,8 @@ def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0
     M, K = x.shape
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     out = torch.empty(M, N, dtype=out_dtype, device=x.device)
-    ks, splits = native().gemv_plan(M, N, K, epi)
+    mode = 2 if folded else (1 if norm_w is not None else 0)
+    ks, splits = native().gemv_plan(M, N, K, epi, mode)
     part = torch.empty(splits * M * w.shape[0], dtype=F32, device=x.device) if splits > 1 else None
     pp = part.data_ptr() if part is not None else 0
     ri = _chk(res_in, BF16, "res_in") if res_in is not None else 0
