@@ -217,9 +217,12 @@ PYBIND11_MODULE(_C, m) {
         for (const auto& h : hs) v.emplace_back(h);
         c.open(v);
       })
-      .def("all_reduce_bf16", [](XgmiComm& c, uintptr_t in, uintptr_t out, long long bytes, int64_t s) {
-        c.all_reduce_bf16(P(in), P(out), bytes, S(s));
-      })
+      .def(
+          "all_reduce_bf16",
+          [](XgmiComm& c, uintptr_t in, uintptr_t out, long long bytes, int64_t s, uintptr_t residual) {
+            c.all_reduce_bf16(P(in), P(out), bytes, S(s), P(residual));
+          },
+          py::arg("inp"), py::arg("out"), py::arg("bytes"), py::arg("stream") = -1, py::arg("residual") = 0)
       .def("all_gather", [](XgmiComm& c, uintptr_t in, uintptr_t out, long long bytes, int64_t s) {
         c.all_gather(P(in), P(out), bytes, S(s));
       })

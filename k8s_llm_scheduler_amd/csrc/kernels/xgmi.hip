@@ -36,6 +36,7 @@ struct XgArgs {
   uint32_t* err;             // set non-zero on a poll timeout
   const char* in;
   char* out;
+  const char* res;           // optional bf16 residual added to the sum (AR + residual add, K14 + K2)
   long long bytes;           // payload bytes per rank (multiple of 16)
   long long slot_bytes;      // capacity of one (slot, source) row
   int rank, world;
@@ -120,6 +121,11 @@ __global__ __launch_bounds__(XG_THREADS) void xg_allreduce_bf16_kernel(XgArgs a)
 #pragma unroll
       for (int j = 0; j < 4; ++j) { acc[2 * j] += lo_bf(rows[t][j]); acc[2 * j + 1] += hi_bf(rows[t][j]); }
     }
+    if (a.res != nullptr) {
+      const u32x4 rv = reinterpret_cast<const u32x4*>(a.res)[v];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { acc[2 * j] += lo_bf(rv[j]); acc[2 * j + 1] += hi_bf(rv[j]); }
+    }
     u32x4 r;
 #pragma unroll
     for (int j = 0; j < 4; ++j) r[j] = pack_bf2(acc[2 * j], acc[2 * j + 1]);
@@ -184,6 +190,11 @@ __global__ __launch_bounds__(XG_THREADS) void xg_allreduce_ll_kernel(XgArgs a) {
       lo += lo_bf(d[t]);
       hi += hi_bf(d[t]);
     }
+    if (a.res != nullptr) {
+      const uint32_t rr = reinterpret_cast<const uint32_t*>(a.res)[v];
+      lo += lo_bf(rr);
+      hi += hi_bf(rr);
+    }
     out[v] = pack_bf2(lo, hi);
   }
 }
@@ -219,16 +230,18 @@ static int xg_fill(XgArgs& a, void* const* bases, uint32_t* counters, uint32_t* 
   if (XG_FLAG_BYTES + 2LL * world * slot_bytes > 0x7fffffffLL) return -3;
   for (int i = 0; i < XG_MAX_WORLD; ++i) a.base[i] = i < world ? static_cast<char*>(bases[i]) : nullptr;
   a.counters = counters; a.err = err;
-  a.in = static_cast<const char*>(in); a.out = static_cast<char*>(out);
+  a.in = static_cast<const char*>(in); a.out = static_cast<char*>(out); a.res = nullptr;
   a.bytes = bytes; a.slot_bytes = slot_bytes; a.rank = rank; a.world = world; a.timeout_ticks = timeout_ticks;
   return 0;
 }
 
 extern "C" int k8s_xgmi_allreduce_bf16(void* const* bases, uint32_t* counters, uint32_t* err, const void* in,
                                        void* out, long long bytes, long long slot_bytes, int rank, int world,
-                                       int blocks, long long timeout_ticks, hipStream_t s) {
+                                       int blocks, long long timeout_ticks, const void* residual, hipStream_t s) {
   XgArgs a;
   if (int rc = xg_fill(a, bases, counters, err, in, out, bytes, slot_bytes, rank, world, timeout_ticks)) return rc;
+  if ((uintptr_t)residual & 15) return -2;
+  a.res = static_cast<const char*>(residual);
   if (blocks < 1 || blocks > XG_MAX_BLOCKS) return -4;
   switch (world) {
     case 2: xg_allreduce_bf16_kernel<2><<<blocks, XG_THREADS, 0, s>>>(a); break;
@@ -245,10 +258,12 @@ extern "C" int k8s_xgmi_allreduce_bf16(void* const* bases, uint32_t* counters, u
 
 extern "C" int k8s_xgmi_allreduce_ll_bf16(void* const* bases, uint32_t* counters, uint32_t* err, const void* in,
                                           void* out, long long bytes, long long slot_bytes, int rank, int world,
-                                          int blocks, long long timeout_ticks, hipStream_t s) {
+                                          int blocks, long long timeout_ticks, const void* residual, hipStream_t s) {
   XgArgs a;
   if (2 * bytes > slot_bytes) return -2;  // LL rows carry a flag word per data word
   if (int rc = xg_fill(a, bases, counters, err, in, out, bytes, slot_bytes, rank, world, timeout_ticks)) return rc;
+  if ((uintptr_t)residual & 3) return -2;
+  a.res = static_cast<const char*>(residual);
   if (blocks < 1 || blocks > XG_MAX_BLOCKS) return -4;
   switch (world) {
     case 2: xg_allreduce_ll_kernel<2><<<blocks, XG_THREADS, 0, s>>>(a); break;

@@ -9,10 +9,10 @@ long long k8s_xgmi_flag_bytes();
 int k8s_xgmi_max_blocks();
 int k8s_xgmi_allreduce_bf16(void* const* bases, uint32_t* counters, uint32_t* err, const void* in, void* out,
                             long long bytes, long long slot_bytes, int rank, int world, int blocks,
-                            long long timeout_ticks, hipStream_t s);
+                            long long timeout_ticks, const void* residual, hipStream_t s);
 int k8s_xgmi_allreduce_ll_bf16(void* const* bases, uint32_t* counters, uint32_t* err, const void* in, void* out,
                                long long bytes, long long slot_bytes, int rank, int world, int blocks,
-                               long long timeout_ticks, hipStream_t s);
+                               long long timeout_ticks, const void* residual, hipStream_t s);
 int k8s_xgmi_allgather(void* const* bases, uint32_t* counters, uint32_t* err, const void* in, void* out,
                        long long bytes, long long slot_bytes, int rank, int world, int blocks,
                        long long timeout_ticks, hipStream_t s);
@@ -79,16 +79,16 @@ void XgmiComm::open(const std::vector<std::string>& handles) {
   opened_ = true;
 }
 
-void XgmiComm::all_reduce_bf16(const void* in, void* out, long long bytes, hipStream_t s) {
+void XgmiComm::all_reduce_bf16(const void* in, void* out, long long bytes, hipStream_t s, const void* residual) {
   if (!opened_) throw std::runtime_error("XgmiComm: not open");
   if (bytes <= ll_max_bytes_ && 2 * bytes <= slot_bytes_) {
     ckrc(k8s_xgmi_allreduce_ll_bf16(bases_.data(), counters_, counters_ + k8s_xgmi_max_blocks(), in, out, bytes,
-                                    slot_bytes_, rank_, world_, blocks_, timeout_ticks_, s),
+                                    slot_bytes_, rank_, world_, blocks_, timeout_ticks_, residual, s),
          "xgmi all_reduce (LL)");
     return;
   }
   ckrc(k8s_xgmi_allreduce_bf16(bases_.data(), counters_, counters_ + k8s_xgmi_max_blocks(), in, out, bytes,
-                               slot_bytes_, rank_, world_, blocks_, timeout_ticks_, s),
+                               slot_bytes_, rank_, world_, blocks_, timeout_ticks_, residual, s),
        "xgmi all_reduce");
 }
 

@@ -19,7 +19,8 @@ class XgmiComm {
 
   std::string handle() const;                        // hipIpcMemHandle_t bytes of this rank's region
   void open(const std::vector<std::string>& handles);  // map every peer's region (index = rank)
-  void all_reduce_bf16(const void* in, void* out, long long bytes, hipStream_t s);
+  // out = sum over ranks of in (+ residual, a bf16 tensor of the same size, when given)
+  void all_reduce_bf16(const void* in, void* out, long long bytes, hipStream_t s, const void* residual = nullptr);
   void all_gather(const void* in, void* out, long long bytes_per_rank, hipStream_t s);
   uint32_t error();                                   // poll-timeout bitmask (synchronizes the device)
   void reset_error();

@@ -274,6 +274,8 @@ class LlamaModel:
         The residual stream ping-pongs between two buffers (a norm-GEMV reads one, writes the other)."""
         c, kv = self.cfg, self.kv_cache
         h = ops.embedding(tokens, self.embed)
+        if self.tp.world > 1:
+            return self._forward_decode_fused_tp(h, context_lens, block_tables, max_context)
         res_a = torch.empty_like(h)
         res_b = torch.empty_like(h)
         res_in = None
@@ -291,6 +293,29 @@ class LlamaModel:
         logits = ops.linear_norm(h, self.lm_head, None if self.norm_folded else self.norm, c.rms_eps, res_in, None,
                                  epi=ops.EPI_F32)
         return self.tp.all_gather_shards(logits)
+
+    def _forward_decode_fused_tp(self, h: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
+                                 max_context: int) -> torch.Tensor:
+        """TP > 1 decode: the residual add rides on the all-reduce (xGMI kernels add it before their
+        single rounding: SURVEY K14 + K2), so the residual stream IS the all-reduce outputs and the
+        norm-GEMV prologues read one tensor (no residual read, no residual write)."""
+        c, kv = self.cfg, self.kv_cache
+        g1 = None if self.norm_folded else (lambda w: w.ln1)
+        g2 = None if self.norm_folded else (lambda w: w.ln2)
+        x = h
+        for l, w in enumerate(self.layers):
+            qkv = ops.linear_norm(x, w.wqkv, g1(w) if g1 else None, c.rms_eps, None, None)
+            a = ops.decode_attention_fused(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
+                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
+            o = ops.linear(a, w.wo)
+            self.tp.all_reduce_(o, residual=x)                 # o = x + attention branch
+            g = ops.linear_norm(o, w.wgu, g2(w) if g2 else None, c.rms_eps, None, None, epi=ops.EPI_SWIGLU)
+            x = ops.linear(g, w.wdown)
+            self.tp.all_reduce_(x, residual=o)                 # x = o + MLP branch
+        logits = ops.linear_norm(x, self.lm_head, None if self.norm_folded else self.norm, c.rms_eps, None, None,
+                                 epi=ops.EPI_F32)
+        return self.tp.all_gather_shards(logits)
+
 
 
 def save_hf_checkpoint(model: LlamaModel, path: Path) -> None:

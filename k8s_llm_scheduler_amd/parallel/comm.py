@@ -62,10 +62,18 @@ class TPGroup:
     def enabled(self) -> bool:
         return self.world > 1
 
-    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+    def all_reduce_(self, t: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """In-place sum over the TP group; with ``residual`` the result is sum + residual (the xGMI
+        kernels fuse the residual add, SURVEY K14 + K2; other transports add it afterwards)."""
         if self.world > 1 and not self.simulate:
             if t.dtype == torch.bfloat16 and t.is_contiguous() and self._xgmi_ok(t):
-                self.xgmi.all_reduce_bf16(t.data_ptr(), t.data_ptr(), t.numel() * 2, -1)
+                rp = 0
+                if residual is not None:
+                    if residual.dtype != t.dtype or residual.shape != t.shape or not residual.is_contiguous():
+                        raise ValueError("residual must match the reduced tensor")
+                    rp = residual.data_ptr()
+                self.xgmi.all_reduce_bf16(t.data_ptr(), t.data_ptr(), t.numel() * 2, -1, rp)
+                return t
             elif self.rccl is not None and t.is_cuda:
                 self.rccl.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], 0, -1)
             elif self.backend == "gloo" and t.dtype == torch.bfloat16:
@@ -74,6 +82,8 @@ class TPGroup:
                 t.copy_(f)
             else:
                 dist.all_reduce(t, group=self.group)
+            if residual is not None:
+                t.add_(residual)
         return t
 
     def all_gather_shards(self, t: torch.Tensor) -> torch.Tensor:

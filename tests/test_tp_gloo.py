@@ -38,6 +38,11 @@ def _worker(rank, world, port, q):
         lg, bt = _prefill(m, IDS)
         ctx = torch.tensor([len(IDS) + 1], dtype=torch.int32)
         m2_lg = m.forward_decode(torch.tensor([77], dtype=torch.int32), ctx, bt, 512)
+        # the GPU decode path for TP > 1 (residual carried by the all-reduce) on the CPU oracles
+        from k8s_llm_scheduler_amd import ops
+
+        ftp = m._forward_decode_fused_tp(ops.embedding(torch.tensor([77], dtype=torch.int32), m.embed), ctx, bt, 512)
+        torch.testing.assert_close(ftp, m2_lg, atol=3e-2, rtol=3e-2)
         eng = build_engine("tiny", tp=tp, device="cpu", max_batch=2, max_model_len=512, num_blocks=64, seed=1)
         toks = eng.generate(["tensor parallel"], SamplingParams(max_tokens=5, temperature=0.8, seed=9,
                                                                 ignore_eos=True))[0].token_ids

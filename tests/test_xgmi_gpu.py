@@ -61,6 +61,14 @@ def _worker(rank, world, port, q):
             torch.cuda.synchronize()
             assert torch.equal(y.cpu(), want), f"all_reduce n={n}"
             assert torch.equal(x.cpu(), want), f"in-place all_reduce n={n}"
+        # all-reduce + residual add fused (decode: the residual stream rides on the collective)
+        for seed, n in enumerate([8192, 65536]):
+            x = _data(rank, n, seed + 10).cuda()
+            r = _data(99, n, seed + 10).cuda()          # identical on both ranks
+            want = (sum(_data(q, n, seed + 10).float() for q in range(world)) + r.cpu().float()).to(torch.bfloat16)
+            tp.all_reduce_(x, residual=r)
+            torch.cuda.synchronize()
+            assert torch.equal(x.cpu(), want), f"all_reduce + residual n={n}"
         # the same sizes with the LL protocol off (flagged one-shot kernel for every size)
         ll = xg.ll_max_bytes
         xg.ll_max_bytes = 0
