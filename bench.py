@@ -55,6 +55,9 @@ def main() -> int:
     ap.add_argument("--tp", type=int, default=0,
                     help="TP degree of one engine replica (0 = all GPUs); WORLD_SIZE / tp replicas decide in "
                          "parallel (data parallelism, e.g. --tp 4 on 8 GPUs = two half-node engines)")
+    ap.add_argument("--prompt-layout", choices=["reference", "cluster_first"], default="reference",
+                    help="cluster_first (opt-in compat.prompt_layout): node block before the pod block, so a batch "
+                         "decided against one snapshot prefills the cluster state once")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--simulate-tp", type=int, default=0,
                     help="PROFILING ONLY: run one TP rank's shapes on one GPU with collectives skipped")
@@ -99,18 +102,19 @@ def main() -> int:
     backend = LocalEngineBackend(eng, ignore_eos=True)
     svc = DecisionService(backend, max_retries=3, max_tokens=args.gen_tokens, temperature=0.3, top_p=1.0,
                           timeout=None, cache=None, breaker=CircuitBreaker())
-    pe = PromptEngine()
+    pe = PromptEngine(layout=args.prompt_layout)
     rng = random.Random(1234)
     base_nodes, base_pods = reference_cluster(args.nodes)
 
     def make_items():
+        # one cluster snapshot per step, as the batched scheduler takes one snapshot per round
+        # (scheduler.py schedule_batch); utilisation varies from step to step (cache is off anyway)
+        nodes = base_nodes if args.nodes == 3 else random_nodes(rng, args.nodes)
+        for n in nodes:
+            n.pod_count = rng.randint(2, 12)
+            n.cpu_usage_percent = n.memory_usage_percent = n.pod_count / n.max_pods * 50
         items = []
         for _ in range(args.batch):
-            nodes = base_nodes if args.nodes == 3 else random_nodes(rng, args.nodes)
-            # vary utilisation a little so no two snapshots are identical (cache is off anyway)
-            for n in nodes:
-                n.pod_count = rng.randint(2, 12)
-                n.cpu_usage_percent = n.memory_usage_percent = n.pod_count / n.max_pods * 50
             pod = rng.choice(base_pods) if rng.random() < 0.5 else random_pod(rng)
             items.append((pe.construct_scheduling_prompt(pod, nodes), pod, list(nodes)))
         return items
@@ -170,6 +174,7 @@ def main() -> int:
             "parallelism": (f"dp{dp}-" if dp > 1 else "") + f"tp{tp.world}" + ("-SIMULATED-no-comm" if tp.simulate else ""),
             "cuda_graphs": eng.use_graphs,
             "prefix_cache": not args.no_prefix_cache,
+            "prompt_layout": args.prompt_layout,
         },
         "p50_decision_latency_ms": round(1000 * statistics.median(lat), 2),
         "p99_decision_latency_ms": round(1000 * sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))], 2),

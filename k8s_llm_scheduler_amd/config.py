@@ -123,6 +123,7 @@ class CompatSection:
     quantity_parsing: str = "full"               # "reference" reproduces scheduler.py:172-187/747-753
     watch_all_event_types: bool = False          # scheduler.py:664-681 (False: skip DELETED, dedupe)
     snapshot_mode: str = "informer"              # "direct" = N+1 REST calls (scheduler.py:124-147)
+    prompt_layout: str = "reference"             # "cluster_first": node block before the pod block (prefix sharing)
 
 
 @dataclass

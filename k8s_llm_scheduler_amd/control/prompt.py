@@ -72,12 +72,25 @@ def _node_block(node: NodeMetrics, status_always_ready: bool) -> str:
     ])
 
 
-class PromptEngine:
-    """Builds the user prompt for one (pod, cluster snapshot) pair."""
+LAYOUTS = ("reference", "cluster_first")
 
-    def __init__(self, status_always_ready: bool = True, system_instructions: str = SYSTEM_INSTRUCTIONS):
+
+class PromptEngine:
+    """Builds the user prompt for one (pod, cluster snapshot) pair.
+
+    ``layout="reference"`` (default) is byte-identical to the reference: instructions, pod, nodes.
+    ``layout="cluster_first"`` (opt-in, ``compat.prompt_layout``) puts the node block before the pod
+    block, with the same lines.  Every pod decided against one snapshot then shares the prompt up to
+    the pod block, so the engine's prefix cache prefills the cluster state once per batch instead of
+    once per pod (long-context row)."""
+
+    def __init__(self, status_always_ready: bool = True, system_instructions: str = SYSTEM_INSTRUCTIONS,
+                 layout: str = "reference"):
+        if layout not in LAYOUTS:
+            raise ValueError(f"prompt layout must be one of {LAYOUTS}, got {layout!r}")
         self.system_prompt = system_instructions
         self.status_always_ready = status_always_ready
+        self.layout = layout
 
     def cluster_block(self, nodes: Sequence[NodeMetrics]) -> str:
         names: List[str] = [n.name for n in nodes]
@@ -86,8 +99,10 @@ class PromptEngine:
 
     def construct_scheduling_prompt(self, pod: PodSpec, nodes: Sequence[NodeMetrics]) -> str:
         names = ", ".join(n.name for n in nodes)
-        return (self.system_prompt + "\n\n" + _pod_block(pod) + "\n" + self.cluster_block(nodes)
-                + "\n\nSelect the best node from [" + names + "] and respond with JSON only:")
+        closing = "\n\nSelect the best node from [" + names + "] and respond with JSON only:"
+        if self.layout == "cluster_first":
+            return self.system_prompt + "\n\n" + self.cluster_block(nodes) + "\n" + _pod_block(pod) + closing
+        return self.system_prompt + "\n\n" + _pod_block(pod) + "\n" + self.cluster_block(nodes) + closing
 
     # Name used by the rest of this package.
     build = construct_scheduling_prompt

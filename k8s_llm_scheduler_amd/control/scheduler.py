@@ -45,11 +45,11 @@ class CustomScheduler:
                  status_always_ready: bool = True, watch_all_event_types: bool = False,
                  mode: str = "sequential", max_batch: int = 64, batch_window_ms: float = 20.0,
                  watch_timeout: int = 60, error_backoff_s: float = 5.0,
-                 engine_label: str = "local Llama-3.3-70B", metrics=None):
+                 engine_label: str = "local Llama-3.3-70B", metrics=None, prompt_layout: str = "reference"):
         self.scheduler_name = name
         self.api = api
         self.context_manager = ClusterSnapshotter(api, snapshot_mode, quantity_mode)
-        self.prompt_engine = PromptEngine(status_always_ready)
+        self.prompt_engine = PromptEngine(status_always_ready, layout=prompt_layout)
         self.llm_client = decision_service
         self.integration_layer = IntegrationLayer(api)
         self.qmode = quantity_mode
@@ -79,7 +79,7 @@ class CustomScheduler:
                    mode=cfg.scheduler.mode, max_batch=cfg.scheduler.max_batch,
                    batch_window_ms=cfg.scheduler.batch_window_ms,
                    watch_timeout=cfg.scheduler.watch_interval, error_backoff_s=cfg.scheduler.error_backoff_s,
-                   engine_label=label, metrics=metrics)
+                   engine_label=label, metrics=metrics, prompt_layout=cfg.compat.prompt_layout)
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self) -> None:

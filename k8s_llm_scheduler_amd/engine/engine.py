@@ -121,6 +121,8 @@ class LLMEngine:
                                f"({self.max_blocks_per_seq})")
         self.num_blocks = num_blocks
         model.allocate_kv(num_blocks, block_size)
+        self.prefix_caching = prefix_caching
+        self._share_deferred = False
         self.allocator = ops.native().BlockAllocator(num_blocks, block_size, prefix_caching) if ops.available() \
             else _PyBlockAllocator(num_blocks, block_size, prefix_caching)
         self.max_new_cap = self.max_model_len
@@ -267,6 +269,27 @@ class LLMEngine:
         return bool(self.waiting or self.prefilling or self.running)
 
     # ------------------------------------------------------------------ scheduling
+    SHARE_MIN_BLOCKS = 2   # in-batch prefix sharing: defer a request that shares this many blocks
+
+    def _shares_pending_prefix(self, r: Request) -> bool:
+        """True when ``r`` shares at least SHARE_MIN_BLOCKS full KV blocks of its prompt with a request
+        that is still prefilling them.  Admitting ``r`` now would recompute that prefix (blocks are
+        published to the prefix cache only once their KV is written); one step later it is a cache
+        hit.  This is what makes a batch of pods decided against one cluster snapshot prefill the
+        shared part once (``compat.prompt_layout: cluster_first``)."""
+        if not self.prefix_caching:
+            return False
+        bs = self.block_size
+        ids = r.prompt_ids
+        for p in self.prefilling:
+            n = min(len(p.prompt_ids), len(ids)) - 1   # the last prompt token is never cached
+            c = 0
+            while c + bs <= n and p.prompt_ids[c:c + bs] == ids[c:c + bs]:
+                c += bs
+            if c // bs >= self.SHARE_MIN_BLOCKS and p.computed < c:
+                return True
+        return False
+
     def _admit(self) -> None:
         while self.waiting and self.free_slots:
             r = self.waiting[0]
@@ -274,6 +297,9 @@ class LLMEngine:
                 self.waiting.popleft()
                 self._finish(r, "abort")
                 continue
+            if self._shares_pending_prefix(r):
+                self._share_deferred = True
+                break   # admitted next step, with the shared prefix served from the cache
             total = len(r.prompt_ids) + r.params.max_tokens
             if not self.allocator.can_allocate(r.prompt_ids, total):
                 if not self.running and not self.prefilling:
@@ -440,10 +466,15 @@ class LLMEngine:
             if not self._sync():
                 raise StopIteration("engine stopped by rank 0")
             self._reap_aborted()
+            self._share_deferred = False
             self._admit()
             if self.prefilling or self.waiting:
                 with trace("engine.prefill"):
                     self._prefill()
+            if self._share_deferred and not any(r.output_ids for r in self.running.values()):
+                # requests are waiting for a prefix this step published: admit them before the
+                # first decode, so the batch decodes in lock-step (no extra tail of decode steps)
+                return []
             with trace("engine.decode"):
                 return self._decode()
 

@@ -223,3 +223,17 @@ def test_fallback_edge_cases():
     d = FallbackPolicy().decide(mk_nodes([1], ready=[False]), "r")
     assert d == SchedulingDecision("", 0.0, "Fallback failed: r", True)
     assert FallbackPolicy().decide(mk_nodes([0], max_pods=0), "r").selected_node == "kind-worker"
+
+
+def test_cluster_first_layout_same_lines_shared_prefix():
+    from k8s_llm_scheduler_amd.control.prompt import PromptEngine
+
+    nodes = mk_nodes([4, 7, 2])
+    pods = [PodSpec(f"p{i}", "default", 0.25 * (i + 1), 0.5, {}, [], {}, 0) for i in range(2)]
+    ref_pe, cf_pe = PromptEngine(), PromptEngine(layout="cluster_first")
+    a, b = (cf_pe.build(p, nodes) for p in pods)
+    assert sorted(a.splitlines()) == sorted(ref_pe.build(pods[0], nodes).splitlines())
+    shared = len(cf_pe.system_prompt) + len(cf_pe.cluster_block(nodes))
+    assert a[:shared] == b[:shared] and a != b
+    with pytest.raises(ValueError):
+        PromptEngine(layout="bogus")

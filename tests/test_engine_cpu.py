@@ -188,3 +188,18 @@ def test_forced_decode_emits_script_and_stops_on_json(engine):
     ids = engine.tok.encode(ans)
     o = engine.generate(["pick a node"], SamplingParams(max_tokens=200, temperature=0.3, forced_output_ids=ids))[0]
     assert o.text == ans and o.finish_reason == "json"
+
+
+def test_in_batch_prefix_sharing(engine):
+    """Requests submitted together that share a long prompt prefix: the first prefills it, the
+    others are admitted one step later and read it from the prefix cache; results are unchanged."""
+    engine.allocator.reset_prefix_cache()
+    shared = "AVAILABLE NODES: kind-worker cpu 20% mem 30% pods 4/110; kind-worker2 cpu 35% mem 10% " * 6
+    prompts = [engine.render_chat("system", shared + f" POD pod-{i}") for i in range(3)]
+    p = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True)
+    outs = engine.generate(prompts, p)
+    assert outs[0].cached_tokens == 0
+    assert all(o.cached_tokens >= 2 * engine.block_size for o in outs[1:])
+    engine.allocator.reset_prefix_cache()
+    alone = [engine.generate([q], p)[0].token_ids for q in prompts[1:]]
+    assert [o.token_ids for o in outs[1:]] == alone
