@@ -88,7 +88,7 @@ def main() -> int:
 
     t_init = time.perf_counter()
     bs = 16
-    per_seq = 2048 + args.gen_tokens + bs
+    per_seq = max(2048, args.max_model_len) + args.gen_tokens + bs   # KV blocks reserved per decision
     eng = build_engine(args.preset, tp=tp, max_batch=max(1, args.batch), block_size=bs,
                        num_blocks=max(args.batch, 2) * (per_seq // bs + 2) + 64,
                        max_model_len=args.max_model_len, cuda_graphs=not args.no_graphs,
