@@ -3,13 +3,47 @@
 from __future__ import annotations
 
 import logging
+import os
 import time
+from pathlib import Path
 from typing import Optional
 
 from .sampling import SamplingParams  # noqa: F401
 from .tokenizer import Tokenizer  # noqa: F401
 
 log = logging.getLogger(__name__)
+
+GEMM_TABLE = Path(__file__).resolve().parent / "assets" / "tunableop_gfx950.csv"
+_GEMM_TABLE_LOADED = False
+
+
+def _load_gemm_table() -> bool:
+    """Pin the library GEMMs of batched decode (8 < rows: hipBLASLt / rocBLAS through F.linear) to the
+    solutions ``tools/tune_gemms.py`` measured fastest on MI355X (PyTorch TunableOp table, read with
+    tuning OFF, so captured graphs replay fixed kernels; shapes missing from the table keep the
+    library default).  TP=1, 64 rows: down 157 -> 117 us, gate/up 183 -> 164 us.  K8S_GEMM_TABLE=0
+    disables; a table written by another torch / hipBLASLt / arch fails its validators and is ignored."""
+    global _GEMM_TABLE_LOADED
+    if _GEMM_TABLE_LOADED:
+        return True
+    if os.environ.get("K8S_GEMM_TABLE", "1") == "0" or not GEMM_TABLE.is_file():
+        return False
+    import torch
+
+    t = torch.cuda.tunable
+    try:
+        t.enable(True)
+        t.tuning_enable(False)
+        # anything TunableOp writes back at exit goes to a scratch file, never over the asset
+        t.set_filename(os.path.join(os.environ.get("TMPDIR", "/tmp"), f"k8s_tunableop_{os.getpid()}.csv"))
+        ok = bool(t.read_file(str(GEMM_TABLE)))
+    except Exception as e:  # noqa: BLE001 -- an unusable table only costs the library default
+        log.warning(f" GEMM table not loaded: {e}")
+        ok = False
+    if not ok:
+        t.enable(False)
+    _GEMM_TABLE_LOADED = ok
+    return ok
 
 
 def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str] = None, weights: Optional[str] = None,
@@ -31,6 +65,8 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
     if device is None:
         device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
     cfg = get_config(weights or preset) if weights else get_config(preset)
+    if device.startswith("cuda"):
+        _load_gemm_table()
     t0 = time.perf_counter()
     model = LlamaModel(cfg, tp, device=device, seed=seed, weights=weights, max_model_len=max_model_len,
                        weight_dtype=weight_dtype)
