@@ -40,19 +40,22 @@ __device__ __forceinline__ float dot8(u32x4 w, u32x4 x, float acc) {
   return dot2(w.w, x.w, acc);
 }
 
-// 16 fp8 weights (one 16-byte load) against 16 bf16 activations (two 16-byte LDS vectors).
+// 16 fp8 weights (one 16-byte load) against 16 bf16 activations (two 16-byte LDS vectors): each
+// dword of 4 e4m3 weights becomes two bf16 pairs with gfx950's v_cvt_scalef32_pk_bf16_fp8 (exact:
+// e4m3 fits bf16) and meets its activation pairs in v_dot2_f32_bf16 -- 16 VALU ops per 16 weights
+// and no activation unpacking (the f32 path needed ~40).
 __device__ __forceinline__ float dot16_fp8(u32x4 w, u32x4 x0, u32x4 x1, float acc) {
-  typedef __attribute__((ext_vector_type(2))) float f2;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const f2 lo = __builtin_amdgcn_cvt_pk_f32_fp8(w[j], false);  // bytes 0, 1
-    const f2 hi = __builtin_amdgcn_cvt_pk_f32_fp8(w[j], true);   // bytes 2, 3
+    const bf16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[j], 1.0f, false);  // bytes 0, 1
+    const bf16x2 hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[j], 1.0f, true);   // bytes 2, 3
     const uint32_t xa = j < 2 ? x0[2 * j] : x1[2 * j - 4];
     const uint32_t xb = j < 2 ? x0[2 * j + 1] : x1[2 * j - 3];
-    acc = fmaf(lo.x, lo_bf(xa), acc);
-    acc = fmaf(lo.y, hi_bf(xa), acc);
-    acc = fmaf(hi.x, lo_bf(xb), acc);
-    acc = fmaf(hi.y, hi_bf(xb), acc);
+    bf16x2 a, b;
+    __builtin_memcpy(&a, &xa, 4);
+    __builtin_memcpy(&b, &xb, 4);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(lo, a, acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(hi, b, acc, false);
   }
   return acc;
 }
