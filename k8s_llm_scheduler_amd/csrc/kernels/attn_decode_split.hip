@@ -34,6 +34,24 @@ constexpr int SPLIT_CH = 64;  // context tokens per workgroup (one wave)
 constexpr int SC1 = 16;       // buffer-op cache policy: sc1 (L1 bypass, coherent at the L2)
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_split_t;
 
+// Timeline probe (tools/attn_trace.py builds this file with -DK8S_ATTN_TRACE into its own library):
+// lane 0 of every workgroup stamps s_memrealtime (100 MHz) at 10 points, after draining its memory
+// traffic, into g_attn_trace[workgroup][12].  Compiled out of the production kernel.
+#ifdef K8S_ATTN_TRACE
+__device__ unsigned long long* g_attn_trace;
+#define TR(i)                                                                                  \
+  do {                                                                                         \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                \
+    if (threadIdx.x == 0)                                                                      \
+      g_attn_trace[((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 12 + (i)] = \
+          __builtin_amdgcn_s_memrealtime();                                                    \
+  } while (0)
+#else
+#define TR(i) \
+  do {        \
+  } while (0)
+#endif
+
 __device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t split_rsrc(const void* p) {
@@ -61,13 +79,26 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
   const int* bt = block_tables + (size_t)b * max_blocks;
   const size_t kvs = (size_t)nkv * D;
   const int start = c * CH;
+  TR(0);
 
-  // context length and the chunk's 4 block ids are independent loads: one round trip
+  // context length, the chunk's 4 block ids and the new token's q/k/v (lane p: dims p and p + 64
+  // of every q head, of k and of v) are independent loads: one round trip
   const int ctx = context_lens[b];
   int tblk[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) tblk[t] = bt[min(start / 16 + t, max_blocks - 1)];
+  const int nq = nkv * G;
+  const bf16_t* row = qkv + (size_t)b * (nq + 2 * nkv) * D;
+  bf16_t xa[G], xb[G];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    xa[h] = row[(size_t)(kvh * G + h) * D + lane];
+    xb[h] = row[(size_t)(kvh * G + h) * D + HALF + lane];
+  }
+  const bf16_t ka = row[(size_t)(nq + kvh) * D + lane], kb = row[(size_t)(nq + kvh) * D + HALF + lane];
+  const bf16_t va = row[(size_t)(nq + nkv + kvh) * D + lane], vb2 = row[(size_t)(nq + nkv + kvh) * D + HALF + lane];
   if (ctx <= 0 || start >= ctx) return;
+  TR(1);
 
   // ---- every K and V load of the chunk, issued before anything is consumed
   bf16x8 kf[4][D / 32];
@@ -77,41 +108,33 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
 #pragma unroll
     for (int kk = 0; kk < D / 32; ++kk) kf[t][kk] = *reinterpret_cast<const bf16x8*>(kp + kk * 32);
   }
-  u32x4 vv[16];  // chunk row 4q + g4, 16-byte column chunk li
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int r = 4 * q + g4;
-    vv[q] = *reinterpret_cast<const u32x4*>(v_cache + (size_t)(tblk[q >> 2] * 16 + (r & 15)) * kvs +
-                                            (size_t)kvh * D + li * 8);
-  }
-
+  // V goes straight into LDS (LDS-DMA, no VGPRs): instruction q fills vbuf bytes [1 KiB q, 1 KiB (q+1)) =
+  // rows 4q..4q+3 of the chunk; lane L lands at row 4q + L/16, 16-byte position L%16, which in the
+  // swizzled image holds column chunk (L%16) ^ swz(row % 32) -- so that is the chunk it fetches.  Rows past
+  // the context re-read the last valid row: their P is exactly 0, the bytes only have to be finite.
   const int n = min(CH, ctx - start);
+  {
+    const int lt = (n - 1) >> 4;
+    const int last_row = (lt == 0 ? tblk[0] : lt == 1 ? tblk[1] : lt == 2 ? tblk[2] : tblk[3]) * 16 + ((n - 1) & 15);
+    char* vflat = &vbuf[0][0];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = 4 * q + g4;
+      const int srow = r < n ? tblk[q >> 2] * 16 + (r & 15) : last_row;
+      const bf16_t* src = v_cache + (size_t)srow * kvs + (size_t)kvh * D + (li ^ swz(r & 31)) * 8;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(vflat + 1024 * q), 16, 0, 0);
+    }
+  }
   const int pos = ctx - 1;
   const bool owner = pos < start + n;  // the chunk that holds the new token
-  const int nq = nkv * G;
-  const bf16_t* row = qkv + (size_t)b * (nq + 2 * nkv) * D;
   const float* cs = cos_sin + (size_t)pos * D;
 
   // ---- RoPE: lane p rotates dims (p, p + 64) of every q head (and of the new k in the owner
-  // chunk); every load of this phase is issued before the first is consumed (one round trip)
+  // chunk); the cos/sin row is the only load of this phase
   {
     const int p = lane;
     const float cp = cs[p], sp = cs[HALF + p];
-    bf16_t xa[G], xb[G];
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      xa[h] = row[(size_t)(kvh * G + h) * D + p];
-      xb[h] = row[(size_t)(kvh * G + h) * D + HALF + p];
-    }
-    bf16_t ka = 0, kb = 0, va = 0, vb2 = 0;
-    int pslot = 0;
-    if (owner) {
-      ka = row[(size_t)(nq + kvh) * D + p];
-      kb = row[(size_t)(nq + kvh) * D + HALF + p];
-      va = row[(size_t)(nq + nkv + kvh) * D + p];
-      vb2 = row[(size_t)(nq + nkv + kvh) * D + HALF + p];
-      pslot = bt[pos / 16] * 16 + pos % 16;
-    }
+    const int pslot = owner ? bt[pos / 16] * 16 + pos % 16 : 0;
 #pragma unroll
     for (int h = 0; h < 16; ++h) {
       bf16_t lo = 0, hi = 0;
@@ -139,6 +162,7 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
     }
   }
   __syncthreads();  // one wave: orders the LDS writes above before the reads below
+  TR(2);
 
   // Q^T fragments (B operand): lane holds Q[head li][d = 32kk + 8*g4 + j]
   bf16x8 qf[D / 32];
@@ -183,21 +207,15 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
   }
   l += __shfl_xor(l, 16, WAVE);
   l += __shfl_xor(l, 32, WAVE);
+  TR(3);
 
-  // ---- O = P . V over two 32-key steps; V rows from registers into LDS (swizzled 16-B chunks)
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    if (32 * st < n) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int rr = 4 * q + g4;  // row within the step
-        const int k = 32 * st + rr;
-        u32x4 v = vv[8 * st + q];
-        if (start + k == pos) v = *reinterpret_cast<const u32x4*>(&vcur[li * 8]);
-        if (k >= n) v = u32x4{0u, 0u, 0u, 0u};
-        *reinterpret_cast<u32x4*>(vbuf[st] + rr * (D * 2) + 16 * (li ^ swz(rr))) = v;
-      }
-    }
+  // ---- O = P . V over two 32-key steps.  The V image has landed (the K wait above drained the
+  // DMA too); the owner chunk replaces the new token's row, which the cache did not hold yet.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (owner && lane < 16) {
+    const int rp = pos - start;
+    *reinterpret_cast<u32x4*>(vbuf[rp >> 5] + (rp & 31) * (D * 2) + 16 * (li ^ swz(rp & 31))) =
+        *reinterpret_cast<const u32x4*>(&vcur[li * 8]);
   }
   __syncthreads();
   f32x4 o[D / 16];
@@ -235,6 +253,7 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
   float lh[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) lh[i] = __shfl(l, 4 * g4 + i, WAVE);
+  TR(4);
   const int nlive = (ctx + CH - 1) / CH;
   if (nlive == 1) {
 #pragma unroll
@@ -247,6 +266,7 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
         for (int nn = 0; nn < D / 16; ++nn) op[16 * nn + li] = f2bf(o[nn][i] * inv);
       }
     }
+    TR(7);
     return;
   }
 
@@ -267,9 +287,11 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
     __hip_atomic_store(rec + G * D + G + li, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores land before its arrival counts
+  TR(5);
   uint32_t prev = 0;
   if (lane == 0) prev = __hip_atomic_fetch_add(&counters[pair], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   prev = __shfl(prev, 0, WAVE);
+  TR(6);
   if (prev != (uint32_t)(nlive - 1)) return;
   if (lane == 0) __hip_atomic_store(&counters[pair], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the add
@@ -320,6 +342,7 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
     for (int j = 0; j < 2 * G; ++j) stat[lane * 2 * G + j] = sv[j];
   }
   __syncthreads();
+  TR(8);
   float M = -INFINITY;
   for (int q = 0; q < nlive; ++q) M = fmaxf(M, stat[q * 2 * G + h]);
   float num[DPL];
@@ -339,15 +362,23 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
       }
     }
   }
+  TR(9);
   bf16_t* op = out + ((size_t)b * nq + kvh * G + h) * D + d0;
   const float inv = 1.f / den;
 #pragma unroll
   for (int j = 0; j < DPL; ++j) op[j] = f2bf(num[j] * inv);
+  TR(7);
 }
 
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+#ifdef K8S_ATTN_TRACE
+extern "C" int k8s_attn_trace_set(unsigned long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_trace), &p, sizeof(p));
+}
+#endif
 
 extern "C" long long k8s_decode_split_workspace(int B, int nq, int nkv, int pmax) {
   if (nkv <= 0 || nq % nkv != 0) return -1;
