@@ -46,6 +46,23 @@ def _load_gemm_table() -> bool:
     return ok
 
 
+def warm_library_gemms(model) -> None:
+    """Run every library GEMM shape the engine can issue (layer 0's projections at each row bucket of
+    ops.GEMM_M_BUCKETS) once, so hipBLASLt / rocBLAS load their kernels now instead of inside the first
+    timed prefill (a first-use code-object load cost ~0.3 s in a TP=8-shape run)."""
+    import torch
+
+    from .. import ops
+
+    w = model.layers[0]
+    for W in (w.wqkv, w.wo, w.wgu, w.wdown):
+        K = W.q.shape[1] if ops._is_fp8(W) else W.shape[1]
+        for M in ops.GEMM_M_BUCKETS:
+            x = torch.zeros(M, K, dtype=torch.bfloat16, device=model.device)
+            ops.linear(x, W)
+    torch.cuda.synchronize()
+
+
 def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str] = None, weights: Optional[str] = None,
                  tokenizer: Optional[str] = None, seed: int = 0, max_batch: int = 64, block_size: int = 16,
                  num_blocks: Optional[int] = None, kv_cache_gb: float = 0.0, kv_cache_fraction: float = 0.85,
@@ -79,6 +96,8 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
                     kv_cache_gb=kv_cache_gb, kv_cache_fraction=kv_cache_fraction, max_model_len=max_model_len,
                     max_prefill_tokens=max_prefill_tokens, cuda_graphs=cuda_graphs, prefix_caching=prefix_caching,
                     decode_chunk=decode_chunk, seed=seed, metrics=metrics, control=control)
+    if device.startswith("cuda"):
+        warm_library_gemms(model)
     if capture and eng.use_graphs:
         t1 = time.perf_counter()
         eng.capture_graphs()

@@ -308,6 +308,23 @@ def _use_skinny(M: int, w, K: int) -> bool:
     return SKINNY_ENABLED and not _is_fp8(w) and GEMV_MAX_M < M <= SKINNY_MAX_M and K % 256 == 0
 
 
+# Row counts of the library GEMMs in the tuned table (engine/assets/tunableop_gfx950.csv, written by
+# tools/tune_gemms.py): the engine's batched-decode buckets and the prefill buckets.  With the table
+# loaded, a library GEMM of M rows in (8, 1024] is padded to the next bucket so that it runs the
+# solution measured for that bucket instead of the library heuristic's pick for an odd M (TP=1,
+# 256 prompt rows: down 315 -> 177 us, QKV 80 -> 64 us; tools/prefill_gemm_probe.py).
+GEMM_M_BUCKETS = (16, 32, 48, 64, 96, 128, 192, 256, 320, 384, 448, 512, 640, 768, 896, 1024)
+
+
+def _lib_linear(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    M = x2.shape[0]
+    if M > GEMM_M_BUCKETS[-1] or M in GEMM_M_BUCKETS or not torch.cuda.tunable.is_enabled():
+        return torch.nn.functional.linear(x2, w)
+    Mp = next(b for b in GEMM_M_BUCKETS if b >= M)
+    xp = torch.nn.functional.pad(x2, (0, 0, 0, Mp - M))
+    return torch.nn.functional.linear(xp, w)[:M]
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
     """y = x @ w.T with w [N, K] bf16.  M <= 8 rows: hand-written HBM-streaming GEMV; M <= 64
     (batched decode): MFMA skinny GEMM; larger M (prefill): library GEMM (hipBLASLt via torch)."""
@@ -321,7 +338,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
     elif _is_fp8(w):
         y = _fp8_gemm(x2, w, out_dtype)
     else:
-        y = torch.nn.functional.linear(x2, w)
+        y = _lib_linear(x2, w)
         if out_dtype is not None and out_dtype != y.dtype:
             y = y.to(out_dtype)
     return y.view(*x.shape[:-1], y.shape[-1])
@@ -414,7 +431,7 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     elif _is_fp8(w_gate_up):
         y = silu_mul(_fp8_gemm(x2, w_gate_up))
     else:
-        y = silu_mul(torch.nn.functional.linear(x2, w_gate_up))
+        y = silu_mul(_lib_linear(x2, w_gate_up))
     return y.view(*x.shape[:-1], y.shape[-1])
 
 
