@@ -12,7 +12,9 @@
 //  * V tiles (64 keys x 128 d) are staged in LDS with an XOR swizzle and read with the gfx950
 //    transposing read ds_read_b64_tr_b16, which delivers 4 keys of one d column per lane --
 //    exactly the B-operand layout, so V needs no register transpose.
-//  * K fragments are loaded per lane straight from the cache (16-byte rows pieces).
+//  * K and V tiles are fetched one tile AHEAD into registers by all 256 threads (the loads of tile
+//    t+1 are in flight during tile t's MFMAs), then stored into swizzled LDS images shared by the
+//    4 waves; K fragments are read back with conflict-free ds_read_b128.
 //  * online softmax in the log2 domain (scale * log2(e) folded into S).
 #include "common.h"
 
@@ -28,7 +30,9 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
     const bf16_t* __restrict__ v_cache, const int* __restrict__ cu_q, const int* __restrict__ context_lens,
     const int* __restrict__ block_tables, float scale_log2, int nq, int nkv, int block_size, int max_blocks) {
   static_assert(D == 128, "head_dim 128");
-  constexpr int KT = 64;  // keys per tile
+  constexpr int KT = 64;             // keys per tile
+  constexpr int CPT = KT * D / 8 / 256;  // 16-byte chunks of one tile per thread (K and V each)
+  __shared__ __attribute__((aligned(16))) char klds[KT * D * 2];
   __shared__ __attribute__((aligned(16))) char vlds[KT * D * 2];
 
   const int s = blockIdx.z, h = blockIdx.y, tile = blockIdx.x;
@@ -40,6 +44,29 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int* bt = block_tables + (size_t)s * max_blocks;
+  const size_t kv_stride = (size_t)nkv * D;
+
+  const int last_row = min(tile * 64 + 63, qlen - 1);
+  const int kv_end = qstart + last_row + 1;  // keys needed by this workgroup
+  const int ntiles = (kv_end + KT - 1) / KT;
+
+  // Tile staging, one tile ahead: thread tid fetches chunks idx = tid + 256c (key row idx/16,
+  // 16-byte column chunk idx%16) of K and V into registers while the current tile is computed,
+  // then stores them swizzled into LDS.  Keys past the context: K clamped (their scores are
+  // masked), V zero (P is 0 there, V must be finite).
+  u32x4 kn[CPT], vn[CPT];
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int idx = tid + 256 * c;
+      const int key = t * KT + idx / (D / 8), ch = idx % (D / 8);
+      const int kc = min(key, ctx - 1);
+      const size_t off = (size_t)(bt[kc / block_size] * block_size + kc % block_size) * kv_stride + kvh * D + ch * 8;
+      kn[c] = *reinterpret_cast<const u32x4*>(k_cache + off);
+      vn[c] = key < ctx ? *reinterpret_cast<const u32x4*>(v_cache + off) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  fetch(0);
 
   // my query row (B operand columns / softmax rows)
   const int row = tile * 64 + wid * 16 + li;
@@ -57,38 +84,28 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   for (int n = 0; n < D / 16; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
 
-  const int last_row = min(tile * 64 + 63, qlen - 1);
-  const int kv_end = qstart + last_row + 1;  // keys needed by this workgroup
-  const int ntiles = (kv_end + KT - 1) / KT;
-  const size_t kv_stride = (size_t)nkv * D;
-
   for (int t = 0; t < ntiles; ++t) {
     const int kbase = t * KT;
-    // ---- stage V tile into LDS (swizzled 16-byte chunks); keys >= ctx are zero-filled
+    // ---- tile t: registers -> LDS (both images swizzled: 16-byte chunk ch of row r at ch ^ swz(r))
 #pragma unroll
-    for (int c = 0; c < (KT * D / 8) / 256; ++c) {
+    for (int c = 0; c < CPT; ++c) {
       const int idx = tid + 256 * c;
       const int kr = idx / (D / 8), ch = idx % (D / 8);
-      const int key = kbase + kr;
-      u32x4 val = u32x4{0u, 0u, 0u, 0u};
-      if (key < ctx) {
-        const int slot = bt[key / block_size] * block_size + key % block_size;
-        val = *reinterpret_cast<const u32x4*>(v_cache + slot * kv_stride + kvh * D + ch * 8);
-      }
-      *reinterpret_cast<u32x4*>(vlds + kr * (D * 2) + 16 * (ch ^ v_swz(kr))) = val;
+      *reinterpret_cast<u32x4*>(klds + kr * (D * 2) + 16 * (ch ^ (kr & 15))) = kn[c];
+      *reinterpret_cast<u32x4*>(vlds + kr * (D * 2) + 16 * (ch ^ v_swz(kr))) = vn[c];
     }
+    __syncthreads();
+    if (t + 1 < ntiles) fetch(t + 1);  // in flight during this tile's math
 
-    // ---- S^T = K . Q^T for 4 key sub-tiles of 16
+    // ---- S^T = K . Q^T for 4 key sub-tiles of 16; lane (li, g) reads key row 16m + li, d 32kk + 8g
     f32x4 sacc[KT / 16];
 #pragma unroll
     for (int m = 0; m < KT / 16; ++m) {
-      const int key = min(kbase + m * 16 + li, ctx - 1);
-      const int slot = bt[key / block_size] * block_size + key % block_size;
-      const bf16_t* kp = k_cache + slot * kv_stride + kvh * D + g * 8;
+      const int kr = 16 * m + li;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < D / 32; ++kk) {
-        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kp + kk * 32);
+        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(klds + kr * (D * 2) + 16 * ((4 * kk + g) ^ (kr & 15)));
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[kk], acc, 0, 0, 0);
       }
       sacc[m] = acc;
@@ -147,7 +164,6 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
         pa[st][4 + j] = (__bf16)sacc[2 * st + 1][j];
       }
     }
-    __syncthreads();  // V tile visible
 
     const int qd = li >> 2, pd = li & 3;  // tr-read lane roles: row q, column group p
 #pragma unroll
@@ -168,7 +184,7 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
         o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[st], vb, o[n], 0, 0, 0);
       }
     }
-    __syncthreads();  // before the next tile overwrites vlds
+    __syncthreads();  // before the next tile overwrites the LDS images
   }
 
   // ---- normalise and store: o[n][i] = O[row 4g+i][d 16n + li]

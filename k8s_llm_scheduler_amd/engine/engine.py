@@ -28,6 +28,7 @@ from __future__ import annotations
 import itertools
 import logging
 import math
+import os
 import random
 import threading
 import time
@@ -47,6 +48,12 @@ from ..utils.tracing import trace
 log = logging.getLogger(__name__)
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
+# Single-sequence prompt chunks up to 512 tokens are padded to one of these lengths and replayed
+# from a captured graph, which removes the host launch gaps between the ~10 kernels per layer
+# (tools/prefill_probe.py, 256 tokens: TP=8 shapes 12.53 ms eager -> 12.28 ms replayed; TP=1 44.0 ms
+# either way -- the chunk is GEMM-bound, profiles/rocprof_prefill_tp8.txt).  The padding tokens
+# belong to no sequence (cu_q stops at the real length) and write their K/V into a scratch block.
+PREFILL_GRAPH_BUCKETS = (64, 128, 192, 256, 320, 384, 448, 512)
 
 
 @dataclass
@@ -120,7 +127,9 @@ class LLMEngine:
             raise RuntimeError(f"KV cache too small: {num_blocks} blocks < one full sequence "
                                f"({self.max_blocks_per_seq})")
         self.num_blocks = num_blocks
-        model.allocate_kv(num_blocks, block_size)
+        # one extra block past the allocator's range: the K/V sink of prefill-graph padding tokens
+        model.allocate_kv(num_blocks + 1, block_size)
+        self.scratch_slot = num_blocks * block_size
         self.prefix_caching = prefix_caching
         self._share_deferred = False
         self.allocator = ops.native().BlockAllocator(num_blocks, block_size, prefix_caching) if ops.available() \
@@ -134,10 +143,11 @@ class LLMEngine:
         self.free_slots = list(range(max_batch - 1, -1, -1))
         self.use_graphs = cuda_graphs and self.gpu
         self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}   # (batch bucket, context class)
+        self.prefill_graphs: Dict[int, tuple] = {}             # token bucket -> (graph, logits)
         self._graph_pool = None
         self.lock = threading.RLock()
         self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
-                      "graph_replays": 0, "prefill_time": 0.0, "decode_time": 0.0}
+                      "graph_replays": 0, "prefill_graph_replays": 0, "prefill_time": 0.0, "decode_time": 0.0}
 
     # ------------------------------------------------------------------ device state
     def _alloc_state(self) -> None:
@@ -151,6 +161,11 @@ class LLMEngine:
         self.s_seeds = torch.zeros(B, **i32)
         self.s_steps = torch.zeros(B, **i32)
         self.s_hist = torch.zeros(B, self.max_new_cap, **i32)
+        # prefill-graph inputs, one packed buffer filled by one host->device copy per chunk:
+        # [ids | positions | slots] x Tmax, then cu_q (2), context_lens (1), last_idx (1)
+        Tm = PREFILL_GRAPH_BUCKETS[-1]
+        self.p_packed = torch.zeros(3 * Tm + 4, **i32)
+        self.p_bt = torch.zeros(1, self.max_blocks_per_seq, **i32)
 
     def _ctx_classes(self) -> List[int]:
         """Context-length classes with their own decode graph: contexts <= 1024 tokens (one
@@ -197,7 +212,63 @@ class LLMEngine:
                 if self._graph_pool is None:
                     self._graph_pool = g.pool()
                 self.graphs[(B, mc)] = g
+        if self.prefill_graphs_enabled():
+            for Tb in PREFILL_GRAPH_BUCKETS:
+                if Tb in self.prefill_graphs:
+                    continue
+                # a harmless chunk: Tb tokens of one sequence over block 0 whose K/V all go to the
+                # scratch block (block 0 is only read)
+                self._fill_prefill_state([0] * Tb, list(range(Tb)), [self.scratch_slot] * Tb, Tb, [0], Tb)
+                stream.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(stream):
+                    self._prefill_graph_body(Tb)
+                torch.cuda.current_stream(self.device).wait_stream(stream)
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._graph_pool, stream=stream):
+                    logits = self._prefill_graph_body(Tb)
+                if self._graph_pool is None:
+                    self._graph_pool = g.pool()
+                self.prefill_graphs[Tb] = (g, logits)
         torch.cuda.synchronize(self.device)
+
+    def prefill_graphs_enabled(self) -> bool:
+        """Single-rank engines only by default: a TP > 1 prefill carries 4-8 MiB all-reduces that
+        may leave the xGMI kernels for RCCL (or gloo in the 1-GPU rehearsal, which cannot be
+        captured); ``K8S_PREFILL_GRAPHS=1`` opts a multi-rank RCCL engine in."""
+        tp = self.model.tp
+        single = tp.world <= 1 or tp.simulate
+        env = os.environ.get("K8S_PREFILL_GRAPHS", "")
+        on = env == "1" or (env == "" and single)
+        return on and self.use_graphs and PREFILL_GRAPH_BUCKETS[-1] <= self.max_prefill_tokens
+
+    def _p_views(self, Tb: int):
+        Tm = PREFILL_GRAPH_BUCKETS[-1]
+        pk = self.p_packed
+        return (pk[:Tb], pk[Tm:Tm + Tb], pk[2 * Tm:2 * Tm + Tb], pk[3 * Tm:3 * Tm + 2], pk[3 * Tm + 2:3 * Tm + 3],
+                pk[3 * Tm + 3:3 * Tm + 4])
+
+    def _prefill_graph_body(self, Tb: int) -> torch.Tensor:
+        ids, pos, slots, cu, ctx, last = self._p_views(Tb)
+        return self.model.forward_prefill(ids, pos, slots, cu, ctx, self.p_bt, Tb, last)
+
+    def _fill_prefill_state(self, ids, pos, slots, ctx_len: int, blocks, Tb: int) -> None:
+        """One chunk of ONE sequence into the graph's static inputs; positions Tb-T.. are padding
+        (token 0 at position 0, K/V into the scratch slot, outside cu_q)."""
+        T, Tm = len(ids), PREFILL_GRAPH_BUCKETS[-1]
+        pad = Tb - T
+        host = torch.zeros(3 * Tm + 4, dtype=torch.int32)
+        host[:T] = torch.tensor(ids, dtype=torch.int32)
+        host[Tm:Tm + T] = torch.tensor(pos, dtype=torch.int32)
+        host[2 * Tm:2 * Tm + T] = torch.tensor(slots, dtype=torch.int32)
+        host[2 * Tm + T:2 * Tm + T + pad] = self.scratch_slot
+        host[3 * Tm + 1] = T
+        host[3 * Tm + 2] = ctx_len
+        host[3 * Tm + 3] = T - 1
+        bt = torch.zeros(1, self.max_blocks_per_seq, dtype=torch.int32)
+        bt[0, :len(blocks)] = torch.tensor(blocks, dtype=torch.int32)
+        self.p_packed.copy_(host.to(self.device, non_blocking=True))
+        self.p_bt.copy_(bt.to(self.device, non_blocking=True))
 
     # ------------------------------------------------------------------ requests
     def render_chat(self, system: str, user: str) -> List[int]:
@@ -338,8 +409,16 @@ class LLMEngine:
         dev = self.device
         t = lambda x: torch.tensor(x, dtype=torch.int32).to(dev, non_blocking=True)
         t0 = time.perf_counter()
-        logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx), bt.to(dev, non_blocking=True),
-                                            max(e - s for _, s, e in chunk), t(last))
+        Tb = next((b for b in PREFILL_GRAPH_BUCKETS if b >= len(ids)), None) if len(chunk) == 1 else None
+        if self.use_graphs and Tb is not None and Tb in self.prefill_graphs:
+            r0 = chunk[0][0]
+            self._fill_prefill_state(ids, pos, slots, ctx[0], r0.blocks, Tb)
+            graph, logits = self.prefill_graphs[Tb]
+            graph.replay()
+            self.stats["prefill_graph_replays"] += 1
+        else:
+            logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx), bt.to(dev, non_blocking=True),
+                                                max(e - s for _, s, e in chunk), t(last))
         self.stats["prefill_tokens"] += len(ids)
         done = [(i, r) for i, (r, s, e) in enumerate(chunk) if e == len(r.prompt_ids)]
         for r, s, e in chunk:

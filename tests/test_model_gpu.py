@@ -66,6 +66,9 @@ def test_engine_gpu_generate_and_graph():
     assert [o.token_ids for o in batched] == [o.token_ids for o in single]
     assert all(len(o.token_ids) == 20 for o in batched)
     assert eng.stats["graph_replays"] > 0
+    # single-sequence prompts were prefilled by padded graph replays, the 3-prompt chunk eagerly:
+    # identical tokens above, so the padding tokens touched nothing but the scratch block
+    assert eng.stats["prefill_graph_replays"] >= 3
     # graph replay == eager step
     eng.use_graphs = False
     eager = eng.generate(prompts[:1], p)[0]
