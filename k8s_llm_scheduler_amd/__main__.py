@@ -1,4 +1,4 @@
-"""Command line: ``python -m k8s_llm_scheduler_amd [run|verify|smoke]``.
+"""Command line: ``python -m k8s_llm_scheduler_amd [run|verify|smoke|e2e]``.
 
 ``run`` is the reference's ``python scheduler.py`` (``scheduler.py:775-823``): banner, build the
 scheduler, watch pods until Ctrl+C, print final statistics.  Under ``torchrun`` (one process per
@@ -8,6 +8,8 @@ follows rank 0's engine schedule (tensor parallel over RCCL).
 ``verify`` replaces ``verify_setup.py`` (files, env, packages, GPU + native extension, cluster).
 ``smoke`` replaces ``test_runner.py``: apply the three ai-test-pods, wait, count bound pods --
 against a real cluster, or fully in-process with ``--fake`` (no cluster needed).
+``e2e`` replaces ``test_e2e.py``: verify, clean up, list nodes, start the scheduler, apply the
+test pods, wait 10 s, then require every pod scheduled AND Running.
 """
 
 from __future__ import annotations
@@ -220,12 +222,16 @@ def cmd_verify(args, cfg: Config) -> int:
     return 0 if ok else 1
 
 
-def cmd_smoke(args, cfg: Config) -> int:
-    """test_runner.py semantics: (re)create the 3 test pods, wait, report how many got a node."""
+def _test_pods() -> list:
     import yaml
 
     docs = [d for d in yaml.safe_load_all(TEST_PODS.read_text()) if d]
-    pods = [it for d in docs for it in (d.get("items", []) if d.get("kind") == "List" else [d])]
+    return [it for d in docs for it in (d.get("items", []) if d.get("kind") == "List" else [d])]
+
+
+def cmd_smoke(args, cfg: Config) -> int:
+    """test_runner.py semantics: (re)create the 3 test pods, wait, report how many got a node."""
+    pods = _test_pods()
     if args.fake_cluster:
         api = _fake_cluster(args.fake_cluster)
         backend = build_backend(cfg).backend if cfg.engine.backend != "local" or args.with_engine else None
@@ -270,9 +276,104 @@ def cmd_smoke(args, cfg: Config) -> int:
     return 0 if bound == len(pods) else 1
 
 
+def cmd_e2e(args, cfg: Config) -> int:
+    """test_e2e.py semantics (reference ``test_e2e.py:26-152``) without the human in the loop.
+
+    Steps: 1 verify (exit 1 on failure), 2 delete old test pods, 3 list the cluster's nodes,
+    4 start the scheduler -- in this process by default; ``--external-scheduler`` keeps the
+    reference's "start it in another terminal, press ENTER" step --, 5 apply the test pods and wait
+    ``--wait`` seconds (reference: 10), 6 report phase / node / schedulerName per pod.  Success
+    requires every test pod scheduled AND Running, as the reference's final verdict does."""
+    bar = "=" * 70
+    print(bar + "\n AI Kubernetes Scheduler - End-to-End Test (MI355X decision engine)\n" + bar)
+    print("\n Step 1: Verifying setup...")
+    if cmd_verify(args, cfg) != 0:
+        print(" Setup verification failed. Please fix issues first.")
+        return 1
+    pods = _test_pods()
+    names = [p["metadata"]["name"] for p in pods]
+    if args.fake_cluster:
+        api = _fake_cluster(args.fake_cluster)
+    else:
+        from .kube.rest import KubeConnection, RestKubeAPI
+
+        api = RestKubeAPI(KubeConnection.auto(args.kubeconfig))
+    print("\n Step 2: Cleaning up existing test pods...")
+    for n in names:
+        try:
+            api.delete_pod("default", n)
+        except Exception:  # noqa: BLE001 -- --ignore-not-found
+            pass
+    print("\n Step 3: Checking Kubernetes cluster...")
+    try:
+        nodes = api.list_nodes()
+    except Exception as e:  # noqa: BLE001
+        print(f" Cannot connect to Kubernetes: {e}")
+        return 1
+    print(f" Cluster has {len(nodes)} nodes:")
+    for nd in nodes:
+        print(f"   - {nd['metadata']['name']}")
+
+    print("\n" + bar + "\n Step 4: Start the Scheduler\n" + bar)
+    wait = args.wait if args.wait_set else 10.0
+
+    def apply_and_wait():
+        print("\n Step 5: Creating test pods...")
+        for p in pods:
+            api.create_pod(p)
+        print(f"\n Waiting {wait:.0f} seconds for scheduling...")
+
+    if args.external_scheduler:
+        print("\n Start the scheduler in another terminal: python scheduler.py (wait for 'Watching for pods')")
+        input("\n Press ENTER when the scheduler is running...")
+        apply_and_wait()
+        time.sleep(wait)
+    else:
+        rt = build_backend(cfg) if cfg.engine.backend != "local" or args.with_engine else None
+        sched = build_scheduler(cfg, api, rt.backend if rt else None)
+        print(" scheduler started in-process (schedulerName "
+              f"{cfg.scheduler.name}, backend {cfg.engine.backend if rt else 'fallback'})")
+
+        async def run():
+            task = asyncio.create_task(sched.start())
+            await asyncio.sleep(0.1)
+            apply_and_wait()
+            t0 = time.time()
+            while time.time() - t0 < wait:
+                cur = [api.get_pod("default", n) or {} for n in names]
+                if all((c.get("status") or {}).get("phase") == "Running" for c in cur):
+                    break
+                await asyncio.sleep(0.05)
+            sched.stop()
+            await asyncio.wait_for(task, 10)
+
+        try:
+            asyncio.run(run())
+        finally:
+            if rt is not None:
+                rt.shutdown()
+
+    print("\n Step 6: Checking pod status...\n" + "-" * 70)
+    print(f"{'POD NAME':<20} {'STATUS':<12} {'NODE':<20} SCHEDULER")
+    print("-" * 70)
+    scheduled = running = 0
+    for n in names:
+        cur = api.get_pod("default", n) or {}
+        spec, phase = cur.get("spec") or {}, (cur.get("status") or {}).get("phase", "?")
+        scheduled += bool(spec.get("nodeName"))
+        running += phase == "Running"
+        print(f"{n:<20} {phase:<12} {spec.get('nodeName') or 'Not scheduled':<20} {spec.get('schedulerName', '')}")
+    print("-" * 70 + f"\n Results:\n   - Scheduled: {scheduled}/{len(names)} pods\n"
+          f"   - Running:   {running}/{len(names)} pods")
+    ok = scheduled == running == len(names)
+    print("\n" + bar + ("\n SUCCESS! All pods scheduled and running!" if ok else
+                        "\n FAILED: not every test pod was scheduled and running.") + "\n" + bar)
+    return 0 if ok else 1
+
+
 def main(argv: Optional[list] = None) -> int:
     ap = argparse.ArgumentParser(prog="k8s_llm_scheduler_amd", description=__doc__.splitlines()[0])
-    ap.add_argument("command", nargs="?", default="run", choices=["run", "verify", "smoke"])
+    ap.add_argument("command", nargs="?", default="run", choices=["run", "verify", "smoke", "e2e"])
     ap.add_argument("--config", default=None, help="config.yaml (default: $SCHEDULER_CONFIG or ./config.yaml)")
     ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--fake-cluster", type=int, default=0, metavar="N",
@@ -281,9 +382,15 @@ def main(argv: Optional[list] = None) -> int:
     ap.add_argument("--duration", type=float, default=0.0, help="(run) stop after N seconds")
     ap.add_argument("--backend", choices=["local", "fallback", "scripted"], default=None)
     ap.add_argument("--preset", default=None)
-    ap.add_argument("--wait", type=float, default=30.0, help="(smoke) seconds to wait (test_runner.py: 30)")
+    ap.add_argument("--wait", type=float, default=None,
+                    help="seconds to wait for scheduling (smoke: 30 as test_runner.py, e2e: 10 as test_e2e.py)")
+    ap.add_argument("--external-scheduler", action="store_true",
+                    help="(e2e) the scheduler runs elsewhere: wait for ENTER like test_e2e.py instead of starting it")
     ap.add_argument("--with-engine", action="store_true", help="(smoke --fake-cluster) build the GPU engine")
     args = ap.parse_args(argv)
+    args.wait_set = args.wait is not None
+    if args.wait is None:
+        args.wait = 30.0
     load_dotenv()
     cfg = load_config(args.config)
     if args.backend:
@@ -293,7 +400,7 @@ def main(argv: Optional[list] = None) -> int:
     from .utils.logging import setup_logging
 
     setup_logging(cfg.logging.level, cfg.logging.format, cfg.logging.file)
-    return {"run": cmd_run, "verify": cmd_verify, "smoke": cmd_smoke}[args.command](args, cfg)
+    return {"run": cmd_run, "verify": cmd_verify, "smoke": cmd_smoke, "e2e": cmd_e2e}[args.command](args, cfg)
 
 
 if __name__ == "__main__":

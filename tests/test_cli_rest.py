@@ -20,6 +20,15 @@ def test_cli_smoke_fake_cluster_fallback(capsys):
     assert "Results: 3/3 pods scheduled" in capsys.readouterr().out
 
 
+def test_cli_e2e_fake_cluster_scripted(capsys):
+    """test_e2e.py flow: verify, cleanup, node list, in-process scheduler, apply, scheduled AND Running."""
+    assert cli(["e2e", "--fake-cluster", "3", "--backend", "scripted", "--wait", "5"]) == 0
+    out = capsys.readouterr().out
+    for line in ("Cluster has 3 nodes:", "Scheduled: 3/3 pods", "Running:   3/3 pods", "SUCCESS! All pods scheduled"):
+        assert line in out, line
+    assert out.count("ai-llama-scheduler") >= 3  # schedulerName column
+
+
 def test_cli_run_scripted_demo(capsys):
     assert cli(["run", "--fake-cluster", "3", "--backend", "scripted", "--demo-pods", "--duration", "1.5"]) == 0
     out = capsys.readouterr().out
