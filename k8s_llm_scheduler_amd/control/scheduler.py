@@ -71,7 +71,11 @@ class CustomScheduler:
     @classmethod
     def from_config(cls, cfg, api: KubeAPI, decision_service: DecisionService, metrics=None,
                     engine_label: Optional[str] = None) -> "CustomScheduler":
-        label = engine_label or f"local {cfg.llm.model.split('/')[-1].replace('-Instruct', '')}"
+        label = f"local {cfg.llm.model.split('/')[-1].replace('-Instruct', '')}"
+        eng = getattr(cfg, "engine", None)
+        if eng is not None and eng.backend == "local" and "70b" not in eng.preset.lower():
+            label = f"local {eng.preset}"  # the served model, not the config's llm.model
+        label = engine_label or label
         return cls(cfg.scheduler.name, api, decision_service,
                    snapshot_mode=cfg.compat.snapshot_mode, quantity_mode=cfg.compat.quantity_parsing,
                    status_always_ready=cfg.compat.prompt_status_always_ready,
