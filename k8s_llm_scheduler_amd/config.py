@@ -34,7 +34,7 @@ import yaml
 class SchedulerSection:
     name: str = "ai-llama-scheduler"          # config.yaml:3
     watch_interval: int = 60                  # config.yaml:4 (reference hard-codes 60, scheduler.py:666)
-    mode: str = "sequential"                  # "sequential" (reference) | "batched"
+    mode: str = "sequential"                  # "sequential" (reference) | "batched" | "continuous"
     max_batch: int = 64                       # pending pods drained per batched round
     batch_window_ms: float = 20.0             # how long to wait for more pending pods
     error_backoff_s: float = 5.0              # scheduler.py:685

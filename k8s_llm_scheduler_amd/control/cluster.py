@@ -15,8 +15,8 @@ Two modes (``compat.snapshot_mode``):
 ``informer``  one ``list_nodes`` per snapshot; pod counts per node are maintained from the pod
               watch stream (``observe``) plus an *assume* step right after our own successful
               bindings, so a snapshot taken immediately after a bind already counts the pod --
-              what the apiserver would have answered the reference.  Counts are seeded with one
-              LIST at start-up.
+              what the apiserver would have answered the reference.  Counts are rebuilt from a
+              LIST at the start of every watch stream (LIST + WATCH from its resourceVersion).
 """
 
 from __future__ import annotations
@@ -90,6 +90,12 @@ class ClusterSnapshotter:
     # ------------------------------------------------------------ informer bookkeeping
     def seed(self) -> None:
         pods, _ = self.api.list_pods()
+        self.resync(pods)
+
+    def resync(self, pods: Sequence[Obj]) -> None:
+        """Replace the pod -> node map with one LIST result.  Called at the start of every watch
+        stream (the watch then continues from that LIST's resourceVersion), so pods deleted while
+        no stream was open -- e.g. during the 5 s error back-off -- cannot linger in the counts."""
         with self._lock:
             self._pod_node = {pod_key(p): p["spec"]["nodeName"] for p in pods
                               if (p.get("spec") or {}).get("nodeName")}

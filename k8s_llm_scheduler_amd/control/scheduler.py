@@ -14,6 +14,10 @@ Changed (docs/COMPAT.md):
 * DELETED events are ignored and pods are de-duplicated by UID while in flight and after a
   successful bind (quirk 8: duplicate events double-bind and get 409).  Set
   ``compat.watch_all_event_types`` to restore the reference filter.
+* ``scheduler.mode: continuous`` hands every detected pod to a worker at once (up to ``max_batch``
+  in flight); the engine runs in its background loop, so each decision joins the running decode
+  batch at the next engine step and is bound as soon as it is done (re-validated against the
+  current node counts).
 * ``scheduler.mode: batched`` drains up to ``max_batch`` pending pods and decides them in ONE
   engine call (continuous batching on the GPU).  All pods of a round see the same snapshot;
   bindings are applied in order and each is re-validated against the snapshot updated with
@@ -24,6 +28,7 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import concurrent.futures
 import logging
 import threading
 import time
@@ -37,6 +42,18 @@ from .models import NodeMetrics, SchedulingDecision
 from .prompt import PromptEngine
 
 log = logging.getLogger(__name__)
+
+
+def start_backend_loop(backend) -> bool:
+    """Put the decision engine behind ``backend`` (possibly wrapped, e.g. by FaultInjectingBackend) in
+    background-loop mode, so concurrent decisions share engine steps.  False if there is none."""
+    while backend is not None:
+        eng = getattr(backend, "engine", None)
+        if eng is not None and hasattr(eng, "start_background"):
+            eng.start_background()
+            return True
+        backend = getattr(backend, "inner", None)
+    return False
 
 
 class CustomScheduler:
@@ -65,6 +82,8 @@ class CustomScheduler:
         self._lock = threading.Lock()
         self._inflight: Set[str] = set()
         self._bound: "collections.OrderedDict[str, None]" = collections.OrderedDict()
+        self._bind_lock = threading.Lock()
+        self._pool: Optional[concurrent.futures.ThreadPoolExecutor] = None
         self.decision_latencies: Deque[float] = collections.deque(maxlen=100000)
         self.stats = {"total_scheduled": 0, "llm_decisions": 0, "fallback_decisions": 0, "failed_bindings": 0}
 
@@ -88,12 +107,16 @@ class CustomScheduler:
     # ------------------------------------------------------------------ lifecycle
     async def start(self) -> None:
         self.running = True
+        if self.mode == "continuous":
+            start_backend_loop(self.llm_client.backend)
         log.info(f" Starting {self.scheduler_name}...")
         log.info(f" Watching for pods with schedulerName={self.scheduler_name}")
         await self._watch_pods()
 
     def stop(self) -> None:
         self.running = False
+        if self._pool is not None:
+            self._pool.shutdown(wait=False)
         stopper = getattr(self.api, "stop_watches", None)
         if stopper:
             stopper()
@@ -138,9 +161,14 @@ class CustomScheduler:
 
     # ------------------------------------------------------------------ watch loop
     def _watch_thread(self, loop: asyncio.AbstractEventLoop, q: "asyncio.Queue") -> None:
+        """LIST + WATCH: every (re)stream starts with one LIST, handed to the consumer as a SYNC
+        event (informer counts are rebuilt from it and every listed pod is considered as the
+        reference's re-stream would, quirk 9), then watches from that LIST's resourceVersion."""
         while self.running:
             try:
-                for ev in self.api.watch_pods(None, timeout_seconds=self.watch_timeout):
+                pods, rv = self.api.list_pods()
+                loop.call_soon_threadsafe(q.put_nowait, ("SYNC", pods))
+                for ev in self.api.watch_pods(rv or None, timeout_seconds=self.watch_timeout):
                     if not self.running:
                         break
                     loop.call_soon_threadsafe(q.put_nowait, ev)
@@ -157,30 +185,52 @@ class CustomScheduler:
         t = threading.Thread(target=self._watch_thread, args=(loop, q), name="pod-watch", daemon=True)
         t.start()
         log.info(" Watching for unscheduled pods...")
+        pending: Deque = collections.deque()
+
+        async def next_event(timeout: Optional[float] = None):
+            """Next pod event in stream order (SYNC lists expand to ADDED events); "TIMEOUT" or None
+            (stream closed)."""
+            while not pending:
+                try:
+                    ev = await (asyncio.wait_for(q.get(), timeout) if timeout is not None else q.get())
+                except asyncio.TimeoutError:
+                    return "TIMEOUT"
+                if ev is None:
+                    return None
+                typ, obj = ev
+                if typ == "SYNC":
+                    self.context_manager.resync(obj)
+                    pending.extend(("ADDED", p) for p in obj)
+                else:
+                    self.context_manager.observe(typ, obj)
+                    pending.append(ev)
+            return pending.popleft()
+
+        inflight: Set["asyncio.Future"] = set()
+        slots = asyncio.Semaphore(self.max_batch)
         try:
             while self.running:
-                ev = await q.get()
+                ev = await next_event()
                 if ev is None:
                     break
                 typ, pod = ev
-                self.context_manager.observe(typ, pod)
                 if not self.wants(typ, pod):
                     continue
-                if self.mode == "batched":
+                if self.mode == "continuous":
+                    await self._dispatch(loop, pod, inflight, slots)
+                elif self.mode == "batched":
                     batch = [pod]
                     deadline = loop.time() + self.batch_window
                     while len(batch) < self.max_batch:
                         left = deadline - loop.time()
                         if left <= 0:
                             break
-                        try:
-                            nxt = await asyncio.wait_for(q.get(), timeout=left)
-                        except asyncio.TimeoutError:
+                        nxt = await next_event(left)
+                        if nxt == "TIMEOUT":
                             break
                         if nxt is None:
                             self.running = False
                             break
-                        self.context_manager.observe(*nxt)
                         if self.wants(*nxt) and all(pod_uid(nxt[1]) != pod_uid(b) for b in batch):
                             batch.append(nxt[1])
                     await loop.run_in_executor(None, self.schedule_batch, batch)
@@ -191,6 +241,29 @@ class CustomScheduler:
                     log.info(f"{'=' * 60}\n")
         finally:
             self.running = False
+            if inflight:
+                await asyncio.gather(*inflight, return_exceptions=True)
+
+    async def _dispatch(self, loop, pod: Obj, inflight: Set["asyncio.Future"], slots: asyncio.Semaphore) -> None:
+        """Continuous mode: claim the pod now (duplicates of it are dropped from here on) and run its
+        pipeline on a worker thread; up to ``max_batch`` decisions are in the engine at once and the
+        engine's background loop batches them step by step."""
+        if not self._claim(pod):
+            return
+        t_detect = time.perf_counter()
+        log.info(f" Detected pod: {pod['metadata'].get('namespace')}/{pod['metadata'].get('name')}")
+        await slots.acquire()
+        if self._pool is None:
+            self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=self.max_batch,
+                                                               thread_name_prefix="decide")
+        fut = loop.run_in_executor(self._pool, self._schedule_claimed, pod, t_detect, True)
+        inflight.add(fut)
+
+        def _done(f):
+            inflight.discard(f)
+            slots.release()
+
+        fut.add_done_callback(_done)
 
     # ------------------------------------------------------------------ pipelines
     def _record(self, decision: SchedulingDecision, t0: float) -> None:
@@ -227,9 +300,11 @@ class CustomScheduler:
         """The reference's per-pod pipeline (scheduler.py:690-729), synchronous."""
         if not self._claim(pod):
             return None
+        return self._schedule_claimed(pod, time.perf_counter(), False)
+
+    def _schedule_claimed(self, pod: Obj, t0: float, revalidate: bool) -> Optional[SchedulingDecision]:
         bound = False
         try:
-            t0 = time.perf_counter()
             spec = pod_to_spec(pod, self.qmode)
             nodes = self.context_manager.get_node_metrics()
             if not nodes:
@@ -238,11 +313,28 @@ class CustomScheduler:
             prompt = self.prompt_engine.construct_scheduling_prompt(spec, nodes)
             log.info(f" Calling {self.engine_label} for scheduling decision...")
             decision = self.llm_client.get_scheduling_decision(prompt, spec, nodes)
+            if revalidate and decision.selected_node:
+                # concurrent decisions saw snapshots taken before each other's bindings: re-check the
+                # chosen node against the current counts (which include our own assumed bindings)
+                with self._bind_lock:
+                    decision = self._revalidate(decision)
+                    self._record(decision, t0)
+                    bound = self._bind(pod, decision)
+                return decision
             self._record(decision, t0)
             bound = self._bind(pod, decision)
             return decision
         finally:
             self._release(pod, bound)
+
+    def _revalidate(self, d: SchedulingDecision) -> SchedulingDecision:
+        current = self.context_manager.get_node_metrics()
+        target = find_node(current, d.selected_node)
+        if target is not None and target.max_pods > 0 and target.pod_count >= target.max_pods:
+            return self.llm_client.fallback.decide(
+                [n for n in current if n.max_pods == 0 or n.pod_count < n.max_pods],
+                f"Node {d.selected_node} full after concurrent bindings")
+        return d
 
     def schedule_batch(self, pods: Sequence[Obj]) -> List[Optional[SchedulingDecision]]:
         """Batched round: one snapshot, one engine call, in-order validated bindings."""

@@ -62,6 +62,12 @@ int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, in
 int k8s_silu_mul(void* out, const void* gu, int T, int I, hipStream_t s);
 int k8s_hash_init(void* out, int rows, int cols, long long gcols, long long row0, long long col0, uint32_t seed,
                   uint32_t tensor_id, float scale, float shift, hipStream_t s);
+int k8s_mgemm_num_configs();
+int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* lds_bytes, int* swiglu);
+int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, long long* tiles, int* cmax,
+                        long long* ws_elems);
+int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs, const float* wsc,
+              int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax, hipStream_t s);
 }
 
 namespace {
@@ -184,6 +190,29 @@ PYBIND11_MODULE(_C, m) {
   m.def("hash_init", [](uintptr_t out, int rows, int cols, long long gcols, long long row0, long long col0,
                         uint32_t seed, uint32_t tid, float scale, float shift, int64_t s) {
     check(k8s_hash_init(P(out), rows, cols, gcols, row0, col0, seed, tid, scale, shift, S(s)), "hash_init");
+  });
+
+  m.def("mgemm_configs", []() {
+    py::list out;
+    for (int c = 0; c < k8s_mgemm_num_configs(); ++c) {
+      int bm = 0, bn = 0, th = 0, lds = 0, sw = 0;
+      k8s_mgemm_config(c, &bm, &bn, &th, &lds, &sw);
+      out.append(py::make_tuple(bm, bn, th, lds, sw != 0));
+    }
+    return out;
+  });
+  m.def("mgemm_plan_info", [](int M, int N, int K, int epi, int fp8, int cfg, int nwg) {
+    long long tiles = 0, ws = 0;
+    int cmax = 0;
+    if (k8s_mgemm_plan_info(M, N, K, epi, fp8, cfg, nwg, &tiles, &cmax, &ws) != 0)
+      throw std::invalid_argument("mgemm_plan_info: invalid plan");
+    return py::make_tuple(tiles, cmax, ws);
+  });
+  m.def("mgemm", [](uintptr_t out, uintptr_t ws, uintptr_t tickets, uintptr_t x, uintptr_t W, uintptr_t xs,
+                    uintptr_t wsc, int M, int N, int K, int epi, int fp8, int cfg, int nwg, int cmax, int64_t s) {
+    check(k8s_mgemm(P(out), P<float>(ws), P<unsigned>(tickets), P(x), P(W), P<float>(xs), P<float>(wsc), M, N, K,
+                    epi, fp8, cfg, nwg, cmax, S(s)),
+          "mgemm");
   });
 
   using k8sllm::RcclComm;

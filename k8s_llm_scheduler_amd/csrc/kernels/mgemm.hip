@@ -1,0 +1,490 @@
+// K3 / K8 / K9(+K10) / K11 / K15: hand-written MFMA GEMM for projections with more than 8 rows
+// (prefill chunks, batched decode), bf16 or OCP-e4m3 weights, fp32 accumulate (gfx950).
+//
+//     out[M, N] = epi( x[M, K] . W[N, K]^T )        epi: bf16 | fp32 | SwiGLU (silu(g) * u)
+//
+// Design (MI355X-first, not a library tile recompiled):
+//  * swapped orientation C^T = W . x^T on v_mfma_f32_16x16x32_bf16 (fp8: _16x16x32_fp8_fp8): the
+//    A operand is 16 weight rows, the B operand 16 activation rows, both K-contiguous, so both are
+//    staged the same way and every lane ends with 4 CONSECUTIVE output columns of one row
+//    (one 8-byte bf16 / 16-byte fp32 store, and gate/up pairs side by side for SwiGLU).
+//  * both operands move HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4): no VGPR staging, an
+//    S-deep ring of 128-byte-wide k-steps (64 bf16 or 128 e4m3 per row), counted `s_waitcnt
+//    vmcnt` so S-2 k-steps stay in flight across each raw s_barrier (MI355X_MICROARCH: LDS-DMA
+//    stays in flight across barriers; __syncthreads would drain it).
+//  * the LDS image is lane-linear (DMA destination = base + 16 * lane); the XOR swizzle that makes
+//    the fragment reads (16 rows x one 16-byte column, ds_read_b128) conflict-free is applied on the
+//    per-lane GLOBAL source address: 16-byte chunk c of row r lives at slot c ^ ((r >> 1) & 7).
+//  * block -> tile mapping is XCD-aware (blocks b, b+8, .. share an XCD and get a contiguous
+//    logical range), with the k-slices of one tile adjacent, then the m-tiles of one n-tile:
+//    the weights a tile streams are re-read by its neighbours from the same L2.
+//  * split-K for small grids (TP = 8 shapes: N = 1280, K = 8192): every slice writes an fp32 slab
+//    in fragment order, publishes it (agent release + arrival ticket), and the last arriving slice
+//    of a tile reduces all slabs and applies the epilogue in the same launch (no memset, no
+//    second kernel; the ticket is reset by the reducer).
+//  * fp8: activations are quantized per token (fp8.hip), weights per row; the epilogue applies
+//    sx[m] * sw[n].  Non-scaled fp8 MFMA runs at the bf16 rate but halves the staged bytes.
+#include "common.h"
+
+namespace k8sllm {
+
+namespace {
+constexpr int MG_ROWB = 128;  // bytes of one row per k-step
+enum { MG_BF16 = 0, MG_F32 = 1, MG_SWIGLU = 2 };
+
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+
+__device__ __forceinline__ int mg_swz(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ float mg_silu(float g) { return g / (1.f + __expf(-g)); }
+
+template <int N>
+__device__ __forceinline__ void mg_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wait until at most `after` k-steps of LPS loads each are still in flight (after <= A)
+template <int LPS, int A>
+__device__ __forceinline__ void mg_wait_after(int after) {
+  if constexpr (A == 0) {
+    mg_vmcnt<0>();
+  } else {
+    if (after >= A) mg_vmcnt<A * LPS>();
+    else mg_wait_after<LPS, A - 1>(after);
+  }
+}
+__device__ __forceinline__ void mg_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+}  // namespace
+
+struct MgArgs {
+  void* out;
+  float* ws;             // partial slabs: [tiles][cmax][BM * BN] fp32 (fragment order)
+  unsigned* cnt;         // [tiles] arrival tickets, zero between launches
+  const uint8_t* x;      // [M][K] bf16 or e4m3
+  const uint8_t* W;      // [rows][K] bf16 or e4m3
+  const float* xs;       // fp8: [M] per-token activation scales
+  const float* wsc;      // fp8: [rows] per-row weight scales
+  long long kbytes;      // bytes per row of x / W
+  long long total;       // tiles * T work items (one item = one tile x one 128-byte k-step)
+  int M, N_out, half_rows;
+  int m_tiles, T;        // T: 128-byte k-steps over the whole K
+  int nwg, cmax;         // workgroups; most workgroups sharing one tile
+};
+
+template <int BM, int BN, int WM, int WN, int S, int EPI, bool FP8>
+__global__ void __launch_bounds__(64 * WM * WN) mgemm_kernel(MgArgs a) {
+  constexpr int NW = WM * WN;
+  constexpr int FM = BM / (WM * 16), FN = BN / (WN * 16);
+  static_assert(FM >= 1 && FN >= 1 && BM % (WM * 16) == 0 && BN % (WN * 16) == 0, "tile / wave split");
+  static_assert(EPI != MG_SWIGLU || FN % 2 == 0, "SwiGLU pairs gate and up fragments");
+  static_assert(S >= 2 && S <= 8, "ring depth");
+  constexpr int WREG = BN * MG_ROWB, STAGE_B = (BM + BN) * MG_ROWB;
+  static_assert((BN * 8) % NW == 0 && (BM * 8) % NW == 0, "chunks per wave");
+  constexpr int WCH = BN * 8 / NW, XCH = BM * 8 / NW;  // 16-byte chunks per wave per stage
+  constexpr int WI = (WCH + 63) / 64, XI = (XCH + 63) / 64, LPS = WI + XI;
+  static_assert((S - 2) * LPS <= 63, "vmcnt range");
+#if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the launch stub (its lambdas use device builtins)
+  __shared__ __attribute__((aligned(16))) char lds[S * STAGE_B + 16];
+  unsigned* flag = reinterpret_cast<unsigned*>(lds + S * STAGE_B);
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int li = lane & 15, g = lane >> 4;
+
+  // ---- block -> logical workgroup, XCD-aware and bijective for any grid size; logical workgroup
+  // w streams the work items [w * total / nwg, (w + 1) * total / nwg) (stream-K: every workgroup
+  // moves the same number of bytes, whatever the tile count)
+  const int bid = blockIdx.x, q8 = a.nwg >> 3, r8 = a.nwg & 7, xcd = bid & 7, loc = bid >> 3;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const long long it0 = (long long)lid * a.total / a.nwg, it1 = (long long)(lid + 1) * a.total / a.nwg;
+  const int T = a.T;
+
+  // ---- per-lane DMA geometry (swizzle on the source, lane-linear LDS destination)
+  int wr[WI], wc[WI], xr[XI], xc[XI];
+#pragma unroll
+  for (int i = 0; i < WI; ++i) {
+    const int p = wid * WCH + min(i * 64 + lane, WCH - 1);
+    wr[i] = p >> 3;
+    wc[i] = (p & 7) ^ mg_swz(p >> 3);
+  }
+#pragma unroll
+  for (int i = 0; i < XI; ++i) {
+    const int p = wid * XCH + min(i * 64 + lane, XCH - 1);
+    xr[i] = p >> 3;
+    xc[i] = (p & 7) ^ mg_swz(p >> 3);
+  }
+  // fragment rows of this lane inside the stage images
+  int arow[FN];
+#pragma unroll
+  for (int f = 0; f < FN; ++f) {
+    if (EPI == MG_SWIGLU) {
+      const int half = f / (FN / 2), ff = f % (FN / 2);
+      arow[f] = half * (BN / 2) + wn * (BN / 2 / WN) + ff * 16 + li;
+    } else {
+      arow[f] = wn * (BN / WN) + f * 16 + li;
+    }
+  }
+  const int brow0 = wm * (BM / WM) + li;
+
+  bool first_segment = true;
+  for (long long it = it0; it < it1;) {
+    const int tile = (int)(it / T);
+    const int kb = (int)(it - (long long)tile * T);
+    const int ke = (int)min((long long)T, kb + (it1 - it));
+    it += ke - kb;
+    const int mt = tile % a.m_tiles, nt = tile / a.m_tiles;
+    if (!first_segment) mg_barrier();  // every wave is done reading the ring before it is refilled
+    first_segment = false;
+
+    const uint8_t* wsrc[WI];
+    const uint8_t* xsrc[XI];
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+      const int r = wr[i];
+      int grow;
+      if (EPI == MG_SWIGLU) {
+        const int f = min(nt * (BN / 2) + (r % (BN / 2)), a.N_out - 1);
+        grow = r < BN / 2 ? f : a.half_rows + f;
+      } else {
+        grow = min(nt * BN + r, a.N_out - 1);
+      }
+      wsrc[i] = a.W + (long long)grow * a.kbytes + (long long)kb * MG_ROWB + wc[i] * 16;
+    }
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int grow = min(mt * BM + xr[i], a.M - 1);
+      xsrc[i] = a.x + (long long)grow * a.kbytes + (long long)kb * MG_ROWB + xc[i] * 16;
+    }
+
+    auto issue = [&](int t, int stage) {
+      char* sb = lds + stage * STAGE_B;
+      const long long off = (long long)t * MG_ROWB;
+#pragma unroll
+      for (int i = 0; i < WI; ++i) {
+        if (WCH % 64 == 0 || i * 64 + lane < WCH)
+          __builtin_amdgcn_global_load_lds(wsrc[i] + off,
+                                           (__attribute__((address_space(3))) void*)(sb + (wid * WCH + i * 64) * 16),
+                                           16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < XI; ++i) {
+        if (XCH % 64 == 0 || i * 64 + lane < XCH)
+          __builtin_amdgcn_global_load_lds(
+              xsrc[i] + off, (__attribute__((address_space(3))) void*)(sb + WREG + (wid * XCH + i * 64) * 16), 16, 0,
+              0);
+      }
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int f = 0; f < FN; ++f)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int stage) {
+      const char* wb = lds + stage * STAGE_B;
+      const char* xb = wb + WREG;
+      if constexpr (!FP8) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {  // two k32 steps per 64-wide k-step
+          const int c = kk * 4 + g;
+          bf16x8 af[FN], bfr[FM];
+#pragma unroll
+          for (int f = 0; f < FN; ++f)
+            af[f] = *reinterpret_cast<const bf16x8*>(wb + arow[f] * MG_ROWB + ((c ^ mg_swz(arow[f])) << 4));
+#pragma unroll
+          for (int j = 0; j < FM; ++j) {
+            const int r = brow0 + j * 16;
+            bfr[j] = *reinterpret_cast<const bf16x8*>(xb + r * MG_ROWB + ((c ^ mg_swz(r)) << 4));
+          }
+#pragma unroll
+          for (int f = 0; f < FN; ++f)
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+              acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], bfr[j], acc[f][j], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {  // four k32 steps per 128-wide k-step; lane reads 8 bytes
+          const int c = kk * 2 + (g >> 1), hb = (g & 1) * 8;
+          long af[FN], bfr[FM];
+#pragma unroll
+          for (int f = 0; f < FN; ++f)
+            af[f] = *reinterpret_cast<const long*>(wb + arow[f] * MG_ROWB + ((c ^ mg_swz(arow[f])) << 4) + hb);
+#pragma unroll
+          for (int j = 0; j < FM; ++j) {
+            const int r = brow0 + j * 16;
+            bfr[j] = *reinterpret_cast<const long*>(xb + r * MG_ROWB + ((c ^ mg_swz(r)) << 4) + hb);
+          }
+#pragma unroll
+          for (int f = 0; f < FN; ++f)
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+              acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[f], bfr[j], acc[f][j], 0, 0, 0);
+        }
+      }
+    };
+
+    // ---- K loop over this segment: S-1 k-steps issued ahead; wait for the oldest, barrier,
+    // refill the buffer everyone finished with, compute
+    const int n = ke - kb;
+#pragma unroll
+    for (int t = 0; t < S - 1; ++t)
+      if (t < n) issue(t, t);
+    int stage = 0, fill = S - 1;
+    for (int t = 0; t < n; ++t) {
+      // k-steps issued after step t that may stay in flight
+      mg_wait_after<LPS, S - 2>(min(S - 2, n - 1 - t));
+      mg_barrier();  // step t landed for every wave; every wave finished reading the buffer refilled now
+      if (t + S - 1 < n) issue(t + S - 1, fill);
+      compute(stage);
+      stage = stage + 1 == S ? 0 : stage + 1;
+      fill = fill + 1 == S ? 0 : fill + 1;
+    }
+
+    // ---- a tile shared by several workgroups: publish this partial tile; the last arriver reduces
+    const long long i_first = (long long)tile * T;
+    const int w_first = (int)(((i_first + 1) * a.nwg - 1) / a.total);
+    const int w_last = (int)(((i_first + T) * a.nwg - 1) / a.total);
+    const int nc = w_last - w_first + 1;
+    if (nc > 1) {
+      float* base = a.ws + (long long)tile * a.cmax * (BM * BN);
+      float* slab = base + (long long)(lid - w_first) * (BM * BN);
+#pragma unroll
+      for (int f = 0; f < FN; ++f)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          *reinterpret_cast<f32x4*>(slab + (((wid * FN + f) * FM + j) * 64 + lane) * 4) = acc[f][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned last = old == (unsigned)(nc - 1);
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          a.cnt[tile] = 0u;  // ready for the next launch
+        }
+        *flag = last;
+      }
+      __syncthreads();
+      if (*flag == 0u) continue;
+      // fixed summation order over ALL slabs (own included): the result does not depend on which
+      // workgroup arrived last
+#pragma unroll
+      for (int f = 0; f < FN; ++f)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s2 = 0; s2 < nc; ++s2) {
+        const float* sl = base + (long long)s2 * (BM * BN);
+#pragma unroll
+        for (int f = 0; f < FN; ++f)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(sl + (((wid * FN + f) * FM + j) * 64 + lane) * 4);
+            acc[f][j] += v;
+          }
+      }
+    }
+
+    // ---- epilogue: lane holds out[m = brow][n = 4 g + i], i < 4, of every fragment pair
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int m = mt * BM + wm * (BM / WM) + j * 16 + li;
+      if (m >= a.M) continue;
+      const float sx = FP8 ? a.xs[m] : 1.f;
+      if constexpr (EPI == MG_SWIGLU) {
+#pragma unroll
+        for (int f = 0; f < FN / 2; ++f) {
+          const int n0 = nt * (BN / 2) + wn * (BN / 2 / WN) + f * 16 + 4 * g;
+          if (n0 >= a.N_out) continue;
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float gt = acc[f][j][i] * sx, up = acc[f + FN / 2][j][i] * sx;
+            if (FP8) { gt *= a.wsc[n0 + i]; up *= a.wsc[a.half_rows + n0 + i]; }
+            v[i] = mg_silu(gt) * up;
+          }
+          u32x2 o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+          *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.out) + (long long)m * a.N_out + n0) = o;
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < FN; ++f) {
+          const int n0 = nt * BN + wn * (BN / WN) + f * 16 + 4 * g;
+          if (n0 >= a.N_out) continue;
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = acc[f][j][i] * sx * (FP8 ? a.wsc[n0 + i] : 1.f);
+          if constexpr (EPI == MG_F32) {
+            *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + (long long)m * a.N_out + n0) =
+                f32x4{v[0], v[1], v[2], v[3]};
+          } else {
+            u32x2 o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+            *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.out) + (long long)m * a.N_out + n0) = o;
+          }
+        }
+      }
+    }
+  }
+#endif
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+namespace {
+
+// Tile configurations (BM x BN, waves WM x WN, ring depth S).  Index = config id of the host API.
+struct MgCfg {
+  int bm, bn, wm, wn, s;
+};
+constexpr MgCfg kMgCfgs[] = {
+    {16, 128, 1, 4, 4},   //  0  batched decode, M <= 16
+    {16, 128, 1, 4, 3},   //  1  same, smaller ring (3 workgroups / CU)
+    {32, 128, 1, 4, 3},   //  2  M <= 32
+    {32, 256, 1, 4, 3},   //  3  M <= 32, wide weight tile
+    {64, 128, 1, 4, 3},   //  4  M <= 64
+    {64, 256, 1, 4, 3},   //  5  M <= 64, wide weight tile
+    {64, 64, 2, 2, 4},    //  6  M <= 64, narrow (more tiles)
+    {128, 128, 2, 2, 3},  //  7  M <= 128
+    {128, 64, 2, 2, 4},   //  8  prefill, small N
+    {256, 128, 2, 2, 3},  //  9  prefill
+    {256, 64, 4, 1, 3},   // 10  prefill, small N
+    {128, 256, 2, 4, 3},  // 11  prefill, 8 waves
+    {256, 256, 2, 4, 2},  // 12  prefill, 8 waves, 256 x 256
+    {16, 64, 1, 4, 4},    // 13  decode, narrow (small-N shapes; no SwiGLU)
+    {32, 64, 1, 4, 4},    // 14  decode, narrow (no SwiGLU)
+    {64, 128, 2, 4, 3},   // 15  M <= 64, 8 waves
+    {128, 128, 2, 4, 3},  // 16  M <= 128, 8 waves
+    // deep rings for weight streaming (M <= 64): 5-7 k-steps in flight per workgroup
+    {16, 64, 1, 4, 8},    // 17  (no SwiGLU)
+    {16, 128, 1, 4, 6},   // 18
+    {32, 64, 1, 4, 8},    // 19  (no SwiGLU)
+    {32, 128, 1, 4, 6},   // 20
+    {64, 128, 1, 4, 5},   // 21
+    {64, 64, 2, 2, 7},    // 22
+    {16, 256, 1, 4, 4},   // 23  wide
+};
+constexpr int kMgNumCfgs = sizeof(kMgCfgs) / sizeof(kMgCfgs[0]);
+
+template <int C, int EPI, bool FP8>
+int mg_launch(const MgArgs& a, int grid, hipStream_t s) {
+  constexpr bool ok = EPI != MG_SWIGLU || (kMgCfgs[C].bn / (kMgCfgs[C].wn * 16)) % 2 == 0;
+  if constexpr (!ok) {
+    return -2;
+  } else {
+    hipLaunchKernelGGL(
+        (mgemm_kernel<kMgCfgs[C].bm, kMgCfgs[C].bn, kMgCfgs[C].wm, kMgCfgs[C].wn, kMgCfgs[C].s, EPI, FP8>),
+        dim3(grid), dim3(64 * kMgCfgs[C].wm * kMgCfgs[C].wn), 0, s, a);
+    return (int)hipGetLastError();
+  }
+}
+
+template <int C, bool FP8>
+int mg_epi(const MgArgs& a, int grid, int epi, hipStream_t s) {
+  switch (epi) {
+    case MG_BF16: return mg_launch<C, MG_BF16, FP8>(a, grid, s);
+    case MG_F32: return mg_launch<C, MG_F32, FP8>(a, grid, s);
+    case MG_SWIGLU: return mg_launch<C, MG_SWIGLU, FP8>(a, grid, s);
+  }
+  return -2;
+}
+
+template <bool FP8, int C = 0>
+int mg_cfg(const MgArgs& a, int grid, int cfg, int epi, hipStream_t s) {
+  if constexpr (C < kMgNumCfgs) {
+    if (cfg == C) return mg_epi<C, FP8>(a, grid, epi, s);
+    return mg_cfg<FP8, C + 1>(a, grid, cfg, epi, s);
+  } else {
+    return -4;
+  }
+}
+
+}  // namespace
+
+extern "C" int k8s_mgemm_num_configs() { return kMgNumCfgs; }
+
+// (bm, bn) of a config: the Python planner sizes grids from them.
+extern "C" int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* lds_bytes, int* swiglu) {
+  if (cfg < 0 || cfg >= kMgNumCfgs) return -1;
+  const MgCfg c = kMgCfgs[cfg];
+  *bm = c.bm;
+  *bn = c.bn;
+  *threads = 64 * c.wm * c.wn;
+  *lds_bytes = c.s * (c.bm + c.bn) * MG_ROWB + 16;
+  *swiglu = (c.bn / (c.wn * 16)) % 2 == 0;
+  return 0;
+}
+
+namespace {
+struct MgGeom {
+  long long tiles, T, total;
+};
+MgGeom mg_geom(int M, int N_out, int K, int epi, int fp8, int cfg) {
+  const MgCfg c = kMgCfgs[cfg];
+  const int feat = epi == MG_SWIGLU ? c.bn / 2 : c.bn;
+  MgGeom g;
+  g.tiles = (long long)((N_out + feat - 1) / feat) * ((M + c.bm - 1) / c.bm);
+  g.T = (long long)K * (fp8 ? 1 : 2) / MG_ROWB;
+  g.total = g.tiles * g.T;
+  return g;
+}
+}  // namespace
+
+// Plan facts for a launch of `nwg` workgroups: the tile count, the most workgroups sharing one tile
+// (cmax), the fp32 slab workspace (elements) and the ticket count.  Returns -1 for bad arguments.
+extern "C" int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, long long* tiles,
+                                   int* cmax, long long* ws_elems) {
+  if (cfg < 0 || cfg >= kMgNumCfgs || M <= 0 || N_out <= 0 || K <= 0 || nwg <= 0) return -1;
+  const MgGeom g = mg_geom(M, N_out, K, epi, fp8, cfg);
+  if (g.T <= 0 || nwg > g.total) return -1;
+  int cm = 1;
+  for (long long t = 0; t < g.tiles; ++t) {
+    const long long f = ((t * g.T + 1) * nwg - 1) / g.total, l = (((t + 1) * g.T) * nwg - 1) / g.total;
+    if (l - f + 1 > cm) cm = (int)(l - f + 1);
+  }
+  *tiles = g.tiles;
+  *cmax = cm;
+  *ws_elems = cm > 1 ? g.tiles * cm * kMgCfgs[cfg].bm * kMgCfgs[cfg].bn : 0;
+  return 0;
+}
+
+// out[M, N_out] = epi(x[M, K] . W^T) with `nwg` workgroups streaming equal shares of the
+// (tile, k-step) items.  fp8: x / W are e4m3 bytes with per-row scales xs / wsc.
+// SwiGLU: W holds 2 * N_out rows ([gate; up]); out has N_out columns.
+extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs,
+                         const float* wsc, int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax,
+                         hipStream_t stream) {
+  if (cfg < 0 || cfg >= kMgNumCfgs || M <= 0 || N_out <= 0 || K <= 0 || nwg <= 0 || cmax < 1) return -1;
+  if (N_out % 4 != 0) return -1;
+  const long long kbytes = (long long)K * (fp8 ? 1 : 2);
+  if (kbytes % MG_ROWB != 0) return -1;
+  const MgGeom g = mg_geom(M, N_out, K, epi, fp8, cfg);
+  if (nwg > g.total) return -1;
+  if (cmax > 1 && (ws == nullptr || tickets == nullptr)) return -3;
+  if (fp8 && (xs == nullptr || wsc == nullptr)) return -3;
+  MgArgs a;
+  a.out = out;
+  a.ws = ws;
+  a.cnt = tickets;
+  a.x = static_cast<const uint8_t*>(x);
+  a.W = static_cast<const uint8_t*>(W);
+  a.xs = xs;
+  a.wsc = wsc;
+  a.kbytes = kbytes;
+  a.total = g.total;
+  a.M = M;
+  a.N_out = N_out;
+  a.half_rows = epi == MG_SWIGLU ? N_out : 0;
+  a.m_tiles = (M + kMgCfgs[cfg].bm - 1) / kMgCfgs[cfg].bm;
+  a.T = (int)g.T;
+  a.nwg = nwg;
+  a.cmax = cmax;
+  return fp8 ? mg_cfg<true>(a, nwg, cfg, epi, stream) : mg_cfg<false>(a, nwg, cfg, epi, stream);
+}

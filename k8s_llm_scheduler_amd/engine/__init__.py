@@ -46,6 +46,23 @@ def _load_gemm_table() -> bool:
     return ok
 
 
+def resolve_tokenizer(weights: Optional[str], tokenizer: Optional[str]) -> Optional[str]:
+    """The tokenizer a checkpoint must be served with: an explicit ``engine.tokenizer``, else the
+    checkpoint's own ``tokenizer.json``.  Real weights fed the built-in synthetic vocabulary would
+    answer garbage on every request (all decisions silently falling back), so a checkpoint without a
+    tokenizer is an error; only random-init engines (no weights) use the synthetic tokenizer."""
+    if tokenizer:
+        return tokenizer
+    if not weights:
+        return None
+    cand = Path(weights) / "tokenizer.json" if Path(weights).is_dir() else Path(weights).with_name("tokenizer.json")
+    if cand.is_file():
+        return str(cand)
+    raise FileNotFoundError(f"engine.weights={weights} has no tokenizer.json next to it; set engine.tokenizer "
+                            "to the checkpoint's tokenizer (the built-in synthetic vocabulary only fits "
+                            "random-init weights)")
+
+
 def warm_library_gemms(model) -> None:
     """Run every library GEMM shape the engine can issue (layer 0's projections at each row bucket of
     ops.GEMM_M_BUCKETS) once, so hipBLASLt / rocBLAS load their kernels now instead of inside the first
@@ -91,7 +108,7 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
         torch.cuda.synchronize()
     log.info(f" Model {cfg.name} ready on {device} (tp {tp.rank}/{tp.world}, "
              f"{model.weight_bytes() / 1e9:.1f} GB weights, {time.perf_counter() - t0:.1f}s)")
-    tok = Tokenizer(tokenizer, model_vocab=cfg.vocab)
+    tok = Tokenizer(resolve_tokenizer(weights, tokenizer), model_vocab=cfg.vocab)
     eng = LLMEngine(model, tok, max_batch=max_batch, block_size=block_size, num_blocks=num_blocks,
                     kv_cache_gb=kv_cache_gb, kv_cache_fraction=kv_cache_fraction, max_model_len=max_model_len,
                     max_prefill_tokens=max_prefill_tokens, cuda_graphs=cuda_graphs, prefix_caching=prefix_caching,

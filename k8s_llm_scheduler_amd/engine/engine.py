@@ -73,6 +73,8 @@ class Request:
     first_token_time: Optional[float] = None
     finish_time: Optional[float] = None
     aborted: bool = False
+    done: Optional[threading.Event] = None      # set by _finish (background serving loop)
+    error: Optional[BaseException] = None       # engine failure that ended the request
 
 
 @dataclass
@@ -146,6 +148,14 @@ class LLMEngine:
         self.prefill_graphs: Dict[int, tuple] = {}             # token bucket -> (graph, logits)
         self._graph_pool = None
         self.lock = threading.RLock()
+        # background serving loop (start_background): callers of generate() only touch the inbox and
+        # wait on their requests' events, so a submitter never waits for a whole engine step
+        self._inbox: List[Request] = []
+        self._inbox_lock = threading.Lock()
+        self._wake = threading.Condition(self._inbox_lock)
+        self._bg_thread: Optional[threading.Thread] = None
+        self._bg_stop = False
+        self._bg_error: Optional[BaseException] = None
         self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "graph_replays": 0, "prefill_graph_replays": 0, "prefill_time": 0.0, "decode_time": 0.0}
 
@@ -285,13 +295,28 @@ class LLMEngine:
         if max_new != params.max_tokens:
             params = SamplingParams(**{**params.__dict__, "max_tokens": max_new})
         seed = params.seed if params.seed is not None else self._rng.getrandbits(31)
+        if self._bg_thread is not None:
+            r = Request(next(self._ids), ids, params, seed, done=threading.Event())
+            with self._wake:
+                self._inbox.append(r)
+                self._wake.notify()
+            return r
         with self.lock:
             r = Request(next(self._ids), ids, params, seed)
-            self.requests[r.rid] = r
-            self.waiting.append(r)
-            if self.control is not None:
-                self._outbox.append(r)
+            self._enqueue(r)
         return r
+
+    def _enqueue(self, r: Request) -> None:
+        self.requests[r.rid] = r
+        self.waiting.append(r)
+        if self.control is not None:
+            self._outbox.append(r)
+
+    def _drain_inbox(self) -> None:
+        with self._inbox_lock:
+            new, self._inbox = self._inbox, []
+        for r in new:
+            self._enqueue(r)
 
     def _sync(self) -> bool:
         """Replicate rank 0's new requests and aborts to every rank.  Returns False on a stop
@@ -331,6 +356,10 @@ class LLMEngine:
 
     def abort(self, rid: int) -> None:
         """Mark a request aborted; it is removed at the start of the next step (on every rank)."""
+        with self._inbox_lock:
+            for r in self._inbox:
+                if r.rid == rid:
+                    r.aborted = True
         with self.lock:
             r = self.requests.get(rid)
             if r is not None and not r.finished:
@@ -527,6 +556,8 @@ class LLMEngine:
         r.finished = True
         r.finish_reason = reason
         r.finish_time = time.perf_counter()
+        if r.done is not None:
+            r.done.set()
         if r.slot >= 0:
             self.s_ctx[r.slot] = 0
             self.s_steps[r.slot] = 0
@@ -542,6 +573,7 @@ class LLMEngine:
 
     def step(self) -> List[Request]:
         with self.lock:
+            self._drain_inbox()
             if not self._sync():
                 raise StopIteration("engine stopped by rank 0")
             self._reap_aborted()
@@ -569,6 +601,55 @@ class LLMEngine:
     def kv_utilization(self) -> float:
         return 1.0 - self.allocator.num_free / self.allocator.num_blocks
 
+    # ------------------------------------------------------------------ background serving loop
+    def start_background(self) -> None:
+        """Run engine steps on a dedicated thread.  generate() then only enqueues and waits, so requests
+        from any number of caller threads (the scheduler's continuous mode) join the running batch at the
+        next step instead of waiting for each other's calls to finish."""
+        if self._bg_thread is not None:
+            return
+        self._bg_stop = False
+        self._bg_error = None
+        self._bg_thread = threading.Thread(target=self._bg_loop, name="engine-loop", daemon=True)
+        self._bg_thread.start()
+
+    def stop_background(self) -> None:
+        t = self._bg_thread
+        if t is None:
+            return
+        with self._wake:
+            self._bg_stop = True
+            self._wake.notify_all()
+        t.join()
+        self._bg_thread = None
+
+    @property
+    def background(self) -> bool:
+        return self._bg_thread is not None
+
+    def _bg_loop(self) -> None:
+        if self.gpu:
+            torch.cuda.set_device(self.device)
+        while True:
+            with self._wake:
+                while not self._bg_stop and not self._inbox and not self.has_work():
+                    self._wake.wait(0.05)
+                if self._bg_stop:
+                    return
+            try:
+                self.step()
+            except Exception as e:  # noqa: BLE001 -- every pending request fails, the loop keeps serving
+                log.error(f"Engine step failed: {e!r}")
+                self._bg_error = e
+                with self.lock:
+                    self._drain_inbox()
+                    for r in list(self.requests.values()):
+                        if not r.finished:
+                            r.error = e
+                            if r in self.waiting:
+                                self.waiting.remove(r)
+                            self._finish(r, "error")
+
     # ------------------------------------------------------------------ blocking API
     def output(self, r: Request) -> Output:
         end = r.finish_time or time.perf_counter()
@@ -583,6 +664,8 @@ class LLMEngine:
         TimeoutError -- the decision service counts that as an engine failure."""
         if params is None or isinstance(params, SamplingParams):
             params = [params or SamplingParams()] * len(prompts)
+        if self._bg_thread is not None:
+            return self._generate_bg(prompts, params, deadline)
         with self.lock:
             reqs = [self.add_request(p, sp) for p, sp in zip(prompts, params)]
             while not all(r.finished for r in reqs):
@@ -600,6 +683,25 @@ class LLMEngine:
             for r in reqs:
                 self.requests.pop(r.rid, None)
             return outs
+
+    def _generate_bg(self, prompts, params, deadline: Optional[float]) -> List[Output]:
+        reqs = [self.add_request(p, sp) for p, sp in zip(prompts, params)]
+        try:
+            for r in reqs:
+                left = None if deadline is None else max(0.0, deadline - time.monotonic())
+                if not r.done.wait(timeout=left):
+                    for q in reqs:
+                        self.abort(q.rid)
+                    raise TimeoutError("decision engine deadline exceeded")
+            failed = next((r.error for r in reqs if r.error is not None), None)
+            if failed is not None:
+                raise RuntimeError(f"decision engine failure: {failed}") from failed
+            return [self.output(r) for r in reqs]
+        finally:
+            with self.lock:
+                for r in reqs:
+                    if r.finished:
+                        self.requests.pop(r.rid, None)
 
 
 class _PyBlockAllocator:

@@ -73,6 +73,7 @@ class FakeKubeAPI:
         self.duplicate_events = duplicate_events
         self.run_bound_pods = run_bound_pods     # bound pods transition to Running (kubelet stand-in)
         self.bindings: List[Tuple[str, str]] = []  # (ns/name, node)
+        self._history: List[Tuple[int, WatchEvent]] = []   # (resourceVersion, event): watch-from-rv replay
         self.calls: Dict[str, int] = {}
         for n in nodes or []:
             self.add_node(n)
@@ -133,6 +134,9 @@ class FakeKubeAPI:
 
     def _emit(self, typ: str, obj: Obj) -> None:
         ev = (typ, copy.deepcopy(obj))
+        self._history.append((int(obj.get("metadata", {}).get("resourceVersion", "0") or 0), ev))
+        if len(self._history) > 100000:
+            del self._history[:50000]
         for q in list(self._watchers):
             q.put(ev)
             if self.duplicate_events:
@@ -164,6 +168,12 @@ class FakeKubeAPI:
                 # Like a fresh LIST+WATCH: synthetic ADDED for every existing pod.
                 for p in self._pods.values():
                     q.put(("ADDED", copy.deepcopy(p)))
+            else:
+                # Watch from a LIST's resourceVersion: replay every later change, as the apiserver does.
+                rv = int(resource_version)
+                for erv, (typ, obj) in self._history:
+                    if erv > rv:
+                        q.put((typ, copy.deepcopy(obj)))
             self._watchers.append(q)
         deadline = time.monotonic() + timeout_seconds
         try:

@@ -8,6 +8,7 @@ tensor-parallel tests) and is the numerics oracle of the kernel tests.
 
 from __future__ import annotations
 
+import functools
 import importlib
 import math
 import os
@@ -323,6 +324,123 @@ def _lib_linear(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     Mp = next(b for b in GEMM_M_BUCKETS if b >= M)
     xp = torch.nn.functional.pad(x2, (0, 0, 0, Mp - M))
     return torch.nn.functional.linear(xp, w)[:M]
+
+
+# ----------------------------------------------------------------------------- MFMA GEMM (M > 8)
+# A plan is (cfg, grid): cfg indexes mgemm.hip's tile configurations; grid > 0 launches grid workgroups
+# per output tile (split-K), grid < 0 launches min(-grid, work items) workgroups that stream equal shares
+# of the (tile, k-step) items (stream-K: balanced whatever the tile count).
+_MG_CFGS: Optional[list] = None
+MG_GRIDS = (1, 2, 4, 8, 16, -256, -512, -768, -1024)
+
+
+def mgemm_configs() -> list:
+    """(BM, BN, threads, LDS bytes, SwiGLU-capable) of every compiled mgemm.hip tile configuration."""
+    global _MG_CFGS
+    if _MG_CFGS is None:
+        _MG_CFGS = [tuple(c) for c in native().mgemm_configs()]
+    return _MG_CFGS
+
+
+def _mg_occupancy(cfg: int) -> int:
+    """Workgroups of a configuration resident per CU (LDS and the 32-wave limit)."""
+    _, _, threads, lds, _ = mgemm_configs()[cfg]
+    return max(1, min(160 * 1024 // lds, 2048 // threads))
+
+
+def _mg_tiles(cfg: int, M: int, N: int, epi: int) -> int:
+    bm, bn = mgemm_configs()[cfg][:2]
+    feat = bn // 2 if epi == EPI_SWIGLU else bn
+    return math.ceil(N / feat) * math.ceil(M / bm)
+
+
+def mgemm_nwg(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int) -> int:
+    total = _mg_tiles(cfg, M, N, epi) * (K * (1 if fp8 else 2) // 128)
+    nwg = _mg_tiles(cfg, M, N, epi) * grid if grid > 0 else -grid
+    return max(1, min(nwg, total))
+
+
+def mgemm_valid(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int = 1) -> bool:
+    if cfg < 0 or cfg >= len(mgemm_configs()):
+        return False
+    kb = K * (1 if fp8 else 2)
+    if kb % 128 or N % 4 or M <= 0:
+        return False
+    if epi == EPI_SWIGLU and not mgemm_configs()[cfg][4]:
+        return False
+    return grid != 0
+
+
+@functools.lru_cache(maxsize=4096)
+def _mg_plan_info(M: int, N: int, K: int, epi: int, fp8: bool, cfg: int, nwg: int) -> Tuple[int, int, int]:
+    return tuple(native().mgemm_plan_info(M, N, K, epi, int(fp8), cfg, nwg))
+
+
+def mgemm_heuristic(M: int, N: int, K: int, epi: int, fp8: bool, num_cus: int = 256) -> Tuple[int, int]:
+    """Tile + grid choice when the tuned table has no entry for the shape."""
+    if M <= 128:   # weight streaming: every CU busy, equal shares
+        cfg = 0 if M <= 16 else 2 if M <= 32 else 4 if M <= 64 else 7
+        return cfg, -num_cus * _mg_occupancy(cfg)
+    cfg = 9
+    tiles = _mg_tiles(cfg, M, N, epi)
+    return cfg, (1 if tiles >= num_cus else max(1, min(16, num_cus // tiles)))
+
+
+# Tuned plans per shape: engine/assets/mgemm_gfx950.json, written by tools/mgemm_tune.py.
+# Keys "M_bucket,N,K,epi,fp8" with M_bucket the smallest of GEMM_M_BUCKETS >= M (else the next power of 2).
+_MG_TABLE: Optional[dict] = None
+MG_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "assets",
+                             "mgemm_gfx950.json")
+
+
+def _mg_bucket(M: int) -> int:
+    for b in GEMM_M_BUCKETS:
+        if b >= M:
+            return b
+    return 1 << max(0, (M - 1).bit_length())
+
+
+def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
+    global _MG_TABLE
+    if _MG_TABLE is None:
+        _MG_TABLE = {}
+        if os.environ.get("K8S_MGEMM_TABLE", "1") != "0" and os.path.isfile(MG_TABLE_PATH):
+            import json
+
+            with open(MG_TABLE_PATH) as f:
+                _MG_TABLE = {k: tuple(v) for k, v in json.load(f).get("plans", {}).items()}
+    hit = _MG_TABLE.get(f"{_mg_bucket(M)},{N},{K},{epi},{int(fp8)}")
+    if hit is not None and mgemm_valid(hit[0], M, N, K, epi, fp8, hit[1]):
+        return int(hit[0]), int(hit[1])
+    return mgemm_heuristic(M, N, K, epi, fp8)
+
+
+def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
+          grid: Optional[int] = None) -> torch.Tensor:
+    """Hand-written MFMA GEMM (mgemm.hip): epi(x[M, K] @ w[N, K].T) for M > 8 rows.  ``w``: bf16 or
+    Fp8Weight (activations are then quantized per token by quantize_act_fp8).  SwiGLU: w = [Wg; Wu]."""
+    M, K = x.shape
+    fp8 = _is_fp8(w)
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    if cfg is None:
+        cfg, grid = mgemm_plan(M, N, K, epi, fp8)
+    grid = grid or 1
+    if not mgemm_valid(cfg, M, N, K, epi, fp8, grid):
+        raise ValueError(f"mgemm: cfg {cfg} / grid {grid} invalid for M={M} N={N} K={K} epi={epi}")
+    nwg = mgemm_nwg(cfg, M, N, K, epi, fp8, grid)
+    tiles, cmax, n_ws = _mg_plan_info(M, N, K, epi, fp8, cfg, nwg)
+    out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
+    ws = torch.empty(n_ws, dtype=F32, device=x.device) if n_ws > 0 else None
+    tk = _zeroed_scratch(x.device, "mgemm", 4 * tiles, 64 * 1024) if cmax > 1 else 0
+    if fp8:
+        xq, sx = quantize_act_fp8(x.contiguous())
+        native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, xq.data_ptr(), w.q.data_ptr(),
+                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, nwg, cmax, -1)
+    else:
+        native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"),
+                       _chk(w, BF16, "w"), 0, 0, M, N, K, epi, 0, cfg, nwg, cmax, -1)
+    del ws
+    return out
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:

@@ -158,7 +158,7 @@ def ai_test_pods(api):
     return created
 
 
-@pytest.mark.parametrize("mode", ["sequential", "batched"])
+@pytest.mark.parametrize("mode", ["sequential", "batched", "continuous"])
 def test_e2e_ai_test_pods_all_bound_llm_path(mode):
     api = cluster(run_bound_pods=True)
     pods = ai_test_pods(api)
@@ -227,7 +227,7 @@ def test_fault_injection_hook_drives_retries_breaker_and_fallback():
     assert svc.decide("VALID NODE NAMES: kind-worker\n", pod, nodes).selected_node == "kind-worker"
 
 
-@pytest.mark.parametrize("mode", ["sequential", "batched"])
+@pytest.mark.parametrize("mode", ["sequential", "batched", "continuous"])
 def test_e2e_real_engine_forced_decode_llm_success_path(mode):
     """The whole pipeline through the real (tiny, CPU) engine: chat template -> tokenize ->
     prefill/decode -> detokenize -> JSON extraction -> validation -> bind.  Forced decode makes the
@@ -243,3 +243,45 @@ def test_e2e_real_engine_forced_decode_llm_success_path(mode):
     assert st["total_scheduled"] == 3 and st["llm_decisions"] == 3 and st["fallback_decisions"] == 0
     assert st["llm_client"]["successful_requests"] == 3
     assert eng.stats["decode_tokens"] > 0 and eng.stats["prefill_tokens"] > 0
+
+
+def test_continuous_mode_revalidates_concurrent_bindings():
+    """Continuous mode: decisions run concurrently against snapshots taken before each other's
+    bindings; the bind step re-checks the node (pod limit 1 here) and falls back per pod."""
+    api = FakeKubeAPI([make_node("small", pods="1"), make_node("big", pods="110")])
+    pods = [make_pod(f"c{i}") for i in range(4)]
+    sched = run_scheduler(api, ScriptedBackend(default='{"selected_node": "small"}'), pods, mode="continuous")
+    nodes = [api.get_pod("default", p["metadata"]["name"])["spec"]["nodeName"] for p in pods]
+    assert nodes.count("small") == 1 and nodes.count("big") == 3
+    st = sched.get_stats()
+    assert st["total_scheduled"] == 4 and st["llm_decisions"] == 1 and st["fallback_decisions"] == 3
+
+
+def test_informer_resync_drops_pods_deleted_while_no_stream_was_open():
+    """a pod deleted while the watch was down (no DELETED event ever seen) must leave the
+    informer counts at the next stream's LIST instead of inflating the node's usage for good."""
+    api = cluster()
+    api.create_pod(make_pod("ghost", node_name="kind-worker", phase="Running"))
+    svc, _ = service(None)
+    sched = CustomScheduler("ai-llama-scheduler", api, svc, watch_timeout=1, snapshot_mode="informer")
+
+    def count():
+        return {n.name: n.pod_count for n in sched.context_manager.get_node_metrics()}["kind-worker"]
+
+    async def main():
+        task = asyncio.create_task(sched.start())
+        t0 = time.time()
+        while count() != 1 and time.time() - t0 < 5:
+            await asyncio.sleep(0.02)
+        assert count() == 1
+        with api._lock:                  # deleted behind the watch's back: no DELETED event
+            api._pods.pop("default/ghost")
+        api.stop_watches()               # the stream ends; the next one starts with a LIST
+        t0 = time.time()
+        while count() != 0 and time.time() - t0 < 5:
+            await asyncio.sleep(0.02)
+        sched.stop()
+        await asyncio.wait_for(task, 5)
+
+    asyncio.run(main())
+    assert count() == 0

@@ -203,3 +203,67 @@ def test_in_batch_prefix_sharing(engine):
     engine.allocator.reset_prefix_cache()
     alone = [engine.generate([q], p)[0].token_ids for q in prompts[1:]]
     assert [o.token_ids for o in outs[1:]] == alone
+
+
+def test_background_loop_batches_concurrent_callers_and_matches_sync():
+    """start_background(): generate() from several threads joins one running batch; outputs equal the
+    synchronous engine's (sampling is deterministic per (seed, position))."""
+    import threading
+
+    prompts = [[5, 6, 7, 8 + i] * 6 for i in range(4)]
+    params = [SamplingParams(max_tokens=6, temperature=0.7, seed=11 + i, ignore_eos=True) for i in range(4)]
+    sync = build_engine("tiny", device="cpu", max_batch=4, max_model_len=256, num_blocks=128, seed=1)
+    want = [o.token_ids for o in sync.generate(prompts, params)]
+
+    eng = build_engine("tiny", device="cpu", max_batch=4, max_model_len=256, num_blocks=128, seed=1)
+    eng.start_background()
+    got = [None] * 4
+
+    def call(i):
+        got[i] = eng.generate([prompts[i]], [params[i]])[0].token_ids
+
+    ts = [threading.Thread(target=call, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    eng.stop_background()
+    assert got == want
+    assert not eng.requests and not eng.has_work()
+
+
+def test_background_loop_deadline_and_engine_failure_raise():
+    eng = build_engine("tiny", device="cpu", max_batch=2, max_model_len=256, num_blocks=128, seed=1)
+    eng.start_background()
+    try:
+        with pytest.raises(TimeoutError):
+            eng.generate([[1, 2, 3]], SamplingParams(max_tokens=200, ignore_eos=True), deadline=time.monotonic() + 0.01)
+        real = eng.model.forward_decode
+
+        def boom(*a, **k):
+            raise RuntimeError("xGMI peer timeout (injected)")
+
+        eng.model.forward_decode = boom
+        with pytest.raises(RuntimeError, match="xGMI peer timeout"):
+            eng.generate([[1, 2, 3]], SamplingParams(max_tokens=4, ignore_eos=True))
+        eng.model.forward_decode = real
+        out = eng.generate([[1, 2, 3]], SamplingParams(max_tokens=3, ignore_eos=True))   # still serving
+        assert len(out[0].token_ids) == 3
+    finally:
+        eng.stop_background()
+
+
+def test_checkpoint_without_tokenizer_is_rejected(tmp_path, tiny):
+    """real weights are never paired with the synthetic vocabulary by accident."""
+    import shutil
+
+    from k8s_llm_scheduler_amd.engine import resolve_tokenizer
+    from k8s_llm_scheduler_amd.engine.tokenizer import ASSET
+
+    save_hf_checkpoint(tiny, tmp_path / "ckpt")
+    with pytest.raises(FileNotFoundError, match="tokenizer"):
+        resolve_tokenizer(str(tmp_path / "ckpt"), None)
+    shutil.copy(ASSET, tmp_path / "ckpt" / "tokenizer.json")
+    assert resolve_tokenizer(str(tmp_path / "ckpt"), None) == str(tmp_path / "ckpt" / "tokenizer.json")
+    assert resolve_tokenizer(str(tmp_path / "ckpt"), "/x/tok.json") == "/x/tok.json"
+    assert resolve_tokenizer(None, None) is None
