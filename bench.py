@@ -61,6 +61,10 @@ def main() -> int:
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--simulate-tp", type=int, default=0,
                     help="PROFILING ONLY: run one TP rank's shapes on one GPU with collectives skipped")
+    ap.add_argument("--arrival-rate", type=float, default=0.0,
+                    help="serving mode: pods arrive as a Poisson process at this rate (pods/s) into the scheduler "
+                         "in continuous mode on an in-memory apiserver; reports detect->bind latency "
+                         "(--steps pods after --warmup pods; single rank)")
     args = ap.parse_args()
 
     import torch
@@ -78,8 +82,10 @@ def main() -> int:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-    tp = init_from_env("cuda", tp_size=args.tp)
+    on_gpu = torch.cuda.is_available()   # CPU: reference ops, for trying the harness without a GPU
+    if on_gpu:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    tp = init_from_env("cuda" if on_gpu else "cpu", tp_size=args.tp)
     if args.simulate_tp > 1:
         from k8s_llm_scheduler_amd.parallel import TPGroup
         tp = TPGroup(0, args.simulate_tp, None, "none", simulate=True)
@@ -96,7 +102,8 @@ def main() -> int:
                        weight_dtype=args.dtype)
     if eng.use_graphs:
         eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= max(1, args.batch)] or [1])
-    torch.cuda.synchronize()
+    if on_gpu:
+        torch.cuda.synchronize()
     init_s = time.perf_counter() - t_init
 
     backend = LocalEngineBackend(eng, ignore_eos=True)
@@ -120,13 +127,18 @@ def main() -> int:
         return items
 
     prompt_tokens = len(eng.render_chat(svc.system_message, make_items()[0][0]))
+    if args.arrival_rate > 0:
+        if world > 1 and not tp.simulate:
+            raise SystemExit("--arrival-rate is a single-rank serving benchmark")
+        return run_arrivals(args, eng, svc, prompt_tokens, init_s, tp)
 
     distributed = world > 1 and not tp.simulate
 
     def barrier():
         if distributed:
             dist.barrier()
-        torch.cuda.synchronize()
+        if on_gpu:
+            torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         svc.decide_many(make_items())
@@ -196,6 +208,82 @@ def main() -> int:
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
+
+
+def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
+    """Continuous-mode serving under Poisson arrivals: the reference's watch -> decide -> bind loop
+    (scheduler.py:662-729) with pods created at exponential inter-arrival times on an in-memory
+    apiserver (3-node kind cluster); latency = pod creation -> successful binding."""
+    import asyncio
+
+    from k8s_llm_scheduler_amd.control import CustomScheduler
+    from k8s_llm_scheduler_amd.kube import FakeKubeAPI, make_node, make_pod
+
+    logging.getLogger("k8s_llm_scheduler_amd").setLevel(logging.ERROR)   # one fallback warning per pod otherwise
+    api = FakeKubeAPI([make_node(n, cpu="4", memory="8Gi", pods="110") for n in
+                       ("kind-worker", "kind-worker2", "kind-worker3")])
+    sched = CustomScheduler("ai-llama-scheduler", api, svc, mode="continuous", max_batch=max(8, args.batch),
+                            watch_timeout=3600)
+    rng = random.Random(7)
+    n_total = args.warmup + args.steps
+    created = {}
+
+    async def main():
+        task = asyncio.create_task(sched.start())
+        await asyncio.sleep(0.1)
+        for i in range(n_total):
+            await asyncio.sleep(rng.expovariate(args.arrival_rate))
+            name = f"arrival-{i}"
+            created[f"default/{name}"] = time.perf_counter()
+            api.create_pod(make_pod(name, cpu=f"{rng.choice([100, 250, 500])}m",
+                                    memory=f"{rng.choice([128, 256, 512])}Mi"))
+        deadline = time.perf_counter() + 600
+        while len(api.binding_times) < n_total and time.perf_counter() < deadline:
+            await asyncio.sleep(0.01)
+        sched.stop()
+        await asyncio.wait_for(task, 30)
+
+    t0 = time.perf_counter()
+    asyncio.run(main())
+    eng.stop_background()
+    keys = [f"default/arrival-{i}" for i in range(args.warmup, n_total)]
+    lat = sorted(api.binding_times[k] - created[k] for k in keys if k in api.binding_times)
+    if not lat:
+        raise SystemExit("no pod was bound")
+    first = min(created[k] for k in keys)
+    span = max(api.binding_times[k] for k in keys if k in api.binding_times) - first
+    st = sched.get_stats()
+    res = {
+        "metric": "scheduling_decisions_per_sec",
+        "value": round(len(lat) / span, 4),
+        "unit": "decisions/s",
+        "n_gpus": tp.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * span / max(1, len(lat)), 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": round(len(lat) / span / BASELINE_DECISIONS_PER_S, 3),
+        "dtype": "bf16" if args.dtype == "bf16" else "fp8-e4m3 weights, bf16 activations",
+        "data": "synthetic Poisson pod arrivals on an in-memory apiserver, random-init weights",
+        "config": {"model": args.preset, "arrival_rate_pods_per_s": args.arrival_rate, "prompt_tokens": prompt_tokens,
+                   "gen_tokens": args.gen_tokens, "scheduler_mode": "continuous",
+                   "parallelism": f"tp{tp.world}" + ("-SIMULATED-no-comm" if tp.simulate else "")},
+        "p50_detect_to_bind_ms": round(1000 * statistics.median(lat), 2),
+        "p99_detect_to_bind_ms": round(1000 * lat[min(len(lat) - 1, int(0.99 * len(lat)))], 2),
+        "max_detect_to_bind_ms": round(1000 * lat[-1], 2),
+        "bound": len(lat),
+        "total_scheduled": st["total_scheduled"],
+        "fallback_decisions": st["fallback_decisions"],
+        "wall_s": round(time.perf_counter() - t0, 2),
+        "init_s": round(init_s, 1),
+    }
+    line = json.dumps(res)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(line + "\n")
     return 0
 
 

@@ -63,7 +63,7 @@ int k8s_silu_mul(void* out, const void* gu, int T, int I, hipStream_t s);
 int k8s_hash_init(void* out, int rows, int cols, long long gcols, long long row0, long long col0, uint32_t seed,
                   uint32_t tensor_id, float scale, float shift, hipStream_t s);
 int k8s_mgemm_num_configs();
-int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* lds_bytes, int* swiglu);
+int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* lds_bytes, int* swiglu, int* rb);
 int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, long long* tiles, int* cmax,
                         long long* ws_elems);
 int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs, const float* wsc,
@@ -195,9 +195,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("mgemm_configs", []() {
     py::list out;
     for (int c = 0; c < k8s_mgemm_num_configs(); ++c) {
-      int bm = 0, bn = 0, th = 0, lds = 0, sw = 0;
-      k8s_mgemm_config(c, &bm, &bn, &th, &lds, &sw);
-      out.append(py::make_tuple(bm, bn, th, lds, sw != 0));
+      int bm = 0, bn = 0, th = 0, lds = 0, sw = 0, rb = 0;
+      k8s_mgemm_config(c, &bm, &bn, &th, &lds, &sw, &rb);
+      out.append(py::make_tuple(bm, bn, th, lds, sw != 0, rb));
     }
     return out;
   });
@@ -233,6 +233,7 @@ PYBIND11_MODULE(_C, m) {
       .def("broadcast", [](RcclComm& c, uintptr_t buf, size_t count, int dtype, int root, int64_t s) {
         c.broadcast(P(buf), count, dtype, root, S(s));
       })
+      .def("async_error", &RcclComm::async_error)
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("rank", &RcclComm::rank);
 
@@ -256,6 +257,8 @@ PYBIND11_MODULE(_C, m) {
         c.all_gather(P(in), P(out), bytes, S(s));
       })
       .def("error", &XgmiComm::error)
+      .def("snapshot_error", [](XgmiComm& c, int64_t s) { c.snapshot_error(S(s)); }, py::arg("stream") = -1)
+      .def("last_error", &XgmiComm::last_error)
       .def("reset_error", &XgmiComm::reset_error)
       .def_property_readonly("world", &XgmiComm::world)
       .def_property_readonly("rank", &XgmiComm::rank)

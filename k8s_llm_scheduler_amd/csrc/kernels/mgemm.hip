@@ -29,12 +29,10 @@
 namespace k8sllm {
 
 namespace {
-constexpr int MG_ROWB = 128;  // bytes of one row per k-step
 enum { MG_BF16 = 0, MG_F32 = 1, MG_SWIGLU = 2 };
 
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 
-__device__ __forceinline__ int mg_swz(int r) { return (r >> 1) & 7; }
 __device__ __forceinline__ float mg_silu(float g) { return g / (1.f + __expf(-g)); }
 
 template <int N>
@@ -51,8 +49,11 @@ __device__ __forceinline__ void mg_wait_after(int after) {
     else mg_wait_after<LPS, A - 1>(after);
   }
 }
+// Raw barrier that leaves LDS-DMA (vmcnt) in flight.  The lgkmcnt(0) retires this wave's LDS reads
+// first: a buffer is refilled right after the barrier, and an LDS read still in flight at the barrier
+// (the compiler may sink its consuming MFMA past it) could otherwise return the new bytes (WAR).
 __device__ __forceinline__ void mg_barrier() {
-  asm volatile("" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
@@ -73,29 +74,43 @@ struct MgArgs {
   int nwg, cmax;         // workgroups; most workgroups sharing one tile
 };
 
-template <int BM, int BN, int WM, int WN, int S, int EPI, bool FP8>
-__global__ void __launch_bounds__(64 * WM * WN) mgemm_kernel(MgArgs a) {
-  constexpr int NW = WM * WN;
+// Wave layout: WM x WN waves own (BM / WM) x (BN / WN) output sub-tiles; WK waves share each
+// sub-tile and take every WK-th k32 step of a stage (intra-workgroup split-K, reduced through LDS
+// at the end of the segment).  RB: bytes of one row per k-step (128 / 256 / 512): wider k-steps
+// read longer contiguous runs of every weight row.
+template <int RB>
+__device__ __forceinline__ int mg_swz_rb(int r) {
+  return RB == 128 ? ((r >> 1) & 7) : (r & 15);
+}
+
+template <int BM, int BN, int WM, int WN, int WK, int RB, int S, int EPI, bool FP8>
+__global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
+  constexpr int NW = WM * WN * WK;
   constexpr int FM = BM / (WM * 16), FN = BN / (WN * 16);
   static_assert(FM >= 1 && FN >= 1 && BM % (WM * 16) == 0 && BN % (WN * 16) == 0, "tile / wave split");
   static_assert(EPI != MG_SWIGLU || FN % 2 == 0, "SwiGLU pairs gate and up fragments");
   static_assert(S >= 2 && S <= 8, "ring depth");
-  constexpr int WREG = BN * MG_ROWB, STAGE_B = (BM + BN) * MG_ROWB;
-  static_assert((BN * 8) % NW == 0 && (BM * 8) % NW == 0, "chunks per wave");
-  constexpr int WCH = BN * 8 / NW, XCH = BM * 8 / NW;  // 16-byte chunks per wave per stage
+  static_assert(RB == 128 || RB == 256 || RB == 512, "row bytes per k-step");
+  constexpr int CPR = RB / 16;                       // 16-byte chunks per staged row
+  constexpr int KS = FP8 ? RB / 32 : RB / 64;        // k32 MFMA steps per k-step
+  static_assert(KS % WK == 0, "k32 steps split evenly over WK waves");
+  constexpr int WREG = BN * RB, STAGE_B = (BM + BN) * RB;
+  static_assert((BN * CPR) % NW == 0 && (BM * CPR) % NW == 0, "chunks per wave");
+  constexpr int WCH = BN * CPR / NW, XCH = BM * CPR / NW;  // 16-byte chunks per wave per stage
   constexpr int WI = (WCH + 63) / 64, XI = (XCH + 63) / 64, LPS = WI + XI;
   static_assert((S - 2) * LPS <= 63, "vmcnt range");
+  static_assert(WK == 1 || (WK - 1) * FN * FM * 64 * 16 * WM * WN <= S * STAGE_B, "LDS reduction space");
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the launch stub (its lambdas use device builtins)
   __shared__ __attribute__((aligned(16))) char lds[S * STAGE_B + 16];
   unsigned* flag = reinterpret_cast<unsigned*>(lds + S * STAGE_B);
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid / WN, wn = wid % WN;
+  const int wk = wid % WK, wt = wid / WK;           // k-share, output sub-tile
+  const int wm = wt / WN, wn = wt % WN;
   const int li = lane & 15, g = lane >> 4;
 
   // ---- block -> logical workgroup, XCD-aware and bijective for any grid size; logical workgroup
-  // w streams the work items [w * total / nwg, (w + 1) * total / nwg) (stream-K: every workgroup
-  // moves the same number of bytes, whatever the tile count)
+  // w streams the work items [w * total / nwg, (w + 1) * total / nwg)
   const int bid = blockIdx.x, q8 = a.nwg >> 3, r8 = a.nwg & 7, xcd = bid & 7, loc = bid >> 3;
   const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
   const long long it0 = (long long)lid * a.total / a.nwg, it1 = (long long)(lid + 1) * a.total / a.nwg;
@@ -106,14 +121,14 @@ __global__ void __launch_bounds__(64 * WM * WN) mgemm_kernel(MgArgs a) {
 #pragma unroll
   for (int i = 0; i < WI; ++i) {
     const int p = wid * WCH + min(i * 64 + lane, WCH - 1);
-    wr[i] = p >> 3;
-    wc[i] = (p & 7) ^ mg_swz(p >> 3);
+    wr[i] = p / CPR;
+    wc[i] = (p % CPR) ^ mg_swz_rb<RB>(p / CPR);
   }
 #pragma unroll
   for (int i = 0; i < XI; ++i) {
     const int p = wid * XCH + min(i * 64 + lane, XCH - 1);
-    xr[i] = p >> 3;
-    xc[i] = (p & 7) ^ mg_swz(p >> 3);
+    xr[i] = p / CPR;
+    xc[i] = (p % CPR) ^ mg_swz_rb<RB>(p / CPR);
   }
   // fragment rows of this lane inside the stage images
   int arow[FN];
@@ -135,7 +150,7 @@ __global__ void __launch_bounds__(64 * WM * WN) mgemm_kernel(MgArgs a) {
     const int ke = (int)min((long long)T, kb + (it1 - it));
     it += ke - kb;
     const int mt = tile % a.m_tiles, nt = tile / a.m_tiles;
-    if (!first_segment) mg_barrier();  // every wave is done reading the ring before it is refilled
+    if (!first_segment) mg_barrier();  // every wave is done with the ring (and the reduction space)
     first_segment = false;
 
     const uint8_t* wsrc[WI];
@@ -150,17 +165,17 @@ __global__ void __launch_bounds__(64 * WM * WN) mgemm_kernel(MgArgs a) {
       } else {
         grow = min(nt * BN + r, a.N_out - 1);
       }
-      wsrc[i] = a.W + (long long)grow * a.kbytes + (long long)kb * MG_ROWB + wc[i] * 16;
+      wsrc[i] = a.W + (long long)grow * a.kbytes + (long long)kb * RB + wc[i] * 16;
     }
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int grow = min(mt * BM + xr[i], a.M - 1);
-      xsrc[i] = a.x + (long long)grow * a.kbytes + (long long)kb * MG_ROWB + xc[i] * 16;
+      xsrc[i] = a.x + (long long)grow * a.kbytes + (long long)kb * RB + xc[i] * 16;
     }
 
     auto issue = [&](int t, int stage) {
       char* sb = lds + stage * STAGE_B;
-      const long long off = (long long)t * MG_ROWB;
+      const long long off = (long long)t * RB;
 #pragma unroll
       for (int i = 0; i < WI; ++i) {
         if (WCH % 64 == 0 || i * 64 + lane < WCH)
@@ -186,37 +201,35 @@ __global__ void __launch_bounds__(64 * WM * WN) mgemm_kernel(MgArgs a) {
     auto compute = [&](int stage) {
       const char* wb = lds + stage * STAGE_B;
       const char* xb = wb + WREG;
-      if constexpr (!FP8) {
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {  // two k32 steps per 64-wide k-step
+      for (int q = 0; q < KS / WK; ++q) {
+        const int kk = q * WK + wk;
+        if constexpr (!FP8) {
           const int c = kk * 4 + g;
           bf16x8 af[FN], bfr[FM];
 #pragma unroll
           for (int f = 0; f < FN; ++f)
-            af[f] = *reinterpret_cast<const bf16x8*>(wb + arow[f] * MG_ROWB + ((c ^ mg_swz(arow[f])) << 4));
+            af[f] = *reinterpret_cast<const bf16x8*>(wb + arow[f] * RB + ((c ^ mg_swz_rb<RB>(arow[f])) << 4));
 #pragma unroll
           for (int j = 0; j < FM; ++j) {
             const int r = brow0 + j * 16;
-            bfr[j] = *reinterpret_cast<const bf16x8*>(xb + r * MG_ROWB + ((c ^ mg_swz(r)) << 4));
+            bfr[j] = *reinterpret_cast<const bf16x8*>(xb + r * RB + ((c ^ mg_swz_rb<RB>(r)) << 4));
           }
 #pragma unroll
           for (int f = 0; f < FN; ++f)
 #pragma unroll
             for (int j = 0; j < FM; ++j)
               acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], bfr[j], acc[f][j], 0, 0, 0);
-        }
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {  // four k32 steps per 128-wide k-step; lane reads 8 bytes
+        } else {
           const int c = kk * 2 + (g >> 1), hb = (g & 1) * 8;
           long af[FN], bfr[FM];
 #pragma unroll
           for (int f = 0; f < FN; ++f)
-            af[f] = *reinterpret_cast<const long*>(wb + arow[f] * MG_ROWB + ((c ^ mg_swz(arow[f])) << 4) + hb);
+            af[f] = *reinterpret_cast<const long*>(wb + arow[f] * RB + ((c ^ mg_swz_rb<RB>(arow[f])) << 4) + hb);
 #pragma unroll
           for (int j = 0; j < FM; ++j) {
             const int r = brow0 + j * 16;
-            bfr[j] = *reinterpret_cast<const long*>(xb + r * MG_ROWB + ((c ^ mg_swz(r)) << 4) + hb);
+            bfr[j] = *reinterpret_cast<const long*>(xb + r * RB + ((c ^ mg_swz_rb<RB>(r)) << 4) + hb);
           }
 #pragma unroll
           for (int f = 0; f < FN; ++f)
@@ -244,6 +257,31 @@ __global__ void __launch_bounds__(64 * WM * WN) mgemm_kernel(MgArgs a) {
       fill = fill + 1 == S ? 0 : fill + 1;
     }
 
+    // ---- intra-workgroup split-K: the WK waves of a sub-tile add up through LDS (fixed order)
+    if constexpr (WK > 1) {
+      mg_barrier();  // every wave's last fragment reads are done; no DMA is in flight
+      float* red = reinterpret_cast<float*>(lds);
+      if (wk > 0) {
+#pragma unroll
+        for (int f = 0; f < FN; ++f)
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+            *reinterpret_cast<f32x4*>(red + ((((wk - 1) * WM * WN + wt) * FN + f) * FM + j) * 256 + lane * 4) =
+                acc[f][j];
+      }
+      mg_barrier();
+      if (wk == 0) {
+#pragma unroll
+        for (int k2 = 1; k2 < WK; ++k2)
+#pragma unroll
+          for (int f = 0; f < FN; ++f)
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+              acc[f][j] += *reinterpret_cast<const f32x4*>(red + ((((k2 - 1) * WM * WN + wt) * FN + f) * FM + j) * 256 +
+                                                           lane * 4);
+      }
+    }
+
     // ---- a tile shared by several workgroups: publish this partial tile; the last arriver reduces
     const long long i_first = (long long)tile * T;
     const int w_first = (int)(((i_first + 1) * a.nwg - 1) / a.total);
@@ -252,11 +290,13 @@ __global__ void __launch_bounds__(64 * WM * WN) mgemm_kernel(MgArgs a) {
     if (nc > 1) {
       float* base = a.ws + (long long)tile * a.cmax * (BM * BN);
       float* slab = base + (long long)(lid - w_first) * (BM * BN);
+      if (wk == 0) {
 #pragma unroll
-      for (int f = 0; f < FN; ++f)
+        for (int f = 0; f < FN; ++f)
 #pragma unroll
-        for (int j = 0; j < FM; ++j)
-          *reinterpret_cast<f32x4*>(slab + (((wid * FN + f) * FM + j) * 64 + lane) * 4) = acc[f][j];
+          for (int j = 0; j < FM; ++j)
+            *reinterpret_cast<f32x4*>(slab + (((wt * FN + f) * FM + j) * 64 + lane) * 4) = acc[f][j];
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -275,21 +315,24 @@ __global__ void __launch_bounds__(64 * WM * WN) mgemm_kernel(MgArgs a) {
       if (*flag == 0u) continue;
       // fixed summation order over ALL slabs (own included): the result does not depend on which
       // workgroup arrived last
-#pragma unroll
-      for (int f = 0; f < FN; ++f)
-#pragma unroll
-        for (int j = 0; j < FM; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int s2 = 0; s2 < nc; ++s2) {
-        const float* sl = base + (long long)s2 * (BM * BN);
+      if (wk == 0) {
 #pragma unroll
         for (int f = 0; f < FN; ++f)
 #pragma unroll
-          for (int j = 0; j < FM; ++j) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(sl + (((wid * FN + f) * FM + j) * 64 + lane) * 4);
-            acc[f][j] += v;
-          }
+          for (int j = 0; j < FM; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s2 = 0; s2 < nc; ++s2) {
+          const float* sl = base + (long long)s2 * (BM * BN);
+#pragma unroll
+          for (int f = 0; f < FN; ++f)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+              const f32x4 v = *reinterpret_cast<const f32x4*>(sl + (((wt * FN + f) * FM + j) * 64 + lane) * 4);
+              acc[f][j] += v;
+            }
+        }
       }
     }
+    if (wk != 0) continue;
 
     // ---- epilogue: lane holds out[m = brow][n = 4 g + i], i < 4, of every fragment pair
 #pragma unroll
@@ -342,34 +385,35 @@ namespace {
 
 // Tile configurations (BM x BN, waves WM x WN, ring depth S).  Index = config id of the host API.
 struct MgCfg {
-  int bm, bn, wm, wn, s;
+  int bm, bn, wm, wn, wk, rb, s;
 };
 constexpr MgCfg kMgCfgs[] = {
-    {16, 128, 1, 4, 4},   //  0  batched decode, M <= 16
-    {16, 128, 1, 4, 3},   //  1  same, smaller ring (3 workgroups / CU)
-    {32, 128, 1, 4, 3},   //  2  M <= 32
-    {32, 256, 1, 4, 3},   //  3  M <= 32, wide weight tile
-    {64, 128, 1, 4, 3},   //  4  M <= 64
-    {64, 256, 1, 4, 3},   //  5  M <= 64, wide weight tile
-    {64, 64, 2, 2, 4},    //  6  M <= 64, narrow (more tiles)
-    {128, 128, 2, 2, 3},  //  7  M <= 128
-    {128, 64, 2, 2, 4},   //  8  prefill, small N
-    {256, 128, 2, 2, 3},  //  9  prefill
-    {256, 64, 4, 1, 3},   // 10  prefill, small N
-    {128, 256, 2, 4, 3},  // 11  prefill, 8 waves
-    {256, 256, 2, 4, 2},  // 12  prefill, 8 waves, 256 x 256
-    {16, 64, 1, 4, 4},    // 13  decode, narrow (small-N shapes; no SwiGLU)
-    {32, 64, 1, 4, 4},    // 14  decode, narrow (no SwiGLU)
-    {64, 128, 2, 4, 3},   // 15  M <= 64, 8 waves
-    {128, 128, 2, 4, 3},  // 16  M <= 128, 8 waves
-    // deep rings for weight streaming (M <= 64): 5-7 k-steps in flight per workgroup
-    {16, 64, 1, 4, 8},    // 17  (no SwiGLU)
-    {16, 128, 1, 4, 6},   // 18
-    {32, 64, 1, 4, 8},    // 19  (no SwiGLU)
-    {32, 128, 1, 4, 6},   // 20
-    {64, 128, 1, 4, 5},   // 21
-    {64, 64, 2, 2, 7},    // 22
-    {16, 256, 1, 4, 4},   // 23  wide
+    // --- weight streaming (batched decode): small tiles, many workgroups; wk waves share a tile
+    {16, 16, 1, 1, 4, 512, 4},    //  0  (no SwiGLU)
+    {16, 32, 1, 1, 4, 512, 4},    //  1
+    {16, 32, 1, 2, 2, 512, 4},    //  2  (no SwiGLU)
+    {16, 64, 1, 2, 2, 256, 4},    //  3
+    {16, 64, 1, 4, 1, 256, 5},    //  4  (no SwiGLU)
+    {16, 128, 1, 4, 1, 128, 6},   //  5
+    {32, 32, 1, 1, 4, 512, 3},    //  6
+    {32, 32, 2, 1, 2, 512, 3},    //  7
+    {32, 64, 1, 2, 2, 256, 4},    //  8
+    {32, 128, 1, 4, 1, 128, 6},   //  9
+    {64, 32, 1, 1, 4, 256, 4},    // 10
+    {64, 32, 2, 1, 2, 256, 4},    // 11
+    {64, 64, 2, 2, 1, 256, 4},    // 12
+    {64, 128, 1, 4, 1, 128, 5},   // 13
+    {64, 64, 2, 2, 1, 128, 7},    // 14
+    // --- larger M (prefill chunks): MFMA-dense tiles
+    {128, 128, 2, 2, 1, 128, 3},  // 15
+    {128, 64, 2, 2, 1, 128, 4},   // 16
+    {256, 128, 2, 2, 1, 128, 3},  // 17
+    {256, 64, 4, 1, 1, 128, 3},   // 18
+    {128, 256, 2, 4, 1, 128, 3},  // 19  8 waves
+    {256, 256, 2, 4, 1, 128, 2},  // 20  8 waves
+    {64, 128, 2, 4, 1, 128, 3},   // 21  8 waves
+    {128, 128, 2, 4, 1, 128, 3},  // 22  8 waves
+    {128, 64, 2, 2, 2, 256, 3},   // 23  k-shared waves, 8 waves
 };
 constexpr int kMgNumCfgs = sizeof(kMgCfgs) / sizeof(kMgCfgs[0]);
 
@@ -379,9 +423,9 @@ int mg_launch(const MgArgs& a, int grid, hipStream_t s) {
   if constexpr (!ok) {
     return -2;
   } else {
-    hipLaunchKernelGGL(
-        (mgemm_kernel<kMgCfgs[C].bm, kMgCfgs[C].bn, kMgCfgs[C].wm, kMgCfgs[C].wn, kMgCfgs[C].s, EPI, FP8>),
-        dim3(grid), dim3(64 * kMgCfgs[C].wm * kMgCfgs[C].wn), 0, s, a);
+    hipLaunchKernelGGL((mgemm_kernel<kMgCfgs[C].bm, kMgCfgs[C].bn, kMgCfgs[C].wm, kMgCfgs[C].wn, kMgCfgs[C].wk,
+                                      kMgCfgs[C].rb, kMgCfgs[C].s, EPI, FP8>),
+                       dim3(grid), dim3(64 * kMgCfgs[C].wm * kMgCfgs[C].wn * kMgCfgs[C].wk), 0, s, a);
     return (int)hipGetLastError();
   }
 }
@@ -411,14 +455,15 @@ int mg_cfg(const MgArgs& a, int grid, int cfg, int epi, hipStream_t s) {
 extern "C" int k8s_mgemm_num_configs() { return kMgNumCfgs; }
 
 // (bm, bn) of a config: the Python planner sizes grids from them.
-extern "C" int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* lds_bytes, int* swiglu) {
+extern "C" int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* lds_bytes, int* swiglu, int* rb) {
   if (cfg < 0 || cfg >= kMgNumCfgs) return -1;
   const MgCfg c = kMgCfgs[cfg];
   *bm = c.bm;
   *bn = c.bn;
-  *threads = 64 * c.wm * c.wn;
-  *lds_bytes = c.s * (c.bm + c.bn) * MG_ROWB + 16;
+  *threads = 64 * c.wm * c.wn * c.wk;
+  *lds_bytes = c.s * (c.bm + c.bn) * c.rb + 16;
   *swiglu = (c.bn / (c.wn * 16)) % 2 == 0;
+  *rb = c.rb;
   return 0;
 }
 
@@ -431,7 +476,7 @@ MgGeom mg_geom(int M, int N_out, int K, int epi, int fp8, int cfg) {
   const int feat = epi == MG_SWIGLU ? c.bn / 2 : c.bn;
   MgGeom g;
   g.tiles = (long long)((N_out + feat - 1) / feat) * ((M + c.bm - 1) / c.bm);
-  g.T = (long long)K * (fp8 ? 1 : 2) / MG_ROWB;
+  g.T = (long long)K * (fp8 ? 1 : 2) / c.rb;
   g.total = g.tiles * g.T;
   return g;
 }
@@ -443,7 +488,7 @@ extern "C" int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, in
                                    int* cmax, long long* ws_elems) {
   if (cfg < 0 || cfg >= kMgNumCfgs || M <= 0 || N_out <= 0 || K <= 0 || nwg <= 0) return -1;
   const MgGeom g = mg_geom(M, N_out, K, epi, fp8, cfg);
-  if (g.T <= 0 || nwg > g.total) return -1;
+  if (g.T <= 0 || (long long)K * (fp8 ? 1 : 2) % kMgCfgs[cfg].rb != 0 || nwg > g.total) return -1;
   int cm = 1;
   for (long long t = 0; t < g.tiles; ++t) {
     const long long f = ((t * g.T + 1) * nwg - 1) / g.total, l = (((t + 1) * g.T) * nwg - 1) / g.total;
@@ -464,7 +509,7 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   if (cfg < 0 || cfg >= kMgNumCfgs || M <= 0 || N_out <= 0 || K <= 0 || nwg <= 0 || cmax < 1) return -1;
   if (N_out % 4 != 0) return -1;
   const long long kbytes = (long long)K * (fp8 ? 1 : 2);
-  if (kbytes % MG_ROWB != 0) return -1;
+  if (kbytes % kMgCfgs[cfg].rb != 0) return -1;
   const MgGeom g = mg_geom(M, N_out, K, epi, fp8, cfg);
   if (nwg > g.total) return -1;
   if (cmax > 1 && (ws == nullptr || tickets == nullptr)) return -3;

@@ -85,10 +85,10 @@ __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, co
                                                     uint32_t* __restrict__ row_cnt) {
   __shared__ float sv[ST / 64];
   __shared__ int si[ST / 64];
-  __shared__ float hist_mass[256];
-  __shared__ float red[16];
+  __shared__ unsigned long long hist_mass[256];
+  __shared__ unsigned long long sh_z;
   __shared__ uint32_t sh_prefix;
-  __shared__ float sh_above;
+  __shared__ unsigned long long sh_above;
   const int b = blockIdx.y, part = blockIdx.x;
   if (ctx_inc != nullptr && ctx_inc[b] <= 0) return;  // padded row
   const int V = Vs * shards;
@@ -108,25 +108,34 @@ __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, co
     for (int v = threadIdx.x; v < V; v += ST) mx = better(mx, ArgMax{L(v), v});
     mx = block_argmax(mx, sv, si);
     const float M = mx.v;
-    float z = 0.f;
-    for (int v = threadIdx.x; v < V; v += ST) z += __expf((L(v) - M) * invT);
-    z = block_sum(z, red);
-    const float target = P * z;
+    // Probability mass in 2^-40 fixed point, summed with INTEGER atomics: the histogram, the total
+    // and hence the threshold do not depend on the order the adds land in, so every TP rank (same
+    // logits) picks the same nucleus and the same token.
+    auto mass = [&](float l) -> unsigned long long {
+      return (unsigned long long)(__expf((l - M) * invT) * 1099511627776.0f);
+    };
+    if (threadIdx.x == 0) sh_z = 0ull;
+    __syncthreads();
+    unsigned long long zl = 0ull;
+    for (int v = threadIdx.x; v < V; v += ST) zl += mass(L(v));
+    atomicAdd(&sh_z, zl);
+    __syncthreads();
+    const unsigned long long target = (unsigned long long)((double)sh_z * (double)P);
     uint32_t prefix = 0;
-    float above = 0.f;  // mass of tokens strictly above the current prefix bucket
+    unsigned long long above = 0ull;  // mass of tokens strictly above the current prefix bucket
     for (int round = 0; round < 4; ++round) {
       const int shift = 24 - 8 * round;
-      for (int i = threadIdx.x; i < 256; i += ST) hist_mass[i] = 0.f;
+      for (int i = threadIdx.x; i < 256; i += ST) hist_mass[i] = 0ull;
       __syncthreads();
       for (int v = threadIdx.x; v < V; v += ST) {
         const float l = L(v);
         const uint32_t k = ord_key(l);
         const bool match = round == 0 || (k >> (shift + 8)) == (prefix >> (shift + 8));
-        if (match) atomicAdd(&hist_mass[(k >> shift) & 255], __expf((l - M) * invT));
+        if (match) atomicAdd(&hist_mass[(k >> shift) & 255], mass(l));
       }
       __syncthreads();
       if (threadIdx.x == 0) {
-        float cum = above;
+        unsigned long long cum = above;
         int bsel = 0;
         for (int bk = 255; bk >= 0; --bk) {
           if (cum + hist_mass[bk] >= target || bk == 0) { bsel = bk; break; }

@@ -9,7 +9,9 @@
 //
 // Memory: each rank owns one IPC region (hipExtMallocWithFlags(..., hipDeviceMallocUncached), so no
 // L2 holds stale copies of bytes another GPU wrote), mapped into every peer process:
-//   [flags: XG_MAX_BLOCKS x 8 u32][data: 2 slots x W sources x slot_bytes]
+//   [flags: XG_MAX_BLOCKS x 8 u32][flagged data: 2 slots x W x slot_bytes][LL data: 2 slots x W x slot_bytes]
+// The LL rows are a region of their own: an LL reader accepts a word whose tag equals its epoch, and
+// raw payload bytes left by the flagged kernels could otherwise carry that tag by chance.
 // Protocol per workgroup b of call k (epoch e = per-workgroup counter, identical on every rank since
 // all ranks issue the same sequence of calls with the same fixed grid):
 //   1. stores of its chunk into slot (e & 1), source row `rank`, of every peer   (sc0 sc1, 16 B)
@@ -144,8 +146,9 @@ __global__ __launch_bounds__(XG_THREADS) void xg_allreduce_ll_kernel(XgArgs a) {
   typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
   const uint32_t e = xg_epoch(a);
   const long long nwords = a.bytes >> 2;
-  const long long my_row = XG_FLAG_BYTES + ((long long)(e & 1) * W + a.rank) * a.slot_bytes;
-  const long long slot0 = XG_FLAG_BYTES + (long long)(e & 1) * W * a.slot_bytes;
+  const long long ll0 = XG_FLAG_BYTES + 2LL * W * a.slot_bytes;  // the LL region
+  const long long my_row = ll0 + ((long long)(e & 1) * W + a.rank) * a.slot_bytes;
+  const long long slot0 = ll0 + (long long)(e & 1) * W * a.slot_bytes;
   const uint32_t* in = reinterpret_cast<const uint32_t*>(a.in);
   uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
   const long long stride = (long long)gridDim.x * XG_THREADS;
@@ -227,7 +230,7 @@ static int xg_fill(XgArgs& a, void* const* bases, uint32_t* counters, uint32_t* 
                    long long bytes, long long slot_bytes, int rank, int world, long long timeout_ticks) {
   if (world < 2 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return -1;
   if (bytes <= 0 || bytes > slot_bytes || (bytes & 15) || ((uintptr_t)in & 15) || ((uintptr_t)out & 15)) return -2;
-  if (XG_FLAG_BYTES + 2LL * world * slot_bytes > 0x7fffffffLL) return -3;
+  if (XG_FLAG_BYTES + 4LL * world * slot_bytes > 0x7fffffffLL) return -3;
   for (int i = 0; i < XG_MAX_WORLD; ++i) a.base[i] = i < world ? static_cast<char*>(bases[i]) : nullptr;
   a.counters = counters; a.err = err;
   a.in = static_cast<const char*>(in); a.out = static_cast<char*>(out); a.res = nullptr;

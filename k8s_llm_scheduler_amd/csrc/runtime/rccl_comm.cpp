@@ -65,6 +65,12 @@ void RcclComm::all_gather(const void* send, void* recv, size_t count, int dtype,
   ck(ncclAllGather(send, recv, count, dt(dtype), static_cast<ncclComm_t>(comm_), s), "ncclAllGather");
 }
 
+std::string RcclComm::async_error() const {
+  ncclResult_t r = ncclSuccess;
+  if (ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
+  return r == ncclSuccess ? std::string() : std::string(ncclGetErrorString(r));
+}
+
 void RcclComm::broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s) {
   ck(ncclBroadcast(buf, buf, count, dt(dtype), root, static_cast<ncclComm_t>(comm_), s), "ncclBroadcast");
 }

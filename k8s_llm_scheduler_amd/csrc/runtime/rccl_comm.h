@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 #include <vector>
 
 namespace k8sllm {
@@ -18,6 +19,8 @@ class RcclComm {
   void all_reduce(const void* send, void* recv, size_t count, int dtype, int red, hipStream_t s);
   void all_gather(const void* send, void* recv, size_t count_per_rank, int dtype, hipStream_t s);
   void broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s);
+  // ncclCommGetAsyncError: "" when healthy, else the error text (a peer died, a transport failed)
+  std::string async_error() const;
   int world() const { return world_; }
   int rank() const { return rank_; }
 

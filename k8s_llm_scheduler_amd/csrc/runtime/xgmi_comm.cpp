@@ -36,7 +36,7 @@ XgmiComm::XgmiComm(int world, int rank, long long slot_bytes, int blocks, double
   if (world < 2 || world > 8 || rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad world/rank");
   if (slot_bytes <= 0 || (slot_bytes & 4095)) throw std::invalid_argument("XgmiComm: slot_bytes must be a multiple of 4096");
   if (blocks < 1 || blocks > k8s_xgmi_max_blocks()) throw std::invalid_argument("XgmiComm: bad block count");
-  region_bytes_ = k8s_xgmi_flag_bytes() + 2LL * world * slot_bytes;
+  region_bytes_ = k8s_xgmi_flag_bytes() + 4LL * world * slot_bytes;  // flagged + LL slot regions
   if (region_bytes_ > 0x7fffffffLL) throw std::invalid_argument("XgmiComm: region larger than 2 GiB");
   timeout_ticks_ = static_cast<long long>(timeout_s * 100e6);  // s_memrealtime runs at 100 MHz
   ck(hipGetDevice(&device_), "hipGetDevice");
@@ -44,6 +44,8 @@ XgmiComm::XgmiComm(int world, int rank, long long slot_bytes, int blocks, double
   ck(hipMemset(region_, 0, region_bytes_), "hipMemset");
   ck(hipMalloc(&counters_, (k8s_xgmi_max_blocks() + 1) * sizeof(uint32_t)), "hipMalloc");
   ck(hipMemset(counters_, 0, (k8s_xgmi_max_blocks() + 1) * sizeof(uint32_t)), "hipMemset");
+  ck(hipHostMalloc(reinterpret_cast<void**>(&host_err_), sizeof(uint32_t), hipHostMallocDefault), "hipHostMalloc");
+  *host_err_ = 0;
   ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
   bases_.assign(world, nullptr);
   mapped_.assign(world, false);
@@ -55,6 +57,7 @@ XgmiComm::~XgmiComm() {
     if (mapped_[i] && bases_[i]) (void)hipIpcCloseMemHandle(bases_[i]);
   if (region_) (void)hipFree(region_);
   if (counters_) (void)hipFree(counters_);
+  if (host_err_) (void)hipHostFree(host_err_);
 }
 
 std::string XgmiComm::handle() const {
@@ -105,6 +108,13 @@ uint32_t XgmiComm::error() {
   ck(hipMemcpy(&v, counters_ + k8s_xgmi_max_blocks(), sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy");
   return v;
 }
+
+void XgmiComm::snapshot_error(hipStream_t s) {
+  ck(hipMemcpyAsync(host_err_, counters_ + k8s_xgmi_max_blocks(), sizeof(uint32_t), hipMemcpyDeviceToHost, s),
+     "hipMemcpyAsync(error word)");
+}
+
+uint32_t XgmiComm::last_error() const { return *reinterpret_cast<volatile uint32_t*>(host_err_); }
 
 void XgmiComm::reset_error() {
   ck(hipMemset(counters_ + k8s_xgmi_max_blocks(), 0, sizeof(uint32_t)), "hipMemset");

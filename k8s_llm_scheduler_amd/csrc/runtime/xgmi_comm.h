@@ -23,6 +23,10 @@ class XgmiComm {
   void all_reduce_bf16(const void* in, void* out, long long bytes, hipStream_t s, const void* residual = nullptr);
   void all_gather(const void* in, void* out, long long bytes_per_rank, hipStream_t s);
   uint32_t error();                                   // poll-timeout bitmask (synchronizes the device)
+  // Health check without an extra sync: enqueue a copy of the error word to pinned host memory on
+  // `s`; after the caller's own synchronization of `s`, last_error() is that word.
+  void snapshot_error(hipStream_t s);
+  uint32_t last_error() const;
   void reset_error();
 
   int world() const { return world_; }
@@ -40,6 +44,7 @@ class XgmiComm {
   int device_ = 0;
   void* region_ = nullptr;      // own IPC region (uncached)
   uint32_t* counters_ = nullptr;  // [max_blocks] epochs + 1 error word
+  uint32_t* host_err_ = nullptr;  // pinned copy of the error word (snapshot_error)
   std::vector<void*> bases_;    // every rank's region in this address space
   std::vector<bool> mapped_;    // true where bases_[i] came from hipIpcOpenMemHandle
   bool opened_ = false;

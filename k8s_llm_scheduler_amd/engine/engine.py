@@ -480,7 +480,9 @@ class LLMEngine:
                 self.prefilling.remove(r)
                 self.running[r.slot] = r
         if self.gpu:
+            self.model.tp.snapshot_health()
             torch.cuda.synchronize(self.device)
+            self.model.tp.check_health()
         self.stats["prefill_time"] += time.perf_counter() - t0
 
     def _decode(self) -> List[Request]:
@@ -502,8 +504,11 @@ class LLMEngine:
             else:
                 self._decode_step(B, mc)
         self.stats["decode_steps"] += steps
+        tp = self.model.tp
+        tp.snapshot_health()             # rides on the sync below
         hist = self.s_hist[:B].cpu()     # syncs the stream
         nsteps = self.s_steps[:B].cpu()
+        tp.check_health()                # a failed collective raises into the decision service
         self.stats["decode_time"] += time.perf_counter() - t0
         finished = []
         for slot, r in list(self.running.items()):
@@ -573,6 +578,7 @@ class LLMEngine:
 
     def step(self) -> List[Request]:
         with self.lock:
+            self.model.tp.ensure_healthy()
             self._drain_inbox()
             if not self._sync():
                 raise StopIteration("engine stopped by rank 0")
@@ -678,7 +684,20 @@ class LLMEngine:
                     for r in reqs:
                         self.requests.pop(r.rid, None) if r.finished else None
                     raise TimeoutError("decision engine deadline exceeded")
-                self.step()
+                try:
+                    self.step()
+                except StopIteration:
+                    raise
+                except Exception:
+                    # an engine / collective failure ends these requests (their slots and KV blocks
+                    # are released) and propagates to the decision service's retry / breaker path
+                    for r in reqs:
+                        if not r.finished:
+                            if r in self.waiting:
+                                self.waiting.remove(r)
+                            self._finish(r, "error")
+                        self.requests.pop(r.rid, None)
+                    raise
             outs = [self.output(r) for r in reqs]
             for r in reqs:
                 self.requests.pop(r.rid, None)

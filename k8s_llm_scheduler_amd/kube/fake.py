@@ -73,6 +73,7 @@ class FakeKubeAPI:
         self.duplicate_events = duplicate_events
         self.run_bound_pods = run_bound_pods     # bound pods transition to Running (kubelet stand-in)
         self.bindings: List[Tuple[str, str]] = []  # (ns/name, node)
+        self.binding_times: Dict[str, float] = {}   # ns/name -> time.perf_counter() of the successful bind
         self._history: List[Tuple[int, WatchEvent]] = []   # (resourceVersion, event): watch-from-rv replay
         self.calls: Dict[str, int] = {}
         for n in nodes or []:
@@ -217,5 +218,6 @@ class FakeKubeAPI:
                 pod["status"]["phase"] = "Running"
             pod["metadata"]["resourceVersion"] = str(next(self._rv))
             self.bindings.append((f"{namespace}/{name}", node))
+            self.binding_times[f"{namespace}/{name}"] = time.perf_counter()
             self._emit("MODIFIED", pod)
             return {"kind": "Status", "status": "Success"}

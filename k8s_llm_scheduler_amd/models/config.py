@@ -57,6 +57,10 @@ PRESETS = {
     # tiny: same code paths (GQA 2:1, head_dim 128) at a size that runs on CPU in tests
     "tiny": LlamaConfig("tiny", 2, 256, 4, 2, 128, 512, 16384, bos_id=16128, eos_ids=(16129, 16136, 16137),
                         max_position=4096, rope_scaling=LLAMA3_ROPE_SCALING),
+    # tiny-tp8: the 70B's head layout scaled down (GQA 2:1, 8 kv heads, head_dim 128), so TP = 1/2/4/8 all
+    # shard like the 70B does (one kv head per rank at TP = 8) -- multi-rank tests
+    "tiny-tp8": LlamaConfig("tiny-tp8", 2, 2048, 16, 8, 128, 4096, 16384, bos_id=16128,
+                            eos_ids=(16129, 16136, 16137), max_position=4096, rope_scaling=LLAMA3_ROPE_SCALING),
 }
 PRESETS["llama-3-70b"] = PRESETS["llama-3.3-70b"]
 PRESETS["llama-3.1-8b"] = LlamaConfig("llama-3.1-8b", 32, 4096, 32, 8, 128, 14336, 128256,

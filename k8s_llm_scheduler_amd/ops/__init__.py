@@ -335,7 +335,8 @@ MG_GRIDS = (1, 2, 4, 8, 16, -256, -512, -768, -1024)
 
 
 def mgemm_configs() -> list:
-    """(BM, BN, threads, LDS bytes, SwiGLU-capable) of every compiled mgemm.hip tile configuration."""
+    """(BM, BN, threads, LDS bytes, SwiGLU-capable, row bytes per k-step) of every compiled mgemm.hip tile
+    configuration."""
     global _MG_CFGS
     if _MG_CFGS is None:
         _MG_CFGS = [tuple(c) for c in native().mgemm_configs()]
@@ -344,7 +345,7 @@ def mgemm_configs() -> list:
 
 def _mg_occupancy(cfg: int) -> int:
     """Workgroups of a configuration resident per CU (LDS and the 32-wave limit)."""
-    _, _, threads, lds, _ = mgemm_configs()[cfg]
+    _, _, threads, lds, _, _ = mgemm_configs()[cfg]
     return max(1, min(160 * 1024 // lds, 2048 // threads))
 
 
@@ -355,7 +356,7 @@ def _mg_tiles(cfg: int, M: int, N: int, epi: int) -> int:
 
 
 def mgemm_nwg(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int) -> int:
-    total = _mg_tiles(cfg, M, N, epi) * (K * (1 if fp8 else 2) // 128)
+    total = _mg_tiles(cfg, M, N, epi) * (K * (1 if fp8 else 2) // mgemm_configs()[cfg][5])
     nwg = _mg_tiles(cfg, M, N, epi) * grid if grid > 0 else -grid
     return max(1, min(nwg, total))
 
@@ -364,11 +365,16 @@ def mgemm_valid(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int
     if cfg < 0 or cfg >= len(mgemm_configs()):
         return False
     kb = K * (1 if fp8 else 2)
-    if kb % 128 or N % 4 or M <= 0:
+    if kb % mgemm_configs()[cfg][5] or N % 4 or M <= 0:
         return False
     if epi == EPI_SWIGLU and not mgemm_configs()[cfg][4]:
         return False
     return grid != 0
+
+
+def _mgemm_ok(N: int, K: int, fp8: bool) -> bool:
+    """Some mgemm configuration can run this shape (128-byte k-steps, 4-column output groups)."""
+    return N % 4 == 0 and (K * (1 if fp8 else 2)) % 128 == 0
 
 
 @functools.lru_cache(maxsize=4096)
@@ -377,17 +383,31 @@ def _mg_plan_info(M: int, N: int, K: int, epi: int, fp8: bool, cfg: int, nwg: in
 
 
 def mgemm_heuristic(M: int, N: int, K: int, epi: int, fp8: bool, num_cus: int = 256) -> Tuple[int, int]:
-    """Tile + grid choice when the tuned table has no entry for the shape."""
-    if M <= 128:   # weight streaming: every CU busy, equal shares
-        cfg = 0 if M <= 16 else 2 if M <= 32 else 4 if M <= 64 else 7
-        return cfg, -num_cus * _mg_occupancy(cfg)
-    cfg = 9
+    """Tile + grid choice for a shape the tuned table has never seen (tools/mgemm_tune.py measures the
+    real choices; this only has to be reasonable)."""
+    if M <= 64:    # weight streaming: small tiles, k-shared waves, one workgroup per tile
+        cfg = (1 if epi == EPI_SWIGLU else 0) if M <= 16 else 7 if M <= 32 else 11
+    elif M <= 128:
+        cfg = 12
+    elif M <= 256:
+        cfg = 23
+    else:
+        cfg = 19
+    if not mgemm_valid(cfg, M, N, K, epi, fp8):   # K not a multiple of the config's k-step: 128-byte k-steps
+        cfg = 5 if M <= 16 else 9 if M <= 32 else 13 if M <= 64 else 15 if M <= 128 else 17
     tiles = _mg_tiles(cfg, M, N, epi)
-    return cfg, (1 if tiles >= num_cus else max(1, min(16, num_cus // tiles)))
+    if tiles >= num_cus // 2:
+        return cfg, 1
+    steps = K * (1 if fp8 else 2) // mgemm_configs()[cfg][5]
+    split = 1
+    while tiles * split * 2 <= 2 * num_cus and steps // (split * 2) >= 8:
+        split *= 2
+    return cfg, split
 
 
-# Tuned plans per shape: engine/assets/mgemm_gfx950.json, written by tools/mgemm_tune.py.
-# Keys "M_bucket,N,K,epi,fp8" with M_bucket the smallest of GEMM_M_BUCKETS >= M (else the next power of 2).
+# Tuned plans: engine/assets/mgemm_gfx950.json, written by tools/mgemm_tune.py, keyed
+# "M_bucket,N,K,epi,fp8".  A row count between tuned buckets uses the plan of the nearest bucket
+# above it (the largest one beyond the table).
 _MG_TABLE: Optional[dict] = None
 MG_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "assets",
                              "mgemm_gfx950.json")
@@ -400,7 +420,7 @@ def _mg_bucket(M: int) -> int:
     return 1 << max(0, (M - 1).bit_length())
 
 
-def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
+def _mg_load_table() -> dict:
     global _MG_TABLE
     if _MG_TABLE is None:
         _MG_TABLE = {}
@@ -408,10 +428,22 @@ def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
             import json
 
             with open(MG_TABLE_PATH) as f:
-                _MG_TABLE = {k: tuple(v) for k, v in json.load(f).get("plans", {}).items()}
-    hit = _MG_TABLE.get(f"{_mg_bucket(M)},{N},{K},{epi},{int(fp8)}")
-    if hit is not None and mgemm_valid(hit[0], M, N, K, epi, fp8, hit[1]):
-        return int(hit[0]), int(hit[1])
+                plans = json.load(f).get("plans", {})
+            for k, v in plans.items():
+                mb, n, kk, epi, fp8 = (int(t) for t in k.split(","))
+                _MG_TABLE.setdefault((n, kk, epi, fp8), []).append((mb, int(v[0]), int(v[1])))
+            for lst in _MG_TABLE.values():
+                lst.sort()
+    return _MG_TABLE
+
+
+def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
+    rows = _mg_load_table().get((N, K, epi, int(fp8)))
+    if rows:
+        mb = _mg_bucket(M)
+        pick = next((r for r in rows if r[0] >= mb), rows[-1])
+        if mgemm_valid(pick[1], M, N, K, epi, fp8, pick[2]):
+            return pick[1], pick[2]
     return mgemm_heuristic(M, N, K, epi, fp8)
 
 
@@ -443,16 +475,26 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
     return out
 
 
+# GEMMs with more than GEMV_MAX_M rows run the hand-written MFMA GEMM (mgemm.hip).  K8S_GEMM=library routes
+# them to hipBLASLt / rocBLAS through torch instead (A/B comparisons; tools/mgemm_tune.py times both).
+GEMM_BACKEND = os.environ.get("K8S_GEMM", "mgemm")
+if GEMM_BACKEND not in ("mgemm", "library"):
+    raise ValueError(f"K8S_GEMM must be mgemm or library (got {GEMM_BACKEND!r})")
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
-    """y = x @ w.T with w [N, K] bf16.  M <= 8 rows: hand-written HBM-streaming GEMV; M <= 64
-    (batched decode): MFMA skinny GEMM; larger M (prefill): library GEMM (hipBLASLt via torch)."""
+    """y = x @ w.T with w [N, K] (bf16 or Fp8Weight).  M <= 8 rows: hand-written HBM-streaming GEMV;
+    more rows (batched decode, prefill): hand-written MFMA GEMM (mgemm.hip)."""
     if not _gpu(x, w):
         return ref.linear(_ref_act_quant(x, w), w, out_dtype)
     x2 = x.reshape(-1, x.shape[-1])
+    epi = EPI_F32 if out_dtype == F32 else EPI_BF16
     if x2.shape[0] <= GEMV_MAX_M:
-        y = _gemv(x2.contiguous(), w, EPI_F32 if out_dtype == F32 else EPI_BF16, out_dtype or BF16)
+        y = _gemv(x2.contiguous(), w, epi, out_dtype or BF16)
+    elif GEMM_BACKEND == "mgemm" and _mgemm_ok(w.shape[0], x2.shape[1], _is_fp8(w)) and out_dtype in (None, BF16, F32):
+        y = mgemm(x2.contiguous(), w, epi)
     elif _use_skinny(x2.shape[0], w, x2.shape[1]):
-        y = _skinny(x2.contiguous(), w, EPI_F32 if out_dtype == F32 else EPI_BF16, out_dtype or BF16)
+        y = _skinny(x2.contiguous(), w, epi, out_dtype or BF16)
     elif _is_fp8(w):
         y = _fp8_gemm(x2, w, out_dtype)
     else:
@@ -538,12 +580,14 @@ def _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, contex
 
 
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
-    """silu(x @ Wg.T) * (x @ Wu.T) with w_gate_up = [Wg; Wu] ([2I, K])."""
+    """silu(x @ Wg.T) * (x @ Wu.T) with w_gate_up = [Wg; Wu] ([2I, K]); the SwiGLU is the GEMM's epilogue."""
     if not _gpu(x, w_gate_up):
         return ref.linear_swiglu(_ref_act_quant(x, w_gate_up), w_gate_up)
     x2 = x.reshape(-1, x.shape[-1])
     if x2.shape[0] <= GEMV_MAX_M:
         y = _gemv(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
+    elif GEMM_BACKEND == "mgemm" and _mgemm_ok(w_gate_up.shape[0] // 2, x2.shape[1], _is_fp8(w_gate_up)):
+        y = mgemm(x2.contiguous(), w_gate_up, EPI_SWIGLU)
     elif _use_skinny(x2.shape[0], w_gate_up, x2.shape[1]):
         y = _skinny(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
     elif _is_fp8(w_gate_up):

@@ -1,1 +1,1 @@
-from .comm import ControlChannel, TPGroup, init_from_env, make_control_channel  # noqa: F401
+from .comm import CollectiveError, ControlChannel, TPGroup, init_from_env, make_control_channel  # noqa: F401

@@ -113,6 +113,43 @@ class TPGroup:
         if self.world > 1:
             dist.barrier(group=self.group)
 
+    # ---- failure detection (engine faults must reach the retry / breaker path)
+    failed: Optional[str] = None    # sticky: set by check_health on the first collective failure
+
+    def ensure_healthy(self) -> None:
+        """Fail fast (before launching more collectives) once a failure has been seen."""
+        if self.failed:
+            raise CollectiveError(self.failed)
+
+    def snapshot_health(self) -> None:
+        """Enqueue (on the current stream) a copy of the xGMI error word to pinned host memory; read
+        by :meth:`check_health` after the caller's own stream synchronisation (no extra sync)."""
+        if self.xgmi is not None and not self.simulate:
+            self.xgmi.snapshot_error(-1)
+
+    def check_health(self) -> None:
+        """Raise :class:`CollectiveError` if a collective failed since the communicator was built: an
+        xGMI poll timed out (a peer stalled or died; the kernel drained with partial sums) or RCCL
+        reports an asynchronous error.  The error is sticky -- the ranks' collective sequences are
+        out of step, so every later call fails fast until the engine is rebuilt."""
+        if self.simulate or self.world <= 1:
+            return
+        self.ensure_healthy()
+        if self.xgmi is not None:
+            mask = int(self.xgmi.last_error())
+            if mask:
+                self.failed = (f"xGMI collective timed out waiting for peer rank(s) "
+                               f"{[r for r in range(self.world) if mask >> r & 1]} (rank {self.rank})")
+        if self.rccl is not None and not self.failed:
+            err = self.rccl.async_error()
+            if err:
+                self.failed = f"RCCL communicator error on rank {self.rank}: {err}"
+        self.ensure_healthy()
+
+
+class CollectiveError(RuntimeError):
+    """A tensor-parallel collective failed; the decode results of this step are not trustworthy."""
+
 
 class ControlChannel:
     """TP-rank-0 -> replica object broadcast on a CPU (gloo) group: the replica's leader (global
@@ -245,6 +282,7 @@ def make_xgmi_comm(tp: TPGroup, slot_bytes: Optional[int] = None, blocks: Option
     slot_bytes = int(slot_bytes or os.environ.get("K8S_XGMI_MAX_BYTES", 512 * 1024))
     slot_bytes = (slot_bytes + 4095) // 4096 * 4096
     blocks = int(blocks or os.environ.get("K8S_XGMI_BLOCKS", 16))
+    timeout_s = float(os.environ.get("K8S_XGMI_TIMEOUT_S", timeout_s))
     dev = torch.cuda.current_device()
     comm, handle, err = None, b"", ""
     try:

@@ -1,0 +1,61 @@
+"""Spawn N real rank processes (torch.multiprocessing, one process per rank) that run ``fn(rank, world)``
+under a torchrun-style environment (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*) and collect each rank's
+result or traceback.  Ranks may share one GPU (LOCAL_RANK % device_count) -- the 1-GPU rehearsal of the
+8-GPU node -- or each get their own when the GPUs exist."""
+
+import os
+import queue
+import socket
+import traceback
+
+import torch.multiprocessing as mp
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _entry(fn, rank, world, port, env, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank), HSA_ENABLE_IPC_MODE_LEGACY="0", **env)
+        q.put((rank, "ok", fn(rank, world)))
+    except BaseException:  # noqa: BLE001
+        q.put((rank, "fail", traceback.format_exc()))
+
+
+def run_ranks(fn, world: int, env=None, timeout_s: float = 600.0) -> dict:
+    """Returns {rank: result}; raises AssertionError with every failing rank's traceback."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, dict(env or {}), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    import time
+
+    t0 = time.monotonic()
+    try:
+        while len(got) < world and time.monotonic() - t0 < timeout_s:
+            try:
+                r, status, payload = q.get(timeout=5)
+                got[r] = (status, payload)
+                if status != "ok":
+                    break
+            except queue.Empty:
+                if any(p.exitcode not in (None, 0) for p in procs):
+                    break
+    finally:
+        for p in procs:
+            p.join(60 if len(got) == world else 5)
+            if p.is_alive():
+                p.kill()
+    fails = {r: v[1] for r, v in got.items() if v[0] != "ok"}
+    assert not fails, "\n".join(f"rank {r}:\n{tb}" for r, tb in fails.items())
+    assert len(got) == world, f"ranks finished: {sorted(got)}, exit codes {[p.exitcode for p in procs]}"
+    return {r: v[1] for r, v in got.items()}

@@ -69,9 +69,9 @@ def time_graph(fn, copies: int) -> float:
 
 def candidates(M, N, K, epi, fp8):
     cfgs = ops.mgemm_configs()
-    steps = K * (1 if fp8 else 2) // 128
     out = []
-    for c, (bm, bn, *_r) in enumerate(cfgs):
+    for c, (bm, bn, _th, _lds, _sw, rb) in enumerate(cfgs):
+        steps = K * (1 if fp8 else 2) // rb
         if bm > max(16, 2 * M) or (M > 64 and bm < 64) or (M > 256 and bm < 128):
             continue
         tiles = ops._mg_tiles(c, M, N, epi)
@@ -106,12 +106,15 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tp", type=int, nargs="+", default=[1, 8])
     ap.add_argument("--m", type=int, nargs="+", default=[16, 32, 64, 128, 256, 512])
+    ap.add_argument("--all-buckets", action="store_true", help="every row bucket of ops.GEMM_M_BUCKETS + 2048..8192")
     ap.add_argument("--only", nargs="*", default=None, help="projection names")
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
 
+    if a.all_buckets:
+        a.m = list(ops.GEMM_M_BUCKETS) + [2048, 4096, 8192]
     torch.manual_seed(0)
     lib_table = _load_gemm_table()
     print(f"# library GEMM table loaded: {lib_table}; reps {REPS}; weights cycled over >= {COLD_BYTES >> 20} MiB",
