@@ -265,7 +265,9 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("slot_bytes", &XgmiComm::slot_bytes)
       .def_property_readonly("blocks", &XgmiComm::blocks)
       .def_property_readonly("is_open", &XgmiComm::is_open)
-      .def_property("ll_max_bytes", &XgmiComm::ll_max_bytes, &XgmiComm::set_ll_max_bytes);
+      .def_property("ll_max_bytes", &XgmiComm::ll_max_bytes, &XgmiComm::set_ll_max_bytes)
+      .def_property("twoshot_min_bytes", &XgmiComm::twoshot_min_bytes, &XgmiComm::set_twoshot_min_bytes)
+      .def_property_readonly("max_allreduce_bytes", &XgmiComm::max_allreduce_bytes);
 
   using k8sllm::BlockAllocator;
   py::class_<BlockAllocator::Allocation>(m, "Allocation")

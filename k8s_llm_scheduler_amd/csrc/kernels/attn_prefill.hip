@@ -4,7 +4,13 @@
 // kernel serve plain prefill, chunked prefill and prefix-cached prompts: query i of sequence s
 // sits at absolute position ctx_s - qlen_s + i and attends keys [0, pos].
 //
-// Structure (one workgroup = 4 waves = 64 query rows of ONE query head):
+// GQA packing: one workgroup = 4 waves = 64 (query, head) rows = QT = 64 / G consecutive queries x
+// the G query heads that share ONE kv head (G = nq / nkv), so every K/V tile is fetched once per
+// group instead of once per query head (8x fewer K/V bytes at Llama-3.3-70B's 8:1 GQA), and the
+// causal key range of a workgroup ends at its QT-th query instead of its 64th.  Row r of the
+// workgroup is query tile * QT + r / G, head kvh * G + r % G.
+//
+// Structure:
 //  * "swapped" QK^T: S^T = K . Q^T with v_mfma_f32_16x16x32_bf16, so each lane ends up holding
 //    16 scores of ONE query row (row = lane & 15): the row max/sum need 2 cross-lane steps and
 //    the probabilities feed the P.V MFMA as its A operand straight from registers (the key
@@ -24,7 +30,7 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 __device__ __forceinline__ int v_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
-template <int D>
+template <int D, int G>
 __global__ void __launch_bounds__(256) paged_prefill_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ cu_q, const int* __restrict__ context_lens,
@@ -35,18 +41,18 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   __shared__ __attribute__((aligned(16))) char klds[KT * D * 2];
   __shared__ __attribute__((aligned(16))) char vlds[KT * D * 2];
 
-  const int s = blockIdx.z, h = blockIdx.y, tile = blockIdx.x;
+  constexpr int QT = 64 / G;  // queries per workgroup
+  const int s = blockIdx.z, kvh = blockIdx.y, tile = blockIdx.x;
   const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
-  if (tile * 64 >= qlen) return;
+  if (tile * QT >= qlen) return;
   const int ctx = context_lens[s];
   const int qstart = ctx - qlen;  // absolute position of query 0
-  const int kvh = h / (nq / nkv);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int* bt = block_tables + (size_t)s * max_blocks;
   const size_t kv_stride = (size_t)nkv * D;
 
-  const int last_row = min(tile * 64 + 63, qlen - 1);
+  const int last_row = min(tile * QT + QT - 1, qlen - 1);
   const int kv_end = qstart + last_row + 1;  // keys needed by this workgroup
   const int ntiles = (kv_end + KT - 1) / KT;
 
@@ -68,13 +74,14 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   };
   fetch(0);
 
-  // my query row (B operand columns / softmax rows)
-  const int row = tile * 64 + wid * 16 + li;
+  // my (query, head) row (B operand columns / softmax rows)
+  const int wr = wid * 16 + li;
+  const int row = tile * QT + wr / G, head = kvh * G + wr % G;
   const int row_c = min(row, qlen - 1);  // clamp padding rows to a valid query
   const int qpos = qstart + row_c;
   bf16x8 qf[D / 32];
   {
-    const bf16_t* qp = q + ((size_t)(q0 + row_c) * nq + h) * D;
+    const bf16_t* qp = q + ((size_t)(q0 + row_c) * nq + head) * D;
 #pragma unroll
     for (int kk = 0; kk < D / 32; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(qp + kk * 32 + g * 8);
   }
@@ -196,9 +203,10 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int r = tile * 64 + wid * 16 + g * 4 + i;
+    const int orow = wid * 16 + g * 4 + i;
+    const int r = tile * QT + orow / G, oh = kvh * G + orow % G;
     if (r < qlen) {
-      bf16_t* op = out + ((size_t)(q0 + r) * nq + h) * D + li;
+      bf16_t* op = out + ((size_t)(q0 + r) * nq + oh) * D + li;
 #pragma unroll
       for (int n = 0; n < D / 16; ++n) op[16 * n] = f2bf(o[n][i] * inv_l[i]);
     }
@@ -215,9 +223,24 @@ extern "C" int k8s_paged_prefill_attention(void* out, const void* q, const void*
                                            int block_size, int max_blocks, hipStream_t stream) {
   if (num_seqs <= 0 || max_qlen <= 0) return 0;
   if (D != 128 || nq % nkv != 0) return -1;
-  dim3 grid((max_qlen + 63) / 64, nq, num_seqs);
-  paged_prefill_kernel<128><<<grid, 256, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, (const bf16_t*)k_cache,
-                                                     (const bf16_t*)v_cache, cu_q, context_lens, block_tables,
-                                                     scale * 1.4426950408889634f, nq, nkv, block_size, max_blocks);
+  const int G = nq / nkv;
+  const float sl2 = scale * 1.4426950408889634f;
+#define PF(GG)                                                                                               \
+  {                                                                                                          \
+    dim3 grid((max_qlen + 64 / GG - 1) / (64 / GG), nkv, num_seqs);                                          \
+    paged_prefill_kernel<128, GG><<<grid, 256, 0, stream>>>((bf16_t*)out, (const bf16_t*)q,                 \
+                                                            (const bf16_t*)k_cache, (const bf16_t*)v_cache, \
+                                                            cu_q, context_lens, block_tables, sl2, nq, nkv,  \
+                                                            block_size, max_blocks);                         \
+  }
+  switch (G) {  // query heads per kv head (Llama-3.3-70B: 8; Llama-3-8B: 4)
+    case 1: PF(1) break;
+    case 2: PF(2) break;
+    case 4: PF(4) break;
+    case 8: PF(8) break;
+    case 16: PF(16) break;
+    default: return -1;
+  }
+#undef PF
   return (int)hipGetLastError();
 }

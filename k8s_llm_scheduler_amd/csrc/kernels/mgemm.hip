@@ -80,7 +80,8 @@ struct MgArgs {
 // read longer contiguous runs of every weight row.
 template <int RB>
 __device__ __forceinline__ int mg_swz_rb(int r) {
-  return RB == 128 ? ((r >> 1) & 7) : (r & 15);
+  // 16-byte chunks of 16 consecutive rows read at one column land on 16 distinct bank slots
+  return RB == 64 ? ((r >> 2) & 3) : RB == 128 ? ((r >> 1) & 7) : (r & 15);
 }
 
 template <int BM, int BN, int WM, int WN, int WK, int RB, int S, int EPI, bool FP8>
@@ -90,9 +91,9 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert(FM >= 1 && FN >= 1 && BM % (WM * 16) == 0 && BN % (WN * 16) == 0, "tile / wave split");
   static_assert(EPI != MG_SWIGLU || FN % 2 == 0, "SwiGLU pairs gate and up fragments");
   static_assert(S >= 2 && S <= 8, "ring depth");
-  static_assert(RB == 128 || RB == 256 || RB == 512, "row bytes per k-step");
+  static_assert(RB == 64 || RB == 128 || RB == 256 || RB == 512, "row bytes per k-step");
   constexpr int CPR = RB / 16;                       // 16-byte chunks per staged row
-  constexpr int KS = FP8 ? RB / 32 : RB / 64;        // k32 MFMA steps per k-step
+  constexpr int KS = FP8 ? RB / 32 : RB / 64;        // k32 MFMA steps per k-step (RB = 64: one)
   static_assert(KS % WK == 0, "k32 steps split evenly over WK waves");
   constexpr int WREG = BN * RB, STAGE_B = (BM + BN) * RB;
   static_assert((BN * CPR) % NW == 0 && (BM * CPR) % NW == 0, "chunks per wave");
@@ -116,20 +117,6 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   const long long it0 = (long long)lid * a.total / a.nwg, it1 = (long long)(lid + 1) * a.total / a.nwg;
   const int T = a.T;
 
-  // ---- per-lane DMA geometry (swizzle on the source, lane-linear LDS destination)
-  int wr[WI], wc[WI], xr[XI], xc[XI];
-#pragma unroll
-  for (int i = 0; i < WI; ++i) {
-    const int p = wid * WCH + min(i * 64 + lane, WCH - 1);
-    wr[i] = p / CPR;
-    wc[i] = (p % CPR) ^ mg_swz_rb<RB>(p / CPR);
-  }
-#pragma unroll
-  for (int i = 0; i < XI; ++i) {
-    const int p = wid * XCH + min(i * 64 + lane, XCH - 1);
-    xr[i] = p / CPR;
-    xc[i] = (p % CPR) ^ mg_swz_rb<RB>(p / CPR);
-  }
   // fragment rows of this lane inside the stage images
   int arow[FN];
 #pragma unroll
@@ -153,11 +140,15 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     if (!first_segment) mg_barrier();  // every wave is done with the ring (and the reduction space)
     first_segment = false;
 
-    const uint8_t* wsrc[WI];
-    const uint8_t* xsrc[XI];
+    // per-lane DMA sources as 32-bit offsets from the operand bases (swizzle on the source,
+    // lane-linear LDS destination); the host checks that every operand spans < 4 GiB
+    const uint8_t* wseg = a.W + (long long)kb * RB;
+    const uint8_t* xseg = a.x + (long long)kb * RB;
+    uint32_t woff[WI], xoff[XI];
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
-      const int r = wr[i];
+      const int p = wid * WCH + min(i * 64 + lane, WCH - 1);
+      const int r = p / CPR, c = (p % CPR) ^ mg_swz_rb<RB>(p / CPR);
       int grow;
       if (EPI == MG_SWIGLU) {
         const int f = min(nt * (BN / 2) + (r % (BN / 2)), a.N_out - 1);
@@ -165,21 +156,23 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
       } else {
         grow = min(nt * BN + r, a.N_out - 1);
       }
-      wsrc[i] = a.W + (long long)grow * a.kbytes + (long long)kb * RB + wc[i] * 16;
+      woff[i] = (uint32_t)grow * (uint32_t)a.kbytes + (uint32_t)(c * 16);
     }
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const int grow = min(mt * BM + xr[i], a.M - 1);
-      xsrc[i] = a.x + (long long)grow * a.kbytes + (long long)kb * RB + xc[i] * 16;
+      const int p = wid * XCH + min(i * 64 + lane, XCH - 1);
+      const int r = p / CPR, c = (p % CPR) ^ mg_swz_rb<RB>(p / CPR);
+      xoff[i] = (uint32_t)min(mt * BM + r, a.M - 1) * (uint32_t)a.kbytes + (uint32_t)(c * 16);
     }
 
     auto issue = [&](int t, int stage) {
       char* sb = lds + stage * STAGE_B;
-      const long long off = (long long)t * RB;
+      const uint8_t* wb = wseg + (long long)t * RB;
+      const uint8_t* xb = xseg + (long long)t * RB;
 #pragma unroll
       for (int i = 0; i < WI; ++i) {
         if (WCH % 64 == 0 || i * 64 + lane < WCH)
-          __builtin_amdgcn_global_load_lds(wsrc[i] + off,
+          __builtin_amdgcn_global_load_lds(wb + woff[i],
                                            (__attribute__((address_space(3))) void*)(sb + (wid * WCH + i * 64) * 16),
                                            16, 0, 0);
       }
@@ -187,7 +180,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
       for (int i = 0; i < XI; ++i) {
         if (XCH % 64 == 0 || i * 64 + lane < XCH)
           __builtin_amdgcn_global_load_lds(
-              xsrc[i] + off, (__attribute__((address_space(3))) void*)(sb + WREG + (wid * XCH + i * 64) * 16), 16, 0,
+              xb + xoff[i], (__attribute__((address_space(3))) void*)(sb + WREG + (wid * XCH + i * 64) * 16), 16, 0,
               0);
       }
     };
@@ -414,6 +407,11 @@ constexpr MgCfg kMgCfgs[] = {
     {64, 128, 2, 4, 1, 128, 3},   // 21  8 waves
     {128, 128, 2, 4, 1, 128, 3},  // 22  8 waves
     {128, 64, 2, 2, 2, 256, 3},   // 23  k-shared waves, 8 waves
+    // --- prefill with 32-wide k-steps: the 128 KiB ring holds 4 stages, 3 in flight
+    {256, 256, 2, 4, 1, 64, 4},   // 24  8 waves
+    {256, 128, 2, 2, 1, 64, 5},   // 25
+    {128, 256, 2, 4, 1, 64, 6},   // 26  8 waves
+    {256, 128, 2, 4, 1, 64, 5},   // 27  8 waves
 };
 constexpr int kMgNumCfgs = sizeof(kMgCfgs) / sizeof(kMgCfgs[0]);
 
@@ -513,6 +511,8 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   const MgGeom g = mg_geom(M, N_out, K, epi, fp8, cfg);
   if (nwg > g.total) return -1;
   if (cmax > 1 && (ws == nullptr || tickets == nullptr)) return -3;
+  const long long wrows = epi == MG_SWIGLU ? 2LL * N_out : (long long)N_out;
+  if (wrows * kbytes >= (1LL << 32) || (long long)M * kbytes >= (1LL << 32)) return -5;  // 32-bit DMA offsets
   if (fp8 && (xs == nullptr || wsc == nullptr)) return -3;
   MgArgs a;
   a.out = out;

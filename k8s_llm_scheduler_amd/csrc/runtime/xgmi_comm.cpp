@@ -13,6 +13,9 @@ int k8s_xgmi_allreduce_bf16(void* const* bases, uint32_t* counters, uint32_t* er
 int k8s_xgmi_allreduce_ll_bf16(void* const* bases, uint32_t* counters, uint32_t* err, const void* in, void* out,
                                long long bytes, long long slot_bytes, int rank, int world, int blocks,
                                long long timeout_ticks, const void* residual, hipStream_t s);
+int k8s_xgmi_allreduce_2shot_bf16(void* const* bases, uint32_t* counters, uint32_t* err, const void* in, void* out,
+                                  long long bytes, long long slot_bytes, int rank, int world, int blocks,
+                                  long long timeout_ticks, const void* residual, hipStream_t s);
 int k8s_xgmi_allgather(void* const* bases, uint32_t* counters, uint32_t* err, const void* in, void* out,
                        long long bytes, long long slot_bytes, int rank, int world, int blocks,
                        long long timeout_ticks, hipStream_t s);
@@ -36,7 +39,7 @@ XgmiComm::XgmiComm(int world, int rank, long long slot_bytes, int blocks, double
   if (world < 2 || world > 8 || rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad world/rank");
   if (slot_bytes <= 0 || (slot_bytes & 4095)) throw std::invalid_argument("XgmiComm: slot_bytes must be a multiple of 4096");
   if (blocks < 1 || blocks > k8s_xgmi_max_blocks()) throw std::invalid_argument("XgmiComm: bad block count");
-  region_bytes_ = k8s_xgmi_flag_bytes() + 4LL * world * slot_bytes;  // flagged + LL slot regions
+  region_bytes_ = k8s_xgmi_flag_bytes() + 8LL * world * slot_bytes;  // flagged + LL + two-shot (2 phases)
   if (region_bytes_ > 0x7fffffffLL) throw std::invalid_argument("XgmiComm: region larger than 2 GiB");
   timeout_ticks_ = static_cast<long long>(timeout_s * 100e6);  // s_memrealtime runs at 100 MHz
   ck(hipGetDevice(&device_), "hipGetDevice");
@@ -84,6 +87,12 @@ void XgmiComm::open(const std::vector<std::string>& handles) {
 
 void XgmiComm::all_reduce_bf16(const void* in, void* out, long long bytes, hipStream_t s, const void* residual) {
   if (!opened_) throw std::runtime_error("XgmiComm: not open");
+  if (bytes > slot_bytes_ || (twoshot_min_bytes_ > 0 && bytes >= twoshot_min_bytes_)) {
+    ckrc(k8s_xgmi_allreduce_2shot_bf16(bases_.data(), counters_, counters_ + k8s_xgmi_max_blocks(), in, out, bytes,
+                                       slot_bytes_, rank_, world_, blocks_, timeout_ticks_, residual, s),
+         "xgmi all_reduce (two-shot)");
+    return;
+  }
   if (bytes <= ll_max_bytes_ && 2 * bytes <= slot_bytes_) {
     ckrc(k8s_xgmi_allreduce_ll_bf16(bases_.data(), counters_, counters_ + k8s_xgmi_max_blocks(), in, out, bytes,
                                     slot_bytes_, rank_, world_, blocks_, timeout_ticks_, residual, s),

@@ -37,6 +37,11 @@ class XgmiComm {
   // Messages up to this size use the LL protocol (flag in every 8-byte word); 0 disables it.
   long long ll_max_bytes() const { return ll_max_bytes_; }
   void set_ll_max_bytes(long long b) { ll_max_bytes_ = b; }
+  // Messages of at least this size (and every message above slot_bytes, up to world x slot_bytes) use the
+  // two-shot reduce-scatter + all-gather kernel; 0 = only the ones above slot_bytes.
+  long long twoshot_min_bytes() const { return twoshot_min_bytes_; }
+  void set_twoshot_min_bytes(long long b) { twoshot_min_bytes_ = b; }
+  long long max_allreduce_bytes() const { return (long long)world_ * slot_bytes_; }
 
  private:
   int world_, rank_, blocks_;
@@ -49,6 +54,7 @@ class XgmiComm {
   std::vector<bool> mapped_;    // true where bases_[i] came from hipIpcOpenMemHandle
   bool opened_ = false;
   long long ll_max_bytes_ = 64 * 1024;
+  long long twoshot_min_bytes_ = 256 * 1024;
 };
 
 }  // namespace k8sllm

@@ -431,20 +431,38 @@ def _mg_load_table() -> dict:
                 plans = json.load(f).get("plans", {})
             for k, v in plans.items():
                 mb, n, kk, epi, fp8 = (int(t) for t in k.split(","))
-                _MG_TABLE.setdefault((n, kk, epi, fp8), []).append((mb, int(v[0]), int(v[1])))
+                mg_us, lib_us = (float(v[2]), float(v[3])) if len(v) >= 4 else (0.0, 0.0)
+                _MG_TABLE.setdefault((n, kk, epi, fp8), []).append((mb, int(v[0]), int(v[1]), mg_us, lib_us))
             for lst in _MG_TABLE.values():
                 lst.sort()
     return _MG_TABLE
 
 
-def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
+def _mg_table_row(M: int, N: int, K: int, epi: int, fp8: bool):
     rows = _mg_load_table().get((N, K, epi, int(fp8)))
-    if rows:
-        mb = _mg_bucket(M)
-        pick = next((r for r in rows if r[0] >= mb), rows[-1])
-        if mgemm_valid(pick[1], M, N, K, epi, fp8, pick[2]):
-            return pick[1], pick[2]
+    if not rows:
+        return None
+    mb = _mg_bucket(M)
+    return next((r for r in rows if r[0] >= mb), rows[-1])
+
+
+def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
+    pick = _mg_table_row(M, N, K, epi, fp8)
+    if pick is not None and mgemm_valid(pick[1], M, N, K, epi, fp8, pick[2]):
+        return pick[1], pick[2]
     return mgemm_heuristic(M, N, K, epi, fp8)
+
+
+def mgemm_preferred(M: int, N: int, K: int, epi: int, fp8: bool) -> bool:
+    """K8S_GEMM=auto: the hand-written GEMM unless the tuned table measured the library GEMM more than 3 %
+    faster at this shape (prefill-size row counts, where mgemm's tiles are not yet at the library's
+    MFMA efficiency: profiles/mgemm_vs_hipblaslt_bf16.txt)."""
+    if GEMM_BACKEND == "mgemm":
+        return True
+    if GEMM_BACKEND == "library":
+        return False
+    pick = _mg_table_row(M, N, K, epi, fp8)
+    return pick is None or not pick[4] or pick[3] <= 1.03 * pick[4]
 
 
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
@@ -478,8 +496,8 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
 # GEMMs with more than GEMV_MAX_M rows run the hand-written MFMA GEMM (mgemm.hip).  K8S_GEMM=library routes
 # them to hipBLASLt / rocBLAS through torch instead (A/B comparisons; tools/mgemm_tune.py times both).
 GEMM_BACKEND = os.environ.get("K8S_GEMM", "mgemm")
-if GEMM_BACKEND not in ("mgemm", "library"):
-    raise ValueError(f"K8S_GEMM must be mgemm or library (got {GEMM_BACKEND!r})")
+if GEMM_BACKEND not in ("mgemm", "library", "auto"):
+    raise ValueError(f"K8S_GEMM must be mgemm, library or auto (got {GEMM_BACKEND!r})")
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
@@ -491,7 +509,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
     epi = EPI_F32 if out_dtype == F32 else EPI_BF16
     if x2.shape[0] <= GEMV_MAX_M:
         y = _gemv(x2.contiguous(), w, epi, out_dtype or BF16)
-    elif GEMM_BACKEND == "mgemm" and _mgemm_ok(w.shape[0], x2.shape[1], _is_fp8(w)) and out_dtype in (None, BF16, F32):
+    elif GEMM_BACKEND != "library" and _mgemm_ok(w.shape[0], x2.shape[1], _is_fp8(w)) and out_dtype in (None, BF16, F32) \
+            and mgemm_preferred(x2.shape[0], w.shape[0], x2.shape[1], epi, _is_fp8(w)):
         y = mgemm(x2.contiguous(), w, epi)
     elif _use_skinny(x2.shape[0], w, x2.shape[1]):
         y = _skinny(x2.contiguous(), w, epi, out_dtype or BF16)
@@ -586,7 +605,8 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     x2 = x.reshape(-1, x.shape[-1])
     if x2.shape[0] <= GEMV_MAX_M:
         y = _gemv(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
-    elif GEMM_BACKEND == "mgemm" and _mgemm_ok(w_gate_up.shape[0] // 2, x2.shape[1], _is_fp8(w_gate_up)):
+    elif GEMM_BACKEND != "library" and _mgemm_ok(w_gate_up.shape[0] // 2, x2.shape[1], _is_fp8(w_gate_up)) \
+            and mgemm_preferred(x2.shape[0], w_gate_up.shape[0] // 2, x2.shape[1], EPI_SWIGLU, _is_fp8(w_gate_up)):
         y = mgemm(x2.contiguous(), w_gate_up, EPI_SWIGLU)
     elif _use_skinny(x2.shape[0], w_gate_up, x2.shape[1]):
         y = _skinny(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)

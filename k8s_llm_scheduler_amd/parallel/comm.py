@@ -54,9 +54,15 @@ class TPGroup:
     def global_rank(self) -> int:
         return self.leader + self.rank
 
-    def _xgmi_ok(self, t: torch.Tensor) -> bool:
+    xgmi_max_ar: int = 0            # all-reduces up to this size use xGMI (autotune_comm; 0 = capacity)
+
+    def _xgmi_ok(self, t: torch.Tensor, reduce: bool = False) -> bool:
         n = t.numel() * t.element_size()
-        return self.xgmi is not None and t.is_cuda and n % 16 == 0 and 0 < n <= self.xgmi.slot_bytes
+        if self.xgmi is None or not t.is_cuda or n % 16 or n <= 0:
+            return False
+        if reduce:
+            return n <= (self.xgmi_max_ar or self.xgmi.max_allreduce_bytes)
+        return n <= self.xgmi.slot_bytes
 
     @property
     def enabled(self) -> bool:
@@ -66,7 +72,7 @@ class TPGroup:
         """In-place sum over the TP group; with ``residual`` the result is sum + residual (the xGMI
         kernels fuse the residual add, SURVEY K14 + K2; other transports add it afterwards)."""
         if self.world > 1 and not self.simulate:
-            if t.dtype == torch.bfloat16 and t.is_contiguous() and self._xgmi_ok(t):
+            if t.dtype == torch.bfloat16 and t.is_contiguous() and self._xgmi_ok(t, reduce=True):
                 rp = 0
                 if residual is not None:
                     if residual.dtype != t.dtype or residual.shape != t.shape or not residual.is_contiguous():
@@ -363,23 +369,58 @@ def _graph_time_us(fn, iters: int = 32, reps: int = 5) -> float:
     return best
 
 
-def autotune_comm(tp: TPGroup, nbytes: int = 16384) -> None:
-    """Graph-time the decode all-reduce (B=1 x 8192 bf16) on both paths, max over ranks; keep
-    xGMI only if it is faster.  Results land in ``tp.comm_info`` (bench.py reports them)."""
+def autotune_comm(tp: TPGroup, sizes=(16384, 65536, 262144, 1 << 20, 4 << 20)) -> None:
+    """Graph-time every all-reduce transport at every message size class the engine issues (decode B=1:
+    16 KiB; batched decode: up to 1 MiB at B=64; prefill chunks: MiBs), max over ranks, and set the
+    thresholds: the LL protocol up to the largest size it wins, the two-shot kernel from the smallest
+    size it beats the one-shot kernel, and xGMI at all only up to the largest size where it beats RCCL.
+    Results land in ``tp.comm_info`` (bench.py reports them)."""
     dev = torch.cuda.current_device()
-    x = torch.ones(nbytes // 2, dtype=torch.bfloat16, device=dev)
     xg, rc = tp.xgmi, tp.rccl
-    dist.barrier(group=tp.group)
-    t_x = _graph_time_us(lambda: xg.all_reduce_bf16(x.data_ptr(), x.data_ptr(), nbytes, -1))
-    dist.barrier(group=tp.group)
-    t_r = _graph_time_us(lambda: rc.all_reduce(x.data_ptr(), x.data_ptr(), nbytes // 2, 0, 0, -1))
-    ts = torch.tensor([t_x, t_r], dtype=torch.float64, device=dev)
-    dist.all_reduce(ts, op=dist.ReduceOp.MAX, group=tp.group)
-    t_x, t_r = float(ts[0]), float(ts[1])
+    cap = xg.max_allreduce_bytes
+    sizes = [n for n in sizes if n <= cap]
+    buf = torch.ones(max(sizes) // 2, dtype=torch.bfloat16, device=dev)
+    keep = (xg.ll_max_bytes, xg.twoshot_min_bytes)
+    table = {}
+
+    def timed(fn) -> float:
+        dist.barrier(group=tp.group)
+        us = _graph_time_us(fn)
+        t = torch.tensor([us], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=tp.group)
+        return float(t[0])
+
+    for n in sizes:
+        row = {}
+        variants = []
+        if 2 * n <= xg.slot_bytes:
+            variants.append(("ll", n + 1, 0))              # LL for this size
+        if n <= xg.slot_bytes:
+            variants.append(("oneshot", 0, 0))             # flagged one-shot
+        variants.append(("twoshot", 0, 16))                # two-shot for everything
+        for name, ll, two in variants:
+            xg.ll_max_bytes, xg.twoshot_min_bytes = ll, two
+            row[name] = round(timed(lambda: xg.all_reduce_bf16(buf.data_ptr(), buf.data_ptr(), n, -1)), 2)
+        if rc is not None:
+            row["rccl"] = round(timed(lambda: rc.all_reduce(buf.data_ptr(), buf.data_ptr(), n // 2, 0, 0, -1)), 2)
+        table[n] = row
+    xg.ll_max_bytes, xg.twoshot_min_bytes = keep
     ok = xg.error() == 0
-    tp.comm_info.update({"allreduce_bytes": nbytes, "xgmi_allreduce_us": round(t_x, 2),
-                         "rccl_allreduce_us": round(t_r, 2)})
-    if not _agree(tp, ok) or t_x >= t_r:
+    # thresholds from the measurements
+    ll_max = max([n for n, r in table.items() if "ll" in r and r["ll"] <= min(r.get("oneshot", 1e9), r["twoshot"])],
+                 default=0)
+    two_min = min([n for n, r in table.items() if r["twoshot"] < r.get("oneshot", 1e9)], default=0)
+    best = {n: min(v for k, v in r.items() if k != "rccl") for n, r in table.items()}
+    xgmi_max = max([n for n in table if "rccl" not in table[n] or best[n] < table[n]["rccl"]], default=0)
+    if xgmi_max == max(sizes):
+        xgmi_max = cap
+    xg.ll_max_bytes = ll_max
+    xg.twoshot_min_bytes = two_min if two_min else cap + 16   # never, unless above the one-shot capacity
+    tp.xgmi_max_ar = xgmi_max
+    tp.comm_info.update({"allreduce_us": {str(k): v for k, v in table.items()}, "ll_max_bytes": ll_max,
+                         "twoshot_min_bytes": two_min, "xgmi_max_bytes": xgmi_max,
+                         "xgmi_allreduce_us": best.get(16384), "rccl_allreduce_us": table.get(16384, {}).get("rccl")})
+    if not _agree(tp, ok) or xgmi_max == 0:
         tp.xgmi = None
-    log.info(f" TP all-reduce {nbytes} B: xGMI one-shot {t_x:.1f} us, RCCL {t_r:.1f} us -> "
-             f"{'xGMI' if tp.xgmi is not None else 'RCCL'}")
+    log.info(f" TP all-reduce transports (us): {table} -> LL <= {ll_max} B, two-shot >= {two_min} B, "
+             f"xGMI <= {xgmi_max} B, RCCL above")

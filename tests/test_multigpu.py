@@ -38,15 +38,15 @@ def _check_collectives(tp, res):
             xg.ll_max_bytes = ll
             for seed, n in enumerate([8, 520, 8192, 32768, xg.slot_bytes // 2]):
                 x = _data(tp.rank, n, seed).cuda()
-                want = sum(_data(r, n, seed).float() for r in range(world)).to(torch.bfloat16)
+                want32 = sum(_data(r, n, seed).float() for r in range(world))   # fixed rank order, fp32
                 tp.all_reduce_(x)
                 torch.cuda.synchronize()
-                assert torch.equal(x.cpu(), want), f"xgmi {path} all_reduce n={n}"
+                assert torch.equal(x.cpu(), want32.to(torch.bfloat16)), f"xgmi {path} all_reduce n={n}"
                 r = _data(99, n, seed).cuda()
                 x = _data(tp.rank, n, seed).cuda()
                 tp.all_reduce_(x, residual=r)
                 torch.cuda.synchronize()
-                assert torch.equal(x.cpu(), (want.float() + r.cpu().float()).to(torch.bfloat16)), \
+                assert torch.equal(x.cpu(), (want32 + r.cpu().float()).to(torch.bfloat16)), \
                     f"xgmi {path} all_reduce+residual n={n}"
             xg.ll_max_bytes = keep
         for n in (4, 4096, 2048 * 4):

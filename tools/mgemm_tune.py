@@ -91,7 +91,9 @@ def lib_fn(x, Ws, epi, fp8):
     def f(i):
         w = Ws[i]
         if fp8:
-            y = ops._fp8_gemm(x, w, ops.F32 if epi == ops.EPI_F32 else None)
+            y = ops._fp8_gemm(x, w)
+            if epi == ops.EPI_F32:
+                y = y.float()
         else:
             y = ops._lib_linear(x, w)
             if epi == ops.EPI_F32:
@@ -146,7 +148,7 @@ def main() -> int:
                 hc = ops.mgemm_heuristic(M, N, K, epi, a.fp8)
                 h_us = time_graph(lambda i: ops.mgemm(x, Ws[i], epi, cfg=hc[0], grid=hc[1]), copies)
                 us, (c, ks) = best
-                plans[f"{ops._mg_bucket(M)},{N},{K},{epi},{int(a.fp8)}"] = [c, ks]
+                plans[f"{ops._mg_bucket(M)},{N},{K},{epi},{int(a.fp8)}"] = [c, ks, round(us, 2), round(lib_us, 2)]
                 row = dict(tp=tp, proj=name, M=M, N=N, K=K, epi=epi, fp8=a.fp8, lib_us=round(lib_us, 2),
                            mgemm_us=round(us, 2), cfg=c, grid=ks, heur_us=round(h_us, 2),
                            speedup=round(lib_us / us, 3), tbps=round(wbytes / us / 1e6, 2))
@@ -156,22 +158,28 @@ def main() -> int:
                 del x
             del Ws
             torch.cuda.empty_cache()
+            if a.write:
+                write_table(plans)
     n_win = sum(r["speedup"] >= 1.0 for r in rows)
     print(f"# mgemm >= library on {n_win}/{len(rows)} shapes; tuning took {time.time() - t_start:.0f}s", flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:
             json.dump(rows, f, indent=1)
     if a.write:
-        path = ops.MG_TABLE_PATH
-        table = {"arch": "gfx950", "plans": {}}
-        if os.path.isfile(path):
-            with open(path) as f:
-                table = json.load(f)
-        table["plans"].update(plans)
-        with open(path, "w") as f:
-            json.dump(table, f, indent=0, sort_keys=True)
-        print(f"# wrote {len(plans)} plans to {path}")
+        write_table(plans)
+        print(f"# wrote {len(plans)} plans to {ops.MG_TABLE_PATH}")
     return 0
+
+
+def write_table(plans) -> None:
+    path = ops.MG_TABLE_PATH
+    table = {"arch": "gfx950", "plans": {}}
+    if os.path.isfile(path):
+        with open(path) as f:
+            table = json.load(f)
+    table["plans"].update(plans)
+    with open(path, "w") as f:
+        json.dump(table, f, indent=0, sort_keys=True)
 
 
 if __name__ == "__main__":
