@@ -124,6 +124,8 @@ class CompatSection:
     watch_all_event_types: bool = False          # scheduler.py:664-681 (False: skip DELETED, dedupe)
     snapshot_mode: str = "informer"              # "direct" = N+1 REST calls (scheduler.py:124-147)
     prompt_layout: str = "reference"             # "cluster_first": node block before the pod block (prefix sharing)
+    yaml_logging: bool = False                   # False: config.yaml's logging section is ignored, LOG_LEVEL /
+                                                 # LOG_FORMAT env only (scheduler.py:27-28); True: section is live
 
 
 @dataclass
@@ -172,7 +174,9 @@ ENV_OVERRIDES = {
 }
 
 # The reference's LOG_LEVEL/LOG_FORMAT come only from env; config.yaml's logging section is
-# ignored there (scheduler.py:27-28).  Here yaml is honoured but env still wins.
+# ignored there (scheduler.py:27-28).  Here the section is honoured only with compat.yaml_logging: true
+# (this repo's config.yaml sets it), so the reference's own config.yaml does not switch on JSON logs to
+# scheduler.log; env still wins either way.
 
 
 def load_dotenv(path: str | os.PathLike = ".env", environ: Optional[Dict[str, str]] = None) -> Dict[str, str]:
@@ -220,8 +224,10 @@ def _merge_section(obj: Any, values: Mapping[str, Any]) -> None:
 
 def from_dict(data: Mapping[str, Any]) -> Config:
     cfg = Config()
-    for sec in ("scheduler", "llm", "cache", "logging", "metrics", "fallback",
-                "circuit_breaker", "engine", "compat"):
+    for sec in ("compat", "scheduler", "llm", "cache", "logging", "metrics", "fallback",
+                "circuit_breaker", "engine"):
+        if sec == "logging" and not cfg.compat.yaml_logging:
+            continue   # the reference never read it: its config.yaml's json/scheduler.log stay inert
         if isinstance(data.get(sec), Mapping):
             _merge_section(getattr(cfg, sec), data[sec])
     return cfg

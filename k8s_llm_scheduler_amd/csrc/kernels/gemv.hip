@@ -15,8 +15,9 @@
 // Epilogues: BF16 store, FP32 store (logits), SWIGLU: W = [gate; up] (2I rows) and the output is
 // silu(gate_j) * up_j (SURVEY.md K10 fused into K9).
 // FP8 weights (BASELINE config 5): W holds OCP e4m3 bytes with one fp32 scale per row; a 16-byte
-// load carries 16 weights (half the HBM bytes of bf16), decoded with v_cvt_pk_f32_fp8 and
-// multiplied in fp32; the row scale is applied once in the epilogue.
+// load carries 16 weights (half the HBM bytes of bf16); every dword of four e4m3 is converted to two
+// bf16 pairs with v_cvt_scalef32_pk_bf16_fp8 (exact) and fed to v_dot2_f32_bf16 against the packed
+// activations; the row scale is applied once in the epilogue.
 #include <cstdlib>
 
 #include "common.h"

@@ -462,7 +462,9 @@ def mgemm_preferred(M: int, N: int, K: int, epi: int, fp8: bool) -> bool:
     if GEMM_BACKEND == "library":
         return False
     pick = _mg_table_row(M, N, K, epi, fp8)
-    return pick is None or not pick[4] or pick[3] <= 1.03 * pick[4]
+    if pick is None or not pick[4]:
+        return M <= 128          # untuned shape: mgemm's streaming tiles are safe, its prefill tiles are not
+    return pick[3] <= 1.03 * pick[4]
 
 
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
@@ -493,9 +495,10 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
     return out
 
 
-# GEMMs with more than GEMV_MAX_M rows run the hand-written MFMA GEMM (mgemm.hip).  K8S_GEMM=library routes
-# them to hipBLASLt / rocBLAS through torch instead (A/B comparisons; tools/mgemm_tune.py times both).
-GEMM_BACKEND = os.environ.get("K8S_GEMM", "mgemm")
+# GEMMs with more than GEMV_MAX_M rows: K8S_GEMM=mgemm runs the hand-written MFMA GEMM (mgemm.hip) for every
+# shape, =library hipBLASLt / rocBLAS through torch, =auto (default) mgemm unless the tuned table measured the
+# library more than 3 % faster at that shape (today: prefill-size row counts; batched decode is mgemm).
+GEMM_BACKEND = os.environ.get("K8S_GEMM", "auto")
 if GEMM_BACKEND not in ("mgemm", "library", "auto"):
     raise ValueError(f"K8S_GEMM must be mgemm, library or auto (got {GEMM_BACKEND!r})")
 

@@ -237,3 +237,19 @@ def test_cluster_first_layout_same_lines_shared_prefix():
     assert a[:shared] == b[:shared] and a != b
     with pytest.raises(ValueError):
         PromptEngine(layout="bogus")
+
+
+def test_reference_config_yaml_logging_section_stays_inert(tmp_path):
+    """the reference's own config.yaml (logging.format json, file scheduler.log) must not switch
+    on JSON file logging -- the reference never read that section (scheduler.py:27-28)."""
+    from k8s_llm_scheduler_amd.config import load_config
+
+    ref = tmp_path / "config.yaml"
+    ref.write_text("logging:\n  level: DEBUG\n  format: json\n  file: scheduler.log\n")
+    cfg = load_config(ref, environ={})
+    assert (cfg.logging.level, cfg.logging.format, cfg.logging.file) == ("INFO", "text", None)
+    ours = tmp_path / "ours.yaml"
+    ours.write_text("compat:\n  yaml_logging: true\nlogging:\n  format: json\n  file: s.log\n")
+    cfg = load_config(ours, environ={})
+    assert (cfg.logging.format, cfg.logging.file) == ("json", "s.log")
+    assert load_config(ours, environ={"LOG_FORMAT": "text"}).logging.format == "text"

@@ -75,8 +75,11 @@ def test_engine_gpu_generate_and_graph():
     assert eager.token_ids == single[0].token_ids
 
 
-def test_batched_decode_matches_cpu_reference(models):
-    """B = 24 > 8: the batched path (MFMA skinny GEMMs + fused RoPE/KV/attention) vs the CPU model."""
+@pytest.mark.parametrize("gemm", ["mgemm", "library"])
+def test_batched_decode_matches_cpu_reference(models, gemm, monkeypatch):
+    """B = 24 > 8: the batched path (projections on the hand-written MFMA GEMM mgemm.hip -- or, as the A/B
+    control, the library GEMM -- + fused RoPE/KV/attention) vs the CPU model."""
+    monkeypatch.setattr(ops, "GEMM_BACKEND", gemm)
     g, c = models
     B, bs, per = 24, 16, 24
     lens = [5 + 13 * i for i in range(B)]
