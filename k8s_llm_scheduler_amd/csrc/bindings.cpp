@@ -67,7 +67,8 @@ int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* lds_bytes, in
 int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, long long* tiles, int* cmax,
                         long long* ws_elems);
 int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs, const float* wsc,
-              int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax, hipStream_t s);
+              int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax, const void* res, int rms,
+              float eps, hipStream_t s);
 }
 
 namespace {
@@ -209,9 +210,10 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(tiles, cmax, ws);
   });
   m.def("mgemm", [](uintptr_t out, uintptr_t ws, uintptr_t tickets, uintptr_t x, uintptr_t W, uintptr_t xs,
-                    uintptr_t wsc, int M, int N, int K, int epi, int fp8, int cfg, int nwg, int cmax, int64_t s) {
+                    uintptr_t wsc, int M, int N, int K, int epi, int fp8, int cfg, int nwg, int cmax, uintptr_t res,
+                    int rms, float eps, int64_t s) {
     check(k8s_mgemm(P(out), P<float>(ws), P<unsigned>(tickets), P(x), P(W), P<float>(xs), P<float>(wsc), M, N, K,
-                    epi, fp8, cfg, nwg, cmax, S(s)),
+                    epi, fp8, cfg, nwg, cmax, P(res), rms, eps, S(s)),
           "mgemm");
   });
 

@@ -72,6 +72,9 @@ struct MgArgs {
   int M, N_out, half_rows;
   int m_tiles, T;        // T: 128-byte k-steps over the whole K
   int nwg, cmax;         // workgroups; most workgroups sharing one tile
+  const bf16_t* res;     // optional residual (bf16 [M][N_out], may alias out): out = acc + res  (bf16 epilogue)
+  int rms;               // 1: RMSNorm prologue -- out scaled by 1 / rms(x row) (the gamma is folded into W)
+  float eps;
 };
 
 // Wave layout: WM x WN waves own (BM / WM) x (BN / WN) output sub-tiles; WK waves share each
@@ -102,8 +105,9 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert((S - 2) * LPS <= 63, "vmcnt range");
   static_assert(WK == 1 || (WK - 1) * FN * FM * 64 * 16 * WM * WN <= S * STAGE_B, "LDS reduction space");
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the launch stub (its lambdas use device builtins)
-  __shared__ __attribute__((aligned(16))) char lds[S * STAGE_B + 16];
+  __shared__ __attribute__((aligned(16))) char lds[S * STAGE_B + 16 + WK * BM * 4];
   unsigned* flag = reinterpret_cast<unsigned*>(lds + S * STAGE_B);
+  float* rss = reinterpret_cast<float*>(lds + S * STAGE_B + 16);   // [WK][BM] row sums of squares
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wk = wid % WK, wt = wid / WK;           // k-share, output sub-tile
@@ -190,6 +194,10 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     for (int f = 0; f < FN; ++f)
 #pragma unroll
       for (int j = 0; j < FM; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float ss[FM];   // RMS prologue: this lane's share of sum(x^2) of its fragment rows
+#pragma unroll
+    for (int j = 0; j < FM; ++j) ss[j] = 0.f;
+    const bool do_rms = !FP8 && a.rms != 0;
 
     auto compute = [&](int stage) {
       const char* wb = lds + stage * STAGE_B;
@@ -213,6 +221,15 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
 #pragma unroll
             for (int j = 0; j < FM; ++j)
               acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], bfr[j], acc[f][j], 0, 0, 0);
+          if (do_rms && wn == 0) {   // the x rows are the same for every wn: count them once
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {   // v_dot2_f32_bf16: two squares per instruction
+                const bf16x2 v2 = {bfr[j][2 * e], bfr[j][2 * e + 1]};
+                ss[j] = __builtin_amdgcn_fdot2_f32_bf16(v2, v2, ss[j], false);
+              }
+          }
         } else {
           const int c = kk * 2 + (g >> 1), hb = (g & 1) * 8;
           long af[FN], bfr[FM];
@@ -275,14 +292,36 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
       }
     }
 
+    // ---- RMS prologue: row sums of squares over this segment's k-steps -> rss[wk][row]
+    if (do_rms) {
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        ss[j] += __shfl_xor(ss[j], 16, WAVE);
+        ss[j] += __shfl_xor(ss[j], 32, WAVE);
+      }
+      if (wn == 0 && g == 0) {
+#pragma unroll
+        for (int j = 0; j < FM; ++j) rss[wk * BM + wm * (BM / WM) + j * 16 + li] = ss[j];
+      }
+      mg_barrier();
+      if (threadIdx.x < BM) {
+        float t = 0.f;
+#pragma unroll
+        for (int k2 = 0; k2 < WK; ++k2) t += rss[k2 * BM + threadIdx.x];
+        rss[threadIdx.x] = t;   // row total of this segment (own thread reads / writes only)
+      }
+    }
+
     // ---- a tile shared by several workgroups: publish this partial tile; the last arriver reduces
     const long long i_first = (long long)tile * T;
     const int w_first = (int)(((i_first + 1) * a.nwg - 1) / a.total);
     const int w_last = (int)(((i_first + T) * a.nwg - 1) / a.total);
     const int nc = w_last - w_first + 1;
+    constexpr int SLAB = BM * BN + BM;   // partial tile + row sums of squares
     if (nc > 1) {
-      float* base = a.ws + (long long)tile * a.cmax * (BM * BN);
-      float* slab = base + (long long)(lid - w_first) * (BM * BN);
+      float* base = a.ws + (long long)tile * a.cmax * SLAB;
+      float* slab = base + (long long)(lid - w_first) * SLAB;
+      if (do_rms && threadIdx.x < BM) slab[BM * BN + threadIdx.x] = rss[threadIdx.x];
       if (wk == 0) {
 #pragma unroll
         for (int f = 0; f < FN; ++f)
@@ -314,7 +353,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
 #pragma unroll
           for (int j = 0; j < FM; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int s2 = 0; s2 < nc; ++s2) {
-          const float* sl = base + (long long)s2 * (BM * BN);
+          const float* sl = base + (long long)s2 * SLAB;
 #pragma unroll
           for (int f = 0; f < FN; ++f)
 #pragma unroll
@@ -324,7 +363,15 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
             }
         }
       }
+      if (do_rms) {
+        if (threadIdx.x < BM) {
+          float t = 0.f;
+          for (int s2 = 0; s2 < nc; ++s2) t += base[(long long)s2 * SLAB + BM * BN + threadIdx.x];
+          rss[threadIdx.x] = t;
+        }
+      }
     }
+    if (do_rms) mg_barrier();   // row totals visible to every wave's epilogue
     if (wk != 0) continue;
 
     // ---- epilogue: lane holds out[m = brow][n = 4 g + i], i < 4, of every fragment pair
@@ -332,7 +379,8 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     for (int j = 0; j < FM; ++j) {
       const int m = mt * BM + wm * (BM / WM) + j * 16 + li;
       if (m >= a.M) continue;
-      const float sx = FP8 ? a.xs[m] : 1.f;
+      float sx = FP8 ? a.xs[m] : 1.f;
+      if (do_rms) sx = rsqrtf(rss[wm * (BM / WM) + j * 16 + li] / (float)(a.kbytes >> 1) + a.eps);
       if constexpr (EPI == MG_SWIGLU) {
 #pragma unroll
         for (int f = 0; f < FN / 2; ++f) {
@@ -360,6 +408,13 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
             *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + (long long)m * a.N_out + n0) =
                 f32x4{v[0], v[1], v[2], v[3]};
           } else {
+            if (a.res != nullptr) {   // residual stream: out = acc + res, one rounding
+              const u32x2 rr = *reinterpret_cast<const u32x2*>(a.res + (long long)m * a.N_out + n0);
+              v[0] += lo_bf(rr[0]);
+              v[1] += hi_bf(rr[0]);
+              v[2] += lo_bf(rr[1]);
+              v[3] += hi_bf(rr[1]);
+            }
             u32x2 o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
             *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.out) + (long long)m * a.N_out + n0) = o;
           }
@@ -494,7 +549,7 @@ extern "C" int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, in
   }
   *tiles = g.tiles;
   *cmax = cm;
-  *ws_elems = cm > 1 ? g.tiles * cm * kMgCfgs[cfg].bm * kMgCfgs[cfg].bn : 0;
+  *ws_elems = cm > 1 ? g.tiles * cm * (kMgCfgs[cfg].bm * kMgCfgs[cfg].bn + kMgCfgs[cfg].bm) : 0;
   return 0;
 }
 
@@ -503,7 +558,7 @@ extern "C" int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, in
 // SwiGLU: W holds 2 * N_out rows ([gate; up]); out has N_out columns.
 extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs,
                          const float* wsc, int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax,
-                         hipStream_t stream) {
+                         const void* res, int rms, float eps, hipStream_t stream) {
   if (cfg < 0 || cfg >= kMgNumCfgs || M <= 0 || N_out <= 0 || K <= 0 || nwg <= 0 || cmax < 1) return -1;
   if (N_out % 4 != 0) return -1;
   const long long kbytes = (long long)K * (fp8 ? 1 : 2);
@@ -514,7 +569,12 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   const long long wrows = epi == MG_SWIGLU ? 2LL * N_out : (long long)N_out;
   if (wrows * kbytes >= (1LL << 32) || (long long)M * kbytes >= (1LL << 32)) return -5;  // 32-bit DMA offsets
   if (fp8 && (xs == nullptr || wsc == nullptr)) return -3;
+  if (res != nullptr && epi != MG_BF16) return -6;   // residual epilogue: bf16 output only
+  if (rms && fp8) return -6;                         // fp8: activations are quantized before the GEMM
   MgArgs a;
+  a.res = static_cast<const bf16_t*>(res);
+  a.rms = rms;
+  a.eps = eps;
   a.out = out;
   a.ws = ws;
   a.cnt = tickets;

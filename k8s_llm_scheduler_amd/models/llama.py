@@ -200,6 +200,37 @@ class LlamaModel:
         return self.cfg.num_layers * 2 * block_size * self.nkv * self.D * torch.finfo(self.dtype).bits // 8
 
     # ------------------------------------------------------------------ forward
+    def _layers_folded(self, h: torch.Tensor, attn) -> torch.Tensor:
+        """All decoder layers with the norm gammas folded into the weights (the default).  The residual stream
+        ``r`` feeds the pre-norm projections directly: their RMS statistics are the GEMM's prologue
+        (ops.linear_rms), and the row-parallel projections add their output into ``r`` in the GEMM epilogue
+        (TP=1, ops.linear_residual) or in the all-reduce (TP>1, the xGMI kernels fuse it) -- no RMSNorm or
+        residual-add kernels between the GEMMs.  Returns the final residual stream."""
+        eps = self.cfg.rms_eps
+        r = h.clone()
+        tp1 = self.tp.world == 1 or self.tp.simulate
+        for l, w in enumerate(self.layers):
+            qkv = ops.linear_rms(r, w.wqkv, eps)
+            a = attn(l, qkv)
+            if tp1:
+                r = ops.linear_residual(a, w.wo, r)
+            else:
+                o = ops.linear(a, w.wo)
+                self.tp.all_reduce_(o, residual=r)     # o = r + attention branch
+                r = o
+            g = ops.linear_rms(r, w.wgu, eps, ops.EPI_SWIGLU)
+            if tp1:
+                r = ops.linear_residual(g, w.wdown, r)
+            else:
+                d = ops.linear(g, w.wdown)
+                self.tp.all_reduce_(d, residual=r)     # d = r + MLP branch
+                r = d
+        return r
+
+    def _logits_folded(self, r: torch.Tensor) -> torch.Tensor:
+        logits = ops.linear_rms(r, self.lm_head, self.cfg.rms_eps, ops.EPI_F32)   # final norm folded: [S, Vs]
+        return self.tp.all_gather_shards(logits)                               # [tp, S, Vs]
+
     def _layers(self, h: torch.Tensor, attn) -> tuple:
         """Run all decoder layers.  ``attn(l, qkv) -> [T, nq*D]`` does rope + KV write + attention."""
         c = self.cfg
@@ -238,8 +269,11 @@ class LlamaModel:
                                             self.scale, self.block_size, max_qlen)
             return a.view(T, self.nq * self.D)
 
-        h, res = self._layers(ops.embedding(ids, self.embed), attn)
         li = last_idx.long()
+        if self.norm_folded:
+            r = self._layers_folded(ops.embedding(ids, self.embed), attn)
+            return self._logits_folded(r.index_select(0, li).contiguous())
+        h, res = self._layers(ops.embedding(ids, self.embed), attn)
         return self._logits(h.index_select(0, li).contiguous(), res.index_select(0, li).contiguous())
 
     def forward_decode(self, tokens: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
@@ -261,6 +295,8 @@ class LlamaModel:
                                            self.block_size, max_context)
             return a.view(B, self.nq * self.D)
 
+        if self.norm_folded:
+            return self._logits_folded(self._layers_folded(ops.embedding(tokens, self.embed), attn))
         h, res = self._layers(ops.embedding(tokens, self.embed), attn)
         return self._logits(h, res)
 

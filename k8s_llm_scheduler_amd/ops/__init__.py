@@ -468,9 +468,13 @@ def mgemm_preferred(M: int, N: int, K: int, epi: int, fp8: bool) -> bool:
 
 
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
-          grid: Optional[int] = None) -> torch.Tensor:
+          grid: Optional[int] = None, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
+          out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Hand-written MFMA GEMM (mgemm.hip): epi(x[M, K] @ w[N, K].T) for M > 8 rows.  ``w``: bf16 or
-    Fp8Weight (activations are then quantized per token by quantize_act_fp8).  SwiGLU: w = [Wg; Wu]."""
+    Fp8Weight (activations are then quantized per token by quantize_act_fp8).  SwiGLU: w = [Wg; Wu].
+    ``rms_eps``: RMSNorm prologue -- the result is scaled by 1/rms(x row) (the norm gamma must be folded into
+    ``w``), so the un-normalised residual stream feeds the GEMM directly.  ``res``: residual epilogue
+    (bf16 output only) -- out = x @ w.T + res, one rounding; ``out`` may be ``res`` (in place)."""
     M, K = x.shape
     fp8 = _is_fp8(w)
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
@@ -481,18 +485,68 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
         raise ValueError(f"mgemm: cfg {cfg} / grid {grid} invalid for M={M} N={N} K={K} epi={epi}")
     nwg = mgemm_nwg(cfg, M, N, K, epi, fp8, grid)
     tiles, cmax, n_ws = _mg_plan_info(M, N, K, epi, fp8, cfg, nwg)
-    out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
+    if fp8 and rms_eps is not None:
+        raise ValueError("mgemm: the RMS prologue needs bf16 activations")
+    if res is not None and (epi != EPI_BF16 or res.shape != (M, N)):
+        raise ValueError("mgemm: residual epilogue needs a bf16 [M, N] residual and the bf16 epilogue")
+    if out is None:
+        out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
     ws = torch.empty(n_ws, dtype=F32, device=x.device) if n_ws > 0 else None
     tk = _zeroed_scratch(x.device, "mgemm", 4 * tiles, 64 * 1024) if cmax > 1 else 0
+    rp = _chk(res, BF16, "res") if res is not None else 0
+    rms, eps = (1, float(rms_eps)) if rms_eps is not None else (0, 0.0)
     if fp8:
         xq, sx = quantize_act_fp8(x.contiguous())
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, xq.data_ptr(), w.q.data_ptr(),
-                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, nwg, cmax, -1)
+                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, nwg, cmax, rp, 0, 0.0, -1)
     else:
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"),
-                       _chk(w, BF16, "w"), 0, 0, M, N, K, epi, 0, cfg, nwg, cmax, -1)
+                       _chk(w, BF16, "w"), 0, 0, M, N, K, epi, 0, cfg, nwg, cmax, rp, rms, eps, -1)
     del ws
     return out
+
+
+def _mgemm_route(M: int, w, K: int, epi: int) -> bool:
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    return GEMM_BACKEND != "library" and _mgemm_ok(N, K, _is_fp8(w)) and mgemm_preferred(M, N, K, epi, _is_fp8(w))
+
+
+def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Tensor:
+    """epi(rmsnorm(r) @ w.T) for M > 8 rows with the norm gamma folded into ``w`` (LlamaModel folds it at
+    load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
+    copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM."""
+    M, K = r.shape
+    if _gpu(r) and M > GEMV_MAX_M and not _is_fp8(w) and _mgemm_route(M, w, K, epi):
+        return mgemm(r.contiguous(), w, epi, rms_eps=eps)
+    ones = _ones(K, r.device)
+    x = rmsnorm(r, ones, eps)
+    if epi == EPI_SWIGLU:
+        return linear_swiglu(x, w)
+    return linear(x, w, F32 if epi == EPI_F32 else None)
+
+
+def linear_residual(x: torch.Tensor, w, res: torch.Tensor) -> torch.Tensor:
+    """res + x @ w.T (bf16), written into ``res`` (the residual stream).  mgemm route: the add is the GEMM's
+    epilogue; otherwise GEMM + add."""
+    M, K = x.shape
+    if _gpu(x) and M > GEMV_MAX_M and _mgemm_route(M, w, K, EPI_BF16):
+        return mgemm(x.contiguous(), w, EPI_BF16, res=res, out=res)
+    y = linear(x, w)
+    if y.is_cuda:
+        res.add_(y)
+    else:
+        res.copy_((res.float() + y.float()).to(res.dtype))
+    return res
+
+
+_ONES: dict = {}
+
+
+def _ones(K: int, dev) -> torch.Tensor:
+    key = (K, str(dev))
+    if key not in _ONES:
+        _ONES[key] = torch.ones(K, dtype=BF16, device=dev)
+    return _ONES[key]
 
 
 # GEMMs with more than GEMV_MAX_M rows: K8S_GEMM=mgemm runs the hand-written MFMA GEMM (mgemm.hip) for every

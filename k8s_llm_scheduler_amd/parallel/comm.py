@@ -245,8 +245,8 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backe
             tp.rccl = make_rccl_comm(tp)
         if comm in ("auto", "xgmi"):
             tp.xgmi = make_xgmi_comm(tp)
-        if comm == "auto" and tp.xgmi is not None and tp.rccl is not None:
-            autotune_comm(tp)
+        if tp.xgmi is not None and os.environ.get("K8S_COMM_AUTOTUNE", "1") == "1":
+            autotune_comm(tp)   # thresholds between the xGMI protocols (and RCCL, when present)
         tp.comm_info["selected"] = "xgmi+rccl" if tp.xgmi is not None and tp.rccl is not None else \
             ("xgmi" if tp.xgmi is not None else ("rccl" if tp.rccl is not None else backend))
     return tp

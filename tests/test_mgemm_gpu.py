@@ -104,3 +104,37 @@ def test_split_k_tickets_reset_between_launches():
         torch.cuda.synchronize()
         assert torch.equal(yg, exp)
     _check(exp, x, w, ops.EPI_F32, tol=1e-3)
+
+
+@pytest.mark.parametrize("epi", [ops.EPI_BF16, ops.EPI_SWIGLU, ops.EPI_F32])
+def test_rms_prologue_and_residual_epilogue(epi):
+    """ops.linear_rms / linear_residual on the mgemm route: the RMS statistics of the un-normalised rows are
+    the GEMM's prologue (1/rms in the epilogue, gamma folded into W) and the residual add is its epilogue
+    (in place on the residual stream) -- every tile configuration, one-workgroup-per-tile, split-K and
+    stream-K grids (the row sums of squares travel with the partial tiles)."""
+    torch.manual_seed(1)
+    K, N, eps = 1024, 200, 1e-5
+    rows = 2 * N if epi == ops.EPI_SWIGLU else N
+    w = _weights(rows, K, False, 5)
+    for cfg, (bm, bn, _t, _l, sw, rb) in enumerate(ops.mgemm_configs()):
+        for M in (13, bm + 7):
+            r = ((torch.rand(M, K, device=DEV) * 2 - 1) * 3).to(torch.bfloat16)
+            rf = r.float().cpu()
+            xn = (rf * torch.rsqrt(rf.pow(2).mean(-1, keepdim=True) + eps))
+            exp = xn @ w.float().cpu().t()
+            if epi == ops.EPI_SWIGLU:
+                exp = torch.nn.functional.silu(exp[:, :N]) * exp[:, N:]
+            for grid in (1, 4, -7):
+                if not ops.mgemm_valid(cfg, M, N, K, epi, False, grid):
+                    continue
+                y = ops.mgemm(r, w, epi, cfg=cfg, grid=grid, rms_eps=eps).float().cpu()
+                err = (y - exp).abs().max().item()
+                assert err <= 2e-2 * exp.abs().max().item(), f"rms cfg {cfg} grid {grid} M {M}: {err}"
+                if epi == ops.EPI_BF16:
+                    x = ((torch.rand(M, K, device=DEV) * 2 - 1)).to(torch.bfloat16)
+                    res = ((torch.rand(M, N, device=DEV) * 2 - 1) * 8).to(torch.bfloat16)
+                    want = (x.float() @ w.float().t() + res.float()).cpu()
+                    out = ops.mgemm(x, w, epi, cfg=cfg, grid=grid, res=res, out=res)   # in place
+                    assert out.data_ptr() == res.data_ptr()
+                    err = (out.float().cpu() - want).abs().max().item()
+                    assert err <= 2e-2 * want.abs().max().item(), f"res cfg {cfg} grid {grid} M {M}: {err}"
