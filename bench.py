@@ -65,7 +65,17 @@ def main() -> int:
                     help="serving mode: pods arrive as a Poisson process at this rate (pods/s) into the scheduler "
                          "in continuous mode on an in-memory apiserver; reports detect->bind latency "
                          "(--steps pods after --warmup pods; single rank)")
+    ap.add_argument("--top-p", type=float, default=1.0,
+                    help="nucleus sampling (the reference sends no top_p: provider default 1.0); < 1 captures the "
+                         "decode graphs with the top-p passes")
+    ap.add_argument("--verbose", action="store_true", help="engine INFO logs (init, autotune, graph capture)")
     args = ap.parse_args()
+    t_start = time.perf_counter()
+
+    def progress(msg: str) -> None:
+        # stage lines on stderr (stdout carries only the JSON line): shows where a slow start is spent
+        print(f"[bench rank {os.environ.get('RANK', '0')} +{time.perf_counter() - t_start:.1f}s] {msg}",
+              file=sys.stderr, flush=True)
 
     import torch
     import torch.distributed as dist
@@ -78,6 +88,9 @@ def main() -> int:
     from k8s_llm_scheduler_amd.parallel import init_from_env
 
     logging.basicConfig(level=logging.WARNING, format="%(asctime)s %(levelname)s %(message)s")
+    if args.verbose:
+        logging.getLogger("k8s_llm_scheduler_amd").setLevel(logging.INFO)
+    progress("imports done")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
@@ -91,6 +104,7 @@ def main() -> int:
         tp = TPGroup(0, args.simulate_tp, None, "none", simulate=True)
     rank = tp.global_rank
     dp = tp.replicas
+    progress(f"process group ready (tp {tp.world}, comm {tp.comm_info.get('selected', '-')})")
 
     t_init = time.perf_counter()
     bs = 16
@@ -100,14 +114,17 @@ def main() -> int:
                        max_model_len=args.max_model_len, cuda_graphs=not args.no_graphs,
                        prefix_caching=not args.no_prefix_cache, capture=False, decode_chunk=8,
                        weight_dtype=args.dtype)
+    progress("engine built")
     if eng.use_graphs:
-        eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= max(1, args.batch)] or [1])
+        eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= max(1, args.batch)] or [1],
+                           nucleus=args.top_p < 1)
     if on_gpu:
         torch.cuda.synchronize()
     init_s = time.perf_counter() - t_init
+    progress(f"graphs captured, init {init_s:.1f}s")
 
     backend = LocalEngineBackend(eng, ignore_eos=True)
-    svc = DecisionService(backend, max_retries=3, max_tokens=args.gen_tokens, temperature=0.3, top_p=1.0,
+    svc = DecisionService(backend, max_retries=3, max_tokens=args.gen_tokens, temperature=0.3, top_p=args.top_p,
                           timeout=None, cache=None, breaker=CircuitBreaker())
     pe = PromptEngine(layout=args.prompt_layout)
     rng = random.Random(1234)
@@ -142,6 +159,7 @@ def main() -> int:
 
     for _ in range(args.warmup):
         svc.decide_many(make_items())
+    progress("warmup done")
     eng.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in eng.stats.items()})
     lat = []
     barrier()
@@ -187,6 +205,8 @@ def main() -> int:
             "cuda_graphs": eng.use_graphs,
             "prefix_cache": not args.no_prefix_cache,
             "prompt_layout": args.prompt_layout,
+            "temperature": 0.3,
+            "top_p": args.top_p,
         },
         "p50_decision_latency_ms": round(1000 * statistics.median(lat), 2),
         "p99_decision_latency_ms": round(1000 * sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))], 2),
@@ -278,6 +298,12 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
         "fallback_decisions": st["fallback_decisions"],
         "wall_s": round(time.perf_counter() - t0, 2),
         "init_s": round(init_s, 1),
+        "engine_decode_steps": eng.stats["decode_steps"],
+        "engine_graph_replays": eng.stats["graph_replays"],
+        "engine_prefill_graph_replays": eng.stats.get("prefill_graph_replays", 0),
+        "mean_decode_batch": round(eng.stats["decode_tokens"] / max(1, eng.stats["decode_steps"]), 2),
+        "engine_prefill_s": round(eng.stats["prefill_time"], 2),
+        "engine_decode_s": round(eng.stats["decode_time"], 2),
     }
     line = json.dumps(res)
     print(line, flush=True)

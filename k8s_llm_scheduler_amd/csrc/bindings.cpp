@@ -56,8 +56,9 @@ int k8s_decode_attention_split(void* out, void* part, uint32_t* counters, const 
                                hipStream_t s);
 int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
                const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist,
-               int hist_stride, int* steps, void* scratch, hipStream_t s);
+               int hist_stride, int* steps, void* scratch, void* nuc_scratch, hipStream_t s);
 long long k8s_sample_scratch_bytes(int B);
+long long k8s_sample_nucleus_bytes(int B, int shards);
 int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab, hipStream_t s);
 int k8s_silu_mul(void* out, const void* gu, int T, int I, hipStream_t s);
 int k8s_hash_init(void* out, int rows, int cols, long long gcols, long long row0, long long col0, uint32_t seed,
@@ -175,13 +176,14 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("sample", [](uintptr_t tokens, uintptr_t logits, int B, int Vs, int shards, uintptr_t temp, uintptr_t top_p,
                      uintptr_t seeds, uintptr_t counter, uintptr_t ctx_inc, uintptr_t hist, int hist_stride,
-                     uintptr_t steps, uintptr_t scratch, int64_t s) {
+                     uintptr_t steps, uintptr_t scratch, uintptr_t nuc_scratch, int64_t s) {
     check(k8s_sample(P<int>(tokens), P<float>(logits), B, Vs, shards, P<float>(temp), P<float>(top_p),
                      P<uint32_t>(seeds), P<int>(counter), P<int>(ctx_inc), P<int>(hist), hist_stride, P<int>(steps),
-                     P(scratch), S(s)),
+                     P(scratch), P(nuc_scratch), S(s)),
           "sample");
   });
   m.def("sample_scratch_bytes", [](int B) { return k8s_sample_scratch_bytes(B); });
+  m.def("sample_nucleus_bytes", [](int B, int shards) { return k8s_sample_nucleus_bytes(B, shards); });
   m.def("embedding", [](uintptr_t out, uintptr_t ids, uintptr_t table, int T, int H, int vocab, int64_t s) {
     check(k8s_embedding(P(out), P<int>(ids), P(table), T, H, vocab, S(s)), "embedding");
   });

@@ -5,30 +5,59 @@
 // after an all-gather, or a single shard).  Per row b:
 //   temperature <= 0       -> greedy argmax (lowest index wins ties, like torch.argmax)
 //   top_p >= 1             -> Gumbel-max: argmax(l / T + G), G = -log(-log(U)), one pass
-//   0 < top_p < 1          -> nucleus: exact logit threshold by a 4 x 8-bit radix select on
-//                             probability MASS (no sort), then Gumbel-max inside the nucleus.
+//   0 < top_p < 1          -> nucleus, then Gumbel-max inside it.  The nucleus is a threshold on
+//                             f(l) = floor((M - l) / T * 65536 / 28): the smallest f* whose tokens
+//                             {f <= f*} carry >= top_p of the probability mass (2^-40 fixed point,
+//                             integer sums: order-independent, so every TP rank picks the same set).
+//                             One fine bin spans 28/65536 of log-probability (0.04 %), so the set is
+//                             the exact sorted-cumsum nucleus up to ties inside one such bin.
 // U comes from a counter-based hash of (seed[b], counter[b], token) so results do not depend on
 // batch composition or on which rank samples (every TP rank draws the same token).
 // After sampling: tokens[b] = tok; hist[b][steps[b]] = tok; steps[b]++; ctx[b]++ (optional).
 //
 // Work split: the per-token work (a hash and two logs for Gumbel) over a 128k vocabulary is
-// compute-bound on one CU (~70 us), so greedy / Gumbel rows spread the vocabulary over NB
-// workgroups: each reduces its slice to one packed 64-bit key (ord(score) << 32 | ~index, so the
-// max key is the best score with the LOWEST index), folds it into a per-row atomicMax, and the
-// workgroup whose arrival-counter add comes last finalizes the row (agent-scope atomics only:
-// the payload is the atomic itself, the last arriver reads it with an agent-scope load) and
-// re-arms the row's key and counter for the next graph replay.  Nucleus rows (top_p < 1) need a
-// global mass histogram and stay on workgroup 0 of their row with the radix-select path.
+// compute-bound on one CU (~70 us), so every pass spreads the vocabulary over NB workgroups per row
+// (each inside one vocab shard).  Greedy / Gumbel: each workgroup reduces its slice to one packed
+// 64-bit key (ord(score) << 32 | ~index, so the max key is the best score with the LOWEST index),
+// folds it into a per-row atomicMax, and the workgroup whose arrival-counter add comes last
+// finalizes the row (agent-scope atomics only) and re-arms the row's key and counter for the next
+// graph replay.  Nucleus rows first run three more passes over the same grid (launched only when
+// the caller asks for the nucleus path):
+//   1. row max (atomicMax of the ordered key);
+//   2. mass histogram over the 256 coarse bins f >> 8 per workgroup (LDS, one copy per wave), written
+//      with sc1 stores; the last-arriving workgroup sums the NB copies, takes Z and the target mass
+//      floor(Z * top_p), and scans for the coarse bin b* where the cumulative mass crosses it;
+//   3. the same over the 256 fine bins inside b* -> f*.
+// The row state (max key, arrival counters) starts zeroed and the sampling pass's last arriver
+// re-arms it, like the argmax key and counter (no memset node in the replayed graph).
 #include "common.h"
 
 namespace k8sllm {
 
 constexpr int ST = 256;   // threads per workgroup
-constexpr int NB = 32;    // workgroups per row (greedy / Gumbel)
+constexpr int NB = 32;    // workgroups per row (split over the vocab shards)
+constexpr float NUC_FS = 65536.f / 28.f;  // fine-bin scale; exp(-28) * 2^40 < 1: no mass beyond
+constexpr int NUC_NONE = 65536;
+
+struct NucRow {             // one per row; maxkey / cnt0 / cnt1 zero between calls
+  unsigned long long target, above;
+  uint32_t maxkey, bstar, fstar, cnt0, cnt1, pad[7];
+};
+static_assert(sizeof(NucRow) == 64, "NucRow is 64 bytes");
 
 __device__ __forceinline__ uint32_t ord_key(float f) {  // monotone float -> uint32
   const uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_float(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
+}
+__device__ __forceinline__ int nuc_fine(float l, float M, float invT) {
+  const float x = ((M - l) * invT) * NUC_FS;
+  return x < 65536.f ? (int)x : NUC_NONE;  // NaN -> none
+}
+__device__ __forceinline__ unsigned long long nuc_mass(float l, float M, float invT) {
+  return (unsigned long long)(__expf((l - M) * invT) * 1099511627776.0f);
 }
 
 struct ArgMax {
@@ -74,105 +103,165 @@ __device__ __forceinline__ void write_token(int b, int tok, int* __restrict__ to
   if (ctx_inc != nullptr) ctx_inc[b] += 1;
 }
 
-// grid (NB, B); row_key [B] u64 and row_cnt [B] u32 must be zero before the first launch (the
-// last arriver of each row restores them).
+// This workgroup's slice: inside ONE shard (gridDim.x = shards * per_shard), so a token is
+// base[j] with id s * Vs + j and no division per token.
+struct Slice {
+  const float* base;
+  int j0, j1, id0;
+};
+__device__ __forceinline__ Slice slice_of(const float* logits, int b, int B, int Vs, int shards) {
+  const int per_shard = gridDim.x / shards;
+  const int s = blockIdx.x / per_shard, q = blockIdx.x - s * per_shard;
+  const int per = (Vs + per_shard - 1) / per_shard;
+  Slice r;
+  r.base = logits + ((size_t)s * B + b) * Vs;
+  r.j0 = q * per;
+  r.j1 = min(Vs, r.j0 + per);
+  r.id0 = s * Vs;
+  return r;
+}
+
+__device__ __forceinline__ bool nuc_row(int b, const int* ctx_inc, const float* temperature, const float* top_p) {
+  return (ctx_inc == nullptr || ctx_inc[b] > 0) && temperature[b] > 0.f && top_p[b] < 1.f;
+}
+
+// pass 1: row max of the logits (ordered-key atomicMax)
+__global__ void __launch_bounds__(ST) nuc_max_kernel(const float* __restrict__ logits, int B, int Vs, int shards,
+                                                     const float* __restrict__ temperature,
+                                                     const float* __restrict__ top_p, const int* __restrict__ ctx_inc,
+                                                     NucRow* __restrict__ st) {
+  __shared__ float red[ST / 64];
+  const int b = blockIdx.y;
+  if (!nuc_row(b, ctx_inc, temperature, top_p)) return;
+  const Slice sl = slice_of(logits, b, B, Vs, shards);
+  float m = -INFINITY;
+  for (int j = sl.j0 + threadIdx.x; j < sl.j1; j += ST) m = fmaxf(m, sl.base[j]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < ST / 64; ++w) m = fmaxf(m, red[w]);
+    __hip_atomic_fetch_max(&st[b].maxkey, ord_key(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// passes 2 (LEVEL 0: coarse bins f >> 8 over every token) and 3 (LEVEL 1: fine bins f & 255 of the
+// tokens in coarse bin b*).  ws: [B][gridDim.x][256] u64 partial histograms.
+template <int LEVEL>
+__global__ void __launch_bounds__(ST) nuc_hist_kernel(const float* __restrict__ logits, int B, int Vs, int shards,
+                                                      const float* __restrict__ temperature,
+                                                      const float* __restrict__ top_p, const int* __restrict__ ctx_inc,
+                                                      NucRow* __restrict__ st, unsigned long long* __restrict__ ws) {
+  __shared__ unsigned long long h[ST / 64][256];   // one histogram per wave: 4x fewer colliding atomics
+  __shared__ unsigned long long scan[2][256];
+  __shared__ uint32_t sh_prev;
+  __shared__ int sh_sel;
+  const int b = blockIdx.y;
+  if (!nuc_row(b, ctx_inc, temperature, top_p)) return;
+  const int tid = threadIdx.x, wid = tid >> 6;
+  const float invT = 1.f / temperature[b];
+  const float M = key_float(__hip_atomic_load(&st[b].maxkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t bstar = LEVEL == 1 ? __hip_atomic_load(&st[b].bstar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+  for (int w = 0; w < ST / 64; ++w) h[w][tid] = 0ull;
+  __syncthreads();
+  const Slice sl = slice_of(logits, b, B, Vs, shards);
+  for (int j = sl.j0 + tid; j < sl.j1; j += ST) {
+    const float l = sl.base[j];
+    const int f = nuc_fine(l, M, invT);
+    if (f == NUC_NONE) continue;
+    if (LEVEL == 1 && (uint32_t)(f >> 8) != bstar) continue;
+    const unsigned long long m = nuc_mass(l, M, invT);
+    if (m) atomicAdd(&h[wid][LEVEL == 0 ? (f >> 8) : (f & 255)], m);
+  }
+  __syncthreads();
+  unsigned long long mine = 0ull;
+#pragma unroll
+  for (int w = 0; w < ST / 64; ++w) mine += h[w][tid];
+  unsigned long long* row_ws = ws + (size_t)b * gridDim.x * 256;
+  __hip_atomic_store(row_ws + (size_t)blockIdx.x * 256 + tid, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores land before the arrival
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t* cnt = LEVEL == 0 ? &st[b].cnt0 : &st[b].cnt1;
+    sh_prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh_sel = 256;
+  }
+  __syncthreads();
+  if (sh_prev != gridDim.x - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the arrival
+
+  // last arriver: bin totals (thread = bin), inclusive scan, first bin where the target is reached
+  unsigned long long tot = 0ull;
+  for (int w = 0; w < (int)gridDim.x; ++w)
+    tot += __hip_atomic_load(row_ws + (size_t)w * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int cur = 0;
+  scan[0][tid] = tot;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const unsigned long long v = scan[cur][tid] + (tid >= o ? scan[cur][tid - o] : 0ull);
+    scan[cur ^ 1][tid] = v;
+    cur ^= 1;
+    __syncthreads();
+  }
+  const unsigned long long incl = scan[cur][tid];
+  unsigned long long target, base;
+  if (LEVEL == 0) {
+    const unsigned long long Z = scan[cur][255];
+    target = (unsigned long long)((double)Z * (double)top_p[b]);
+    base = 0ull;
+  } else {
+    target = __hip_atomic_load(&st[b].target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base = __hip_atomic_load(&st[b].above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tot != 0ull && base + incl >= target) atomicMin(&sh_sel, tid);
+  __syncthreads();
+  if (tid == (sh_sel == 256 ? 255 : sh_sel)) {
+    if (LEVEL == 0) {
+      __hip_atomic_store(&st[b].target, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&st[b].above, incl - tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&st[b].bstar, (uint32_t)tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&st[b].fstar, (bstar << 8) | (uint32_t)tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// grid (nbx, B); row_key [B] u64 and row_cnt [B] u32 must be zero before the first launch (the
+// last arriver of each row restores them).  nuc: the nucleus passes' row state, or null (top_p ignored).
 __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, const float* __restrict__ logits, int B,
                                                     int Vs, int shards, const float* __restrict__ temperature,
                                                     const float* __restrict__ top_p, const uint32_t* __restrict__ seeds,
                                                     const int* __restrict__ counter, int* __restrict__ ctx_inc,
                                                     int* __restrict__ hist, int hist_stride, int* __restrict__ steps,
                                                     unsigned long long* __restrict__ row_key,
-                                                    uint32_t* __restrict__ row_cnt) {
+                                                    uint32_t* __restrict__ row_cnt, NucRow* __restrict__ nuc) {
   __shared__ float sv[ST / 64];
   __shared__ int si[ST / 64];
-  __shared__ unsigned long long hist_mass[256];
-  __shared__ unsigned long long sh_z;
-  __shared__ uint32_t sh_prefix;
-  __shared__ unsigned long long sh_above;
-  const int b = blockIdx.y, part = blockIdx.x;
+  const int b = blockIdx.y;
   if (ctx_inc != nullptr && ctx_inc[b] <= 0) return;  // padded row
-  const int V = Vs * shards;
   const float T = temperature[b];
-  const float P = top_p[b];
   const uint32_t seed = seeds[b];
   const uint32_t ctr = counter ? (uint32_t)counter[b] : 0u;
-  auto L = [&](int v) -> float {
-    const int s = v / Vs, j = v - s * Vs;
-    return logits[((size_t)s * B + b) * Vs + j];
-  };
-
-  if (T > 0.f && P < 1.f) {  // ---- nucleus: exact mass threshold (radix select), one workgroup
-    if (part != 0) return;
-    const float invT = 1.f / T;
-    ArgMax mx{-INFINITY, 0};
-    for (int v = threadIdx.x; v < V; v += ST) mx = better(mx, ArgMax{L(v), v});
-    mx = block_argmax(mx, sv, si);
-    const float M = mx.v;
-    // Probability mass in 2^-40 fixed point, summed with INTEGER atomics: the histogram, the total
-    // and hence the threshold do not depend on the order the adds land in, so every TP rank (same
-    // logits) picks the same nucleus and the same token.
-    auto mass = [&](float l) -> unsigned long long {
-      return (unsigned long long)(__expf((l - M) * invT) * 1099511627776.0f);
-    };
-    if (threadIdx.x == 0) sh_z = 0ull;
-    __syncthreads();
-    unsigned long long zl = 0ull;
-    for (int v = threadIdx.x; v < V; v += ST) zl += mass(L(v));
-    atomicAdd(&sh_z, zl);
-    __syncthreads();
-    const unsigned long long target = (unsigned long long)((double)sh_z * (double)P);
-    uint32_t prefix = 0;
-    unsigned long long above = 0ull;  // mass of tokens strictly above the current prefix bucket
-    for (int round = 0; round < 4; ++round) {
-      const int shift = 24 - 8 * round;
-      for (int i = threadIdx.x; i < 256; i += ST) hist_mass[i] = 0ull;
-      __syncthreads();
-      for (int v = threadIdx.x; v < V; v += ST) {
-        const float l = L(v);
-        const uint32_t k = ord_key(l);
-        const bool match = round == 0 || (k >> (shift + 8)) == (prefix >> (shift + 8));
-        if (match) atomicAdd(&hist_mass[(k >> shift) & 255], mass(l));
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        unsigned long long cum = above;
-        int bsel = 0;
-        for (int bk = 255; bk >= 0; --bk) {
-          if (cum + hist_mass[bk] >= target || bk == 0) { bsel = bk; break; }
-          cum += hist_mass[bk];
-        }
-        sh_prefix = prefix | ((uint32_t)bsel << shift);
-        sh_above = cum;
-      }
-      __syncthreads();
-      prefix = sh_prefix;
-      above = sh_above;
-      __syncthreads();
-    }
-    const uint32_t kthr = prefix;  // include tokens whose ord_key >= kthr
-    ArgMax best{-INFINITY, 0x7fffffff};
-    for (int v = threadIdx.x; v < V; v += ST) {
-      const float l = L(v);
-      if (ord_key(l) < kthr) continue;
-      const float u = u01(hash3(seed, ctr, (uint32_t)v));
-      best = better(best, ArgMax{l * invT - __logf(-__logf(u)), v});
-    }
-    best = block_argmax(best, sv, si);
-    if (threadIdx.x == 0) write_token(b, best.i, tokens, ctx_inc, hist, hist_stride, steps);
-    return;
-  }
-
-  // ---- greedy / Gumbel-max over this workgroup's vocabulary slice
-  const int per = (V + gridDim.x - 1) / gridDim.x;
-  const int v0 = part * per, v1 = min(V, v0 + per);
+  const Slice sl = slice_of(logits, b, B, Vs, shards);
   ArgMax best{-INFINITY, 0x7fffffff};
   if (T <= 0.f) {
-    for (int v = v0 + threadIdx.x; v < v1; v += ST) best = better(best, ArgMax{L(v), v});
+    for (int j = sl.j0 + threadIdx.x; j < sl.j1; j += ST) best = better(best, ArgMax{sl.base[j], sl.id0 + j});
   } else {
     const float invT = 1.f / T;
-    for (int v = v0 + threadIdx.x; v < v1; v += ST) {
+    const bool nucleus = nuc != nullptr && top_p[b] < 1.f;
+    float M = 0.f;
+    int fstar = NUC_NONE;
+    if (nucleus) {
+      M = key_float(__hip_atomic_load(&nuc[b].maxkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      fstar = (int)__hip_atomic_load(&nuc[b].fstar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int j = sl.j0 + threadIdx.x; j < sl.j1; j += ST) {
+      const float l = sl.base[j];
+      if (nucleus && nuc_fine(l, M, invT) > fstar) continue;
+      const int v = sl.id0 + j;
       const float u = u01(hash3(seed, ctr, (uint32_t)v));
-      best = better(best, ArgMax{L(v) * invT - __logf(-__logf(u)), v});
+      best = better(best, ArgMax{l * invT - __logf(-__logf(u)), v});
     }
   }
   best = block_argmax(best, sv, si);
@@ -186,29 +275,52 @@ __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, co
       const int tok = (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull));
       __hip_atomic_store(&row_key[b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&row_cnt[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nuc != nullptr && T > 0.f && top_p[b] < 1.f) {   // re-arm the nucleus row state (every
+        NucRow* w = nuc + b;                                // other workgroup has read it already)
+        __hip_atomic_store(&w->maxkey, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&w->cnt0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&w->cnt1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       write_token(b, tok, tokens, ctx_inc, hist, hist_stride, steps);
     }
   }
 }
+
+__host__ __device__ inline int grid_x(int shards) { return shards * ((NB + shards - 1) / shards); }
 
 }  // namespace k8sllm
 
 using namespace k8sllm;
 
 // row_key [B] u64 + row_cnt [B] u32: zero-initialised scratch owned by the caller (one per
-// concurrently captured sampler), restored to zero by every launch.
+// concurrently captured sampler), restored to zero by every launch.  nuc_scratch (or null: top_p
+// ignored): k8s_sample_nucleus_bytes(B, shards) bytes, zero before the first call and left zero.
 extern "C" int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
                           const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist,
-                          int hist_stride, int* steps, void* scratch, hipStream_t stream) {
+                          int hist_stride, int* steps, void* scratch, void* nuc_scratch, hipStream_t stream) {
   if (B <= 0) return 0;
   if (hist != nullptr && steps == nullptr) return -1;
   if (scratch == nullptr) return -3;
+  if (shards < 1 || Vs < 1) return -2;
   auto* key = static_cast<unsigned long long*>(scratch);
   auto* cnt = reinterpret_cast<uint32_t*>(key + B);
-  dim3 grid(NB, B);
+  const dim3 grid(grid_x(shards), B);
+  NucRow* st = nullptr;
+  if (nuc_scratch != nullptr) {
+    st = static_cast<NucRow*>(nuc_scratch);
+    auto* ws = reinterpret_cast<unsigned long long*>(st + B);
+    nuc_max_kernel<<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, st);
+    nuc_hist_kernel<0><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, st, ws);
+    nuc_hist_kernel<1><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, st, ws);
+  }
   sample_kernel<<<grid, ST, 0, stream>>>(tokens, logits, B, Vs, shards, temperature, top_p, seeds, counter, ctx_inc,
-                                         hist, hist_stride, steps, key, cnt);
+                                         hist, hist_stride, steps, key, cnt, st);
   return (int)hipGetLastError();
 }
 
 extern "C" long long k8s_sample_scratch_bytes(int B) { return (long long)B * 12; }
+
+extern "C" long long k8s_sample_nucleus_bytes(int B, int shards) {
+  if (B <= 0 || shards < 1) return 0;
+  return (long long)B * (long long)sizeof(NucRow) + (long long)B * grid_x(shards) * 256 * 8;
+}

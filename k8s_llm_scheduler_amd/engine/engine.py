@@ -94,8 +94,11 @@ class LLMEngine:
                  num_blocks: Optional[int] = None, kv_cache_gb: float = 0.0, kv_cache_fraction: float = 0.85,
                  max_model_len: Optional[int] = None, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
                  prefix_caching: bool = True, decode_chunk: int = 4, seed: int = 0, metrics=None,
-                 control=None):
+                 control=None, capture_nucleus: bool = False):
         self.model = model
+        # also capture decode graphs with the top-p passes (config llm.top_p < 1); otherwise chunks
+        # holding a top_p < 1 request decode eagerly
+        self.capture_nucleus = capture_nucleus
         # Multi-rank serving: rank 0 announces new requests / aborts to the other TP ranks at the
         # start of every step, so all ranks run the identical schedule (None: single rank, or
         # every rank is fed identical requests, as in bench.py).
@@ -144,7 +147,7 @@ class LLMEngine:
         self.requests: Dict[int, Request] = {}
         self.free_slots = list(range(max_batch - 1, -1, -1))
         self.use_graphs = cuda_graphs and self.gpu
-        self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}   # (batch bucket, context class)
+        self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}   # (batch bucket, context class, nucleus)
         self.prefill_graphs: Dict[int, tuple] = {}             # token bucket -> (graph, logits)
         self._graph_pool = None
         self.lock = threading.RLock()
@@ -182,12 +185,16 @@ class LLMEngine:
         attention partition per sequence: no partial buffers, no merge kernel) and the rest."""
         return sorted({min(1024, self.max_model_len), self.max_model_len})
 
-    def _decode_step(self, B: int, max_context: Optional[int] = None) -> None:
+    def _decode_step(self, B: int, max_context: Optional[int] = None, nucleus: bool = False) -> None:
         logits = self.model.forward_decode(self.s_tokens[:B], self.s_ctx[:B], self.s_bt[:B],
                                            max_context or self.max_model_len)
         ops.sample(logits, self.s_temp[:B], self.s_top_p[:B], self.s_seeds[:B], self.s_ctx[:B],
                    shards=logits.shape[0], tokens_out=self.s_tokens[:B], ctx_inc=self.s_ctx[:B],
-                   hist=self.s_hist[:B], steps=self.s_steps[:B])
+                   hist=self.s_hist[:B], steps=self.s_steps[:B], nucleus=nucleus)
+
+    @staticmethod
+    def _wants_nucleus(reqs) -> bool:
+        return any(r.params.temperature > 0 and r.params.top_p < 1 for r in reqs)
 
     def _bucket(self, n: int) -> int:
         for b in BUCKETS:
@@ -195,33 +202,36 @@ class LLMEngine:
                 return b
         return self.max_batch
 
-    def capture_graphs(self, buckets: Optional[Sequence[int]] = None) -> None:
+    def capture_graphs(self, buckets: Optional[Sequence[int]] = None, nucleus: Optional[bool] = None) -> None:
         """Capture one decode-step graph per batch bucket (all slots must be idle: the kernels
-        skip rows with context length 0, so warm-up and capture do not touch any state)."""
+        skip rows with context length 0, so warm-up and capture do not touch any state).
+        ``nucleus`` (default ``self.capture_nucleus``): also capture the variants with the top-p
+        passes; without them a chunk holding a top_p < 1 request decodes eagerly."""
         if not self.use_graphs:
             return
         with trace("engine.capture_graphs"):
-            self._capture_graphs(buckets)
+            self._capture_graphs(buckets, self.capture_nucleus if nucleus is None else nucleus)
 
-    def _capture_graphs(self, buckets: Optional[Sequence[int]]) -> None:
+    def _capture_graphs(self, buckets: Optional[Sequence[int]], nucleus: bool) -> None:
         assert not self.running and not self.prefilling, "capture needs an idle engine"
         buckets = buckets or [b for b in BUCKETS if b <= self.max_batch]
         stream = torch.cuda.Stream(self.device)
         for B in sorted(set(buckets)):
             for mc in self._ctx_classes():
-                if (B, mc) in self.graphs:
-                    continue
-                stream.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(stream):
-                    self._decode_step(B, mc)   # warm-up: allocator + lazy init outside capture
-                torch.cuda.current_stream(self.device).wait_stream(stream)
-                torch.cuda.synchronize(self.device)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=self._graph_pool, stream=stream):
-                    self._decode_step(B, mc)
-                if self._graph_pool is None:
-                    self._graph_pool = g.pool()
-                self.graphs[(B, mc)] = g
+                for nuc in ((False, True) if nucleus else (False,)):
+                    if (B, mc, nuc) in self.graphs:
+                        continue
+                    stream.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(stream):
+                        self._decode_step(B, mc, nuc)   # warm-up: allocator + lazy init outside capture
+                    torch.cuda.current_stream(self.device).wait_stream(stream)
+                    torch.cuda.synchronize(self.device)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=self._graph_pool, stream=stream):
+                        self._decode_step(B, mc, nuc)
+                    if self._graph_pool is None:
+                        self._graph_pool = g.pool()
+                    self.graphs[(B, mc, nuc)] = g
         if self.prefill_graphs_enabled():
             for Tb in PREFILL_GRAPH_BUCKETS:
                 if Tb in self.prefill_graphs:
@@ -461,7 +471,7 @@ class LLMEngine:
             top_p = torch.tensor([r.params.top_p for r in rs], dtype=torch.float32, device=dev)
             seeds = torch.tensor([r.seed for r in rs], dtype=torch.int32, device=dev)
             ctr = torch.tensor([len(r.prompt_ids) for r in rs], dtype=torch.int32, device=dev)
-            toks = ops.sample(sub, temp, top_p, seeds, ctr, shards=sub.shape[0])
+            toks = ops.sample(sub, temp, top_p, seeds, ctr, shards=sub.shape[0], nucleus=self._wants_nucleus(rs))
             slots_t = torch.tensor([r.slot for r in rs], dtype=torch.long, device=dev)
             self.s_tokens[slots_t] = toks
             self.s_ctx[slots_t] = ctr + 1
@@ -495,14 +505,15 @@ class LLMEngine:
         # context length reached by the end of this chunk decides the graph variant
         top = max(len(r.prompt_ids) + max(len(r.output_ids), 1) for r in self.running.values()) + steps
         mc = next(c for c in self._ctx_classes() if top <= c)
+        nuc = self._wants_nucleus(self.running.values())
         t0 = time.perf_counter()
-        graph = self.graphs.get((B, mc)) if self.use_graphs else None
+        graph = self.graphs.get((B, mc, nuc)) if self.use_graphs else None
         for _ in range(steps):
             if graph is not None:
                 graph.replay()
                 self.stats["graph_replays"] += 1
             else:
-                self._decode_step(B, mc)
+                self._decode_step(B, mc, nuc)
         self.stats["decode_steps"] += steps
         tp = self.model.tp
         tp.snapshot_health()             # rides on the sync below

@@ -698,10 +698,14 @@ def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor,
            counter: torch.Tensor, *, shards: int = 1, tokens_out: Optional[torch.Tensor] = None,
            ctx_inc: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None,
-           steps: Optional[torch.Tensor] = None) -> torch.Tensor:
+           steps: Optional[torch.Tensor] = None, nucleus: Optional[bool] = None) -> torch.Tensor:
     """Sample one token per row.  logits: [B, V] or sharded [shards, B, Vs] fp32.  Optionally
     updates decode state in place: tokens_out[b] = tok, ctx_inc[b] += 1, hist[b, steps[b]] = tok,
-    steps[b] += 1 (rows with ctx_inc[b] <= 0 are padding and untouched)."""
+    steps[b] += 1 (rows with ctx_inc[b] <= 0 are padding and untouched).
+
+    ``nucleus``: run the top-p passes (rows with 0 < temperature and top_p < 1).  None = decide
+    from the tensors (a device sync: not inside graph capture); False = top_p is ignored, which is
+    what a graph captured for top_p = 1 requests does (three fewer launches per token)."""
     if logits.dim() == 3:
         S, B, Vs = logits.shape
     else:
@@ -720,14 +724,18 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
         if ctx_inc is not None:
             ctx_inc[:B] += active.to(ctx_inc.dtype)
         return toks
+    if nucleus is None:
+        nucleus = bool(((top_p < 1) & (temperature > 0)).any())
     out = tokens_out if tokens_out is not None else torch.empty(B, dtype=I32, device=logits.device)
+    nuc = _zeroed_scratch(logits.device, "sample_nucleus", native().sample_nucleus_bytes(B, S),
+                          native().sample_nucleus_bytes(64, S)) if nucleus else 0
     native().sample(_chk(out, I32, "tokens"), _chk(logits, F32, "logits"), B, Vs, S,
                     _chk(temperature, F32, "temperature"), _chk(top_p, F32, "top_p"),
                     _chk(seeds, I32, "seeds"), _chk(counter, I32, "counter"),
                     _chk(ctx_inc, I32, "ctx_inc") if ctx_inc is not None else 0,
                     _chk(hist, I32, "hist") if hist is not None else 0,
                     hist.shape[1] if hist is not None else 0,
-                    _chk(steps, I32, "steps") if steps is not None else 0, _sample_scratch(logits.device, B), -1)
+                    _chk(steps, I32, "steps") if steps is not None else 0, _sample_scratch(logits.device, B), nuc, -1)
     return out
 
 

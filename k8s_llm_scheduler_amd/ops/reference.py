@@ -11,6 +11,7 @@ from __future__ import annotations
 import math
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 U32 = 0xFFFFFFFF
@@ -216,10 +217,41 @@ def _ord_key(l: torch.Tensor) -> torch.Tensor:
     return torch.where(neg, (~u) & U32, u | 0x80000000)
 
 
+NUC_FS = float(np.float32(65536.0 / 28.0))   # sampler.hip NUC_FS
+
+
+def nucleus_mask(l: torch.Tensor, T: float, P: float) -> torch.Tensor:
+    """The nucleus of sampler.hip for one row of fp32 logits: fine bin f = floor((M - l) / T * 65536/28)
+    (none beyond 28), mass = floor(exp((l - M) / T) * 2^40) as an integer, target = floor(Z * P); the
+    smallest f* with mass{f <= f*} >= target is found coarse (f >> 8) then fine (f & 255); keep f <= f*."""
+    l = l.float().cpu()
+    invT = torch.tensor(1.0, dtype=torch.float32) / torch.tensor(T, dtype=torch.float32)
+    M = l.max()
+    x = ((M - l) * invT) * torch.tensor(NUC_FS, dtype=torch.float32)
+    valid = x < 65536.0
+    f = torch.where(valid, x, torch.zeros_like(x)).to(torch.int64)
+    f = torch.where(valid, f, torch.full_like(f, 65536))
+    mass = (torch.exp((l - M) * invT) * 1099511627776.0).to(torch.int64)
+    mass = torch.where(valid, mass, torch.zeros_like(mass))
+    Z = int(mass.sum())
+    target = int(float(Z) * float(np.float32(P)))
+    coarse = torch.zeros(257, dtype=torch.int64).index_add_(0, torch.clamp(f >> 8, max=256), mass)[:256]
+    cum = torch.cumsum(coarse, 0)
+    hit = ((cum >= target) & (coarse != 0)).nonzero()
+    bstar = int(hit[0]) if len(hit) else 255
+    above = int(cum[bstar] - coarse[bstar])
+    inb = (f >> 8) == bstar
+    fine = torch.zeros(256, dtype=torch.int64).index_add_(0, (f & 255)[inb], mass[inb])
+    cum = above + torch.cumsum(fine, 0)
+    hit = ((cum >= target) & (fine != 0)).nonzero()
+    fstar = bstar * 256 + (int(hit[0]) if len(hit) else 255)
+    return f <= fstar
+
+
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor,
            counter: torch.Tensor) -> torch.Tensor:
     """logits [B, V] fp32 -> tokens [B] int32, bit-compatible with sampler.hip (up to fp rounding
-    of the Gumbel scores)."""
+    of the Gumbel scores and of the per-token masses at a nucleus boundary)."""
     B, V = logits.shape
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
     vid = torch.arange(V, dtype=torch.int64, device=logits.device)
@@ -232,12 +264,7 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
         keep = torch.ones(V, dtype=torch.bool, device=l.device)
         P = float(top_p[b])
         if P < 1.0:
-            probs = torch.softmax(l / T, -1).double()
-            order = torch.argsort(l, descending=True, stable=True)
-            cum = torch.cumsum(probs[order], 0)
-            k = int(torch.searchsorted(cum, torch.tensor(P * float(cum[-1]), dtype=cum.dtype, device=cum.device)))
-            thr = _ord_key(l[order[min(k, V - 1)]].reshape(1))
-            keep = _ord_key(l) >= thr
+            keep = nucleus_mask(l, T, P).to(l.device)
         u = u01(hash3(int(seeds[b]), int(counter[b]), vid)).float()
         g = -torch.log(-torch.log(u))
         score = torch.where(keep, l / T + g, torch.full_like(l, float("-inf")))

@@ -245,7 +245,11 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backe
             tp.rccl = make_rccl_comm(tp)
         if comm in ("auto", "xgmi"):
             tp.xgmi = make_xgmi_comm(tp)
-        if tp.xgmi is not None and os.environ.get("K8S_COMM_AUTOTUNE", "1") == "1":
+        tune = os.environ.get("K8S_COMM_AUTOTUNE", "1")
+        # ranks time-sharing one GPU (the 1-GPU rehearsals) measure the scheduler, not the transports:
+        # keep the built-in thresholds there unless forced
+        own_gpu = torch.cuda.device_count() >= tp_size
+        if tp.xgmi is not None and (tune == "force" or (tune == "1" and own_gpu)):
             autotune_comm(tp)   # thresholds between the xGMI protocols (and RCCL, when present)
         tp.comm_info["selected"] = "xgmi+rccl" if tp.xgmi is not None and tp.rccl is not None else \
             ("xgmi" if tp.xgmi is not None else ("rccl" if tp.rccl is not None else backend))
@@ -404,6 +408,7 @@ def autotune_comm(tp: TPGroup, sizes=(16384, 65536, 262144, 1 << 20, 4 << 20)) -
         if rc is not None:
             row["rccl"] = round(timed(lambda: rc.all_reduce(buf.data_ptr(), buf.data_ptr(), n // 2, 0, 0, -1)), 2)
         table[n] = row
+        log.info(f" all-reduce autotune {n} B: {row}")
     xg.ll_max_bytes, xg.twoshot_min_bytes = keep
     ok = xg.error() == 0
     # thresholds from the measurements

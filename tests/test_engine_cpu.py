@@ -267,3 +267,24 @@ def test_checkpoint_without_tokenizer_is_rejected(tmp_path, tiny):
     assert resolve_tokenizer(str(tmp_path / "ckpt"), None) == str(tmp_path / "ckpt" / "tokenizer.json")
     assert resolve_tokenizer(str(tmp_path / "ckpt"), "/x/tok.json") == "/x/tok.json"
     assert resolve_tokenizer(None, None) is None
+
+
+def test_nucleus_bins_cover_exact_nucleus():
+    """ref.nucleus_mask (the sampler.hip top-p rule) keeps the exact sorted-cumsum nucleus, plus at most
+    the rest of its boundary bin (28/65536 of log-probability wide), for peaked and flat rows."""
+    from k8s_llm_scheduler_amd.ops import reference as ref
+
+    g = torch.Generator().manual_seed(3)
+    for scale, T, P in ((3.0, 0.3, 0.9), (1.0, 1.0, 0.5), (0.2, 0.7, 0.95), (2.0, 0.5, 0.0)):
+        l = torch.randn(20000, generator=g) * scale
+        keep = ref.nucleus_mask(l, T, P)
+        probs = torch.softmax(l.double() / T, -1)
+        order = torch.argsort(probs, descending=True)
+        n = int((probs[order].cumsum(0) < P).sum()) + 1
+        exact = set(order[:n].tolist())
+        kept = set(keep.nonzero().flatten().tolist())
+        assert exact <= kept
+        extra = kept - exact
+        if extra:   # only boundary-bin ties: within 28/65536 in (M - l) / T of the last exact token
+            lo = float(l[order[n - 1]])
+            assert max((lo - float(l[i])) / T for i in extra) <= 28.0 / 65536 * 1.01

@@ -229,13 +229,56 @@ def test_sampler_matches_reference_and_distribution():
         assert agree >= 195
         probs = torch.softmax(logits[0].cpu() / 0.8, -1)
         if top_p < 1:
+            keep = ref.nucleus_mask(logits[0].cpu(), 0.8, top_p).nonzero().flatten()
             order = torch.argsort(probs, descending=True)
-            keep = order[: int((probs[order].cumsum(0) < top_p).sum()) + 1]
+            exact = order[: int((probs[order].cumsum(0) < top_p).sum()) + 1]
+            assert set(exact.tolist()) <= set(keep.tolist()) and len(keep) <= len(exact) + 1   # bin ties only
             assert counts[keep].sum() == N            # never samples outside the nucleus
             probs = torch.zeros_like(probs).index_put_((keep,), probs[keep])
             probs /= probs.sum()
         emp = counts / N
         assert (emp - probs).abs().sum() < 0.12       # L1 distance (expected ~0.05 at N=4000)
+
+
+@pytest.mark.parametrize("shards", [1, 8])
+def test_nucleus_full_vocab_matches_reference(shards):
+    """Multi-workgroup nucleus passes on a Llama-3 sized vocabulary (sharded like the TP=8 LM head),
+    rows of different temperature / top_p mixed with a Gumbel and a greedy row, eager and replayed from
+    a hipGraph: the token matches the CPU reference and lies in its nucleus."""
+    V, B = 128256, 4
+    g = torch.Generator(DEV).manual_seed(5)
+    flat = torch.randn(B, V, device=DEV, generator=g) * torch.tensor([[3.0], [1.0], [2.0], [2.0]], device=DEV)
+    logits = flat.reshape(B, shards, V // shards).permute(1, 0, 2).contiguous() if shards > 1 else flat
+    t = torch.tensor([0.3, 1.0, 0.7, 0.0], device=DEV)
+    p = torch.tensor([0.9, 0.5, 1.0, 0.9], device=DEV)
+    seeds = torch.tensor([1, 2, 3, 4], device=DEV, dtype=torch.int32)
+    agree = 0
+    for c in range(12):
+        ctr = torch.full((B,), c, device=DEV, dtype=torch.int32)
+        got = ops.sample(logits, t, p, seeds, ctr, shards=shards).cpu()
+        want = ref.sample(flat.cpu(), t.cpu(), p.cpu(), seeds.cpu(), ctr.cpu())
+        agree += int((got == want).sum())
+        for b in (0, 1):
+            assert bool(ref.nucleus_mask(flat[b].cpu(), float(t[b]), float(p[b]))[int(got[b])])
+        assert int(got[3]) == int(flat[3].argmax())
+    assert agree >= 12 * B - 2
+    # graph replay: the memset node re-arms the row state every replay
+    ctr = torch.full((B,), 3, device=DEV, dtype=torch.int32)
+    out = torch.zeros(B, device=DEV, dtype=torch.int32)
+    exp = ops.sample(logits, t, p, seeds, ctr, shards=shards, nucleus=True).clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.sample(logits, t, p, seeds, ctr, shards=shards, tokens_out=out, nucleus=True)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        ops.sample(logits, t, p, seeds, ctr, shards=shards, tokens_out=out, nucleus=True)
+    for _ in range(3):
+        out.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert out.tolist() == exp.tolist()
 
 
 def test_hash_init_matches_reference():

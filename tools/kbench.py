@@ -119,12 +119,12 @@ def main():
     t = torch.full((M,), 0.3, device=dev)
     p = torch.ones(M, device=dev)
     sd = torch.zeros(M, dtype=torch.int32, device=dev)
-    res.append(("sampler (gumbel, full vocab)", timeit(lambda: ops.sample(logits, t, p, sd, sd, shards=a.tp), a.iters), 0))
+    res.append(("sampler (gumbel, full vocab)", timeit(lambda: ops.sample(logits, t, p, sd, sd, shards=a.tp, nucleus=False), a.iters), 0))
     p09 = torch.full((M,), 0.9, device=dev)
     res.append(("sampler (nucleus top_p=0.9, T=0.3)",
-                timeit(lambda: ops.sample(logits, t, p09, sd, sd, shards=a.tp), a.iters), 0))
+                timeit(lambda: ops.sample(logits, t, p09, sd, sd, shards=a.tp, nucleus=True), a.iters), 0))
     t0 = torch.zeros(M, device=dev)
-    res.append(("sampler (greedy)", timeit(lambda: ops.sample(logits, t0, p, sd, sd, shards=a.tp), a.iters), 0))
+    res.append(("sampler (greedy)", timeit(lambda: ops.sample(logits, t0, p, sd, sd, shards=a.tp, nucleus=False), a.iters), 0))
     empty = torch.zeros(1, device=dev)
     res.append(("trivial torch kernel (launch floor)", timeit(lambda: empty.add_(1), a.iters), 0))
     print(f"# tp={a.tp} M={M} ctx={ctx}")

@@ -145,16 +145,24 @@ def main() -> int:
                     us = time_graph(lambda i, c=c, gr=gr: ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr), copies)
                     if us < best[0]:
                         best = (us, (c, gr))
+                gemv_us = None
+                if M <= ops.GEMV_MAX_M:   # the decode GEMV path these rows take today
+                    if epi == ops.EPI_SWIGLU:
+                        gfn = lambda i: ops.linear_swiglu(x, Ws[i])
+                    else:
+                        gfn = lambda i: ops.linear(x, Ws[i], out_dtype=torch.float32 if epi == ops.EPI_F32 else None)
+                    gemv_us = round(time_graph(gfn, copies), 2)
                 hc = ops.mgemm_heuristic(M, N, K, epi, a.fp8)
                 h_us = time_graph(lambda i: ops.mgemm(x, Ws[i], epi, cfg=hc[0], grid=hc[1]), copies)
                 us, (c, ks) = best
                 plans[f"{ops._mg_bucket(M)},{N},{K},{epi},{int(a.fp8)}"] = [c, ks, round(us, 2), round(lib_us, 2)]
                 row = dict(tp=tp, proj=name, M=M, N=N, K=K, epi=epi, fp8=a.fp8, lib_us=round(lib_us, 2),
                            mgemm_us=round(us, 2), cfg=c, grid=ks, heur_us=round(h_us, 2),
-                           speedup=round(lib_us / us, 3), tbps=round(wbytes / us / 1e6, 2))
+                           speedup=round(lib_us / us, 3), tbps=round(wbytes / us / 1e6, 2), gemv_us=gemv_us)
                 rows.append(row)
                 print(f"{tp:>3} {name:8} {M:>5} {N:>6} {K:>6} {lib_us:8.2f} {us:9.2f} {c:>4} {ks:>5} {h_us:8.2f} "
-                      f"{lib_us / us:7.2f} {wbytes / us / 1e6:6.2f}", flush=True)
+                      f"{lib_us / us:7.2f} {wbytes / us / 1e6:6.2f}" + (f" gemv {gemv_us:8.2f}" if gemv_us else ""),
+                      flush=True)
                 del x
             del Ws
             torch.cuda.empty_cache()
