@@ -211,7 +211,8 @@ def main() -> int:
         "p50_decision_latency_ms": round(1000 * statistics.median(lat), 2),
         "p99_decision_latency_ms": round(1000 * sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))], 2),
         "decode_ms_per_step": round(dec_tok_ms, 3),
-        "prefill_ms_per_decision": round(1000 * st["prefill_time"] / max(1, args.steps), 2),
+        "prefill_ms_per_step": round(1000 * st["prefill_time"] / max(1, args.steps), 2),
+        "prefill_ms_per_decision": round(1000 * st["prefill_time"] / max(1, args.steps * args.batch), 2),
         "prefill_tokens_per_decision": round(st["prefill_tokens"] / max(1, args.steps * args.batch), 1),
         "prefill_graph_replays": st.get("prefill_graph_replays", 0),
         "fallback_rate": round(fallbacks / (args.steps * args.batch), 3),
@@ -274,6 +275,9 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
     first = min(created[k] for k in keys)
     span = max(api.binding_times[k] for k in keys if k in api.binding_times) - first
     st = sched.get_stats()
+    fl = list(eng.finished_log)[args.warmup:]
+    ttft = sorted(f - a for a, f, _, _ in fl) or [0.0]
+    e2e = sorted(e - a for a, _, e, _ in fl) or [0.0]
     res = {
         "metric": "scheduling_decisions_per_sec",
         "value": round(len(lat) / span, 4),
@@ -298,6 +302,8 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
         "fallback_decisions": st["fallback_decisions"],
         "wall_s": round(time.perf_counter() - t0, 2),
         "init_s": round(init_s, 1),
+        "engine_p50_queue_to_first_token_ms": round(1000 * ttft[len(ttft) // 2], 1),
+        "engine_p50_request_ms": round(1000 * e2e[len(e2e) // 2], 1),
         "engine_decode_steps": eng.stats["decode_steps"],
         "engine_graph_replays": eng.stats["graph_replays"],
         "engine_prefill_graph_replays": eng.stats.get("prefill_graph_replays", 0),

@@ -192,9 +192,23 @@ __global__ void __launch_bounds__(ST) nuc_hist_kernel(const float* __restrict__ 
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the arrival
 
   // last arriver: bin totals (thread = bin), inclusive scan, first bin where the target is reached
+  // sc1 buffer loads (not atomics): independent, so all NB copies are in flight in one round trip
   unsigned long long tot = 0ull;
-  for (int w = 0; w < (int)gridDim.x; ++w)
-    tot += __hip_atomic_load(row_ws + (size_t)w * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  {
+    typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row_ws, 0, 0x7fffffff, 0x00020000);
+    constexpr int SC1 = 16;
+    for (int w0 = 0; w0 < (int)gridDim.x; w0 += 16) {
+      u32x2 v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        v[k] = w0 + k < (int)gridDim.x
+                   ? __builtin_amdgcn_raw_buffer_load_b64(rs, ((w0 + k) * 256 + tid) * 8, 0, SC1)
+                   : u32x2{0u, 0u};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) tot += ((unsigned long long)v[k][1] << 32) | v[k][0];
+    }
+  }
   int cur = 0;
   scan[0][tid] = tot;
   __syncthreads();

@@ -159,6 +159,7 @@ class LLMEngine:
         self._bg_thread: Optional[threading.Thread] = None
         self._bg_stop = False
         self._bg_error: Optional[BaseException] = None
+        self.finished_log: Deque[tuple] = deque(maxlen=4096)
         self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "graph_replays": 0, "prefill_graph_replays": 0, "prefill_time": 0.0, "decode_time": 0.0}
 
@@ -572,6 +573,8 @@ class LLMEngine:
         r.finished = True
         r.finish_reason = reason
         r.finish_time = time.perf_counter()
+        # (arrival, first token, finish, tokens) of the last requests: queueing vs service time
+        self.finished_log.append((r.arrival, r.first_token_time or r.finish_time, r.finish_time, len(r.output_ids)))
         if r.done is not None:
             r.done.set()
         if r.slot >= 0:

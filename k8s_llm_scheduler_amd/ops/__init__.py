@@ -245,7 +245,13 @@ def paged_prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: tor
 
 
 # ----------------------------------------------------------------------------- linear
-GEMV_MAX_M = 8
+GEMV_KERNEL_MAX_M = 8   # rows the GEMV kernels (gemv.hip) accept
+# rows up to which linear() / the decode step take the GEMV; above it the MFMA GEMM (mgemm.hip) is faster
+# (profiles/mgemm_small_m.txt: at 4 rows mgemm wins every 70B projection at TP = 1 and 8, bf16 and fp8;
+# at 2 rows the GEMV still wins or ties)
+GEMV_MAX_M = int(os.environ.get("K8S_GEMV_MAX_M", "2"))
+if not 1 <= GEMV_MAX_M <= GEMV_KERNEL_MAX_M:
+    raise ValueError(f"K8S_GEMV_MAX_M must be 1..{GEMV_KERNEL_MAX_M}")
 SKINNY_MAX_M = 64
 
 
@@ -413,8 +419,11 @@ MG_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__f
                              "mgemm_gfx950.json")
 
 
+MG_M_BUCKETS = (2, 4, 8) + GEMM_M_BUCKETS   # row buckets of the mgemm plan table
+
+
 def _mg_bucket(M: int) -> int:
-    for b in GEMM_M_BUCKETS:
+    for b in MG_M_BUCKETS:
         if b >= M:
             return b
     return 1 << max(0, (M - 1).bit_length())
@@ -598,8 +607,8 @@ def linear_norm(x: torch.Tensor, w, norm_w: Optional[torch.Tensor], eps: float,
         if epi == EPI_SWIGLU:
             return ref.linear_swiglu(h, w)
         return ref.linear(h, w, F32 if epi == EPI_F32 else None)
-    if M > GEMV_MAX_M:
-        raise ValueError("linear_norm is the decode path (M <= 8)")
+    if M > GEMV_KERNEL_MAX_M:
+        raise ValueError("linear_norm is the decode GEMV (M <= 8)")
     return _gemv(x, w, epi, F32 if epi == EPI_F32 else BF16, norm_w=norm_w, eps=eps, res_in=res_in, res_out=res_out,
                  folded=norm_w is None)
 

@@ -27,13 +27,17 @@ def test_quantize_roundtrip_error_bound():
 
 def test_fp8_linear_ops_match_dequantized_math():
     g = torch.Generator().manual_seed(1)
-    x = torch.randn(5, 256, generator=g).bfloat16()
+    x = torch.randn(ops.GEMV_MAX_M, 256, generator=g).bfloat16()   # GEMV rows: bf16 activations
     w = ops.quantize_fp8((torch.randn(96, 256, generator=g) * 0.05).bfloat16())
     wd = w.dequant(torch.float32)
     torch.testing.assert_close(ops.linear(x, w).float(), (x.float() @ wd.T).bfloat16().float())
+    xb = torch.randn(ops.GEMV_MAX_M + 3, 256, generator=g).bfloat16()   # GEMM rows: per-token e4m3 activations
+    q, sc = ref.quantize_fp8(xb)
+    xq = ref.dequant_fp8(q, sc, torch.float32)
+    torch.testing.assert_close(ops.linear(xb, w).float(), (xq.bfloat16().float() @ wd.T).bfloat16().float())
     gu = ops.quantize_fp8((torch.randn(2 * 48, 256, generator=g) * 0.05).bfloat16())
-    y = ops.linear_swiglu(x, gu)
-    want = ref.linear_swiglu(x, gu.dequant(torch.float32))
+    y = ops.linear_swiglu(xb, gu)
+    want = ref.linear_swiglu(xq.bfloat16(), gu.dequant(torch.float32))
     torch.testing.assert_close(y.float(), want.float())
 
 

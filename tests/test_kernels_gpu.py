@@ -136,37 +136,41 @@ def test_prefill_attention_spike_forces_rescale():
 @pytest.mark.parametrize("M", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("N,K", [(1280, 8192), (8192, 1024), (16032, 8192), (8192, 3584), (96, 512)])
 def test_gemv(M, N, K):
+    """The GEMV kernel at every row count it accepts, and ops.linear's routing (GEMV up to GEMV_MAX_M rows,
+    mgemm above) at the same shapes."""
     x, w = rnd(M, K), rnd(N, K, scale=0.05)
-    got = ops.linear(x, w)
     want = ref.linear(x.cpu(), w.cpu())
-    close(got, want, 3e-2)
-    got32 = ops.linear(x, w, out_dtype=torch.float32)
-    close(got32, ref.linear(x.cpu(), w.cpu(), torch.float32), 1e-2, 1e-3)
+    want32 = ref.linear(x.cpu(), w.cpu(), torch.float32)
+    close(ops._gemv(x, w, ops.EPI_BF16, torch.bfloat16), want, 3e-2)
+    close(ops._gemv(x, w, ops.EPI_F32, torch.float32), want32, 1e-2, 1e-3)
+    close(ops.linear(x, w), want, 3e-2)
+    close(ops.linear(x, w, out_dtype=torch.float32), want32, 1e-2, 1e-3)
 
 
 @pytest.mark.parametrize("M", [1, 4, 8])
 @pytest.mark.parametrize("I,K", [(3584, 8192), (128, 512)])
 def test_gemv_swiglu(M, I, K):
     x, w = rnd(M, K), rnd(2 * I, K, scale=0.05)
-    close(ops.linear_swiglu(x, w), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)
+    want = ref.linear_swiglu(x.cpu(), w.cpu())
+    close(ops._gemv(x, w, ops.EPI_SWIGLU, torch.bfloat16), want, 3e-2)
+    close(ops.linear_swiglu(x, w), want, 3e-2)
 
 
 @pytest.mark.parametrize("M", [9, 16, 17, 40, 64])
 @pytest.mark.parametrize("N,K", [(1280, 8192), (10240, 8192), (8192, 3584), (100, 256), (16032, 8192)])
 def test_skinny_mfma_gemm(M, N, K, monkeypatch):
-    """Batched-decode path (8 < M <= 64): MFMA skinny GEMM (stream-K, fp32 atomics), all epilogues."""
-    monkeypatch.setattr(ops, "SKINNY_ENABLED", True)
+    """The opt-in MFMA skinny GEMM kernel (skinny_mfma.hip: stream-K, fp32 atomics; K8S_SKINNY=1, superseded by
+    mgemm on the default route), called directly, all epilogues."""
     x, w = rnd(M, K), rnd(N, K, scale=0.05)
-    close(ops.linear(x, w), ref.linear(x.cpu(), w.cpu()), 3e-2)
-    close(ops.linear(x, w, out_dtype=torch.float32), ref.linear(x.cpu(), w.cpu(), torch.float32), 1e-2, 1e-3)
+    close(ops._skinny(x, w, ops.EPI_BF16, torch.bfloat16), ref.linear(x.cpu(), w.cpu()), 3e-2)
+    close(ops._skinny(x, w, ops.EPI_F32, torch.float32), ref.linear(x.cpu(), w.cpu(), torch.float32), 1e-2, 1e-3)
 
 
 @pytest.mark.parametrize("M", [12, 64])
 @pytest.mark.parametrize("I,K", [(3584, 8192), (128, 512), (28672, 8192)])
 def test_skinny_mfma_swiglu(M, I, K, monkeypatch):
-    monkeypatch.setattr(ops, "SKINNY_ENABLED", True)
     x, w = rnd(M, K), rnd(2 * I, K, scale=0.05)
-    close(ops.linear_swiglu(x, w), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)
+    close(ops._skinny(x, w, ops.EPI_SWIGLU, torch.bfloat16), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)
 
 
 def test_prefill_linear_and_silu_mul():
@@ -362,8 +366,9 @@ def test_gemv_fp8(M, N, K):
     x = rnd(M, K)
     w = ops.quantize_fp8(rnd(N, K, scale=0.05))
     want = x.float().cpu() @ ref.dequant_fp8(w.q.cpu(), w.scale.cpu()).T   # exact fp32 dequant
-    close(ops.linear(x, w), want.bfloat16(), 3e-2)
-    close(ops.linear(x, w, out_dtype=torch.float32), want, 1e-2, 1e-3)
+    # the GEMV kernel itself at every row count it accepts (ops.linear routes M > GEMV_MAX_M to mgemm)
+    close(ops._gemv(x, w, ops.EPI_BF16, torch.bfloat16), want.bfloat16(), 3e-2)
+    close(ops._gemv(x, w, ops.EPI_F32, torch.float32), want, 1e-2, 1e-3)
 
 
 @pytest.mark.parametrize("M", [1, 4])

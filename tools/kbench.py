@@ -60,7 +60,7 @@ def main():
         w = (torch.randn(N * (2 if epi == 2 else 1), K, device=dev) * 0.02).to(bf)
         nw = torch.ones(K, device=dev, dtype=bf)
         ri, ro = torch.randn(M, K, device=dev).to(bf), torch.empty(M, K, device=dev, dtype=bf)
-        if norm and M > ops.GEMV_MAX_M:
+        if norm and M > ops.GEMV_KERNEL_MAX_M:
             return
         if norm:  # the model's layout: norm weight folded into W, 1/rms in the epilogue
             fn = lambda: ops.linear_norm(x, w, None, 1e-5, ri, ro, epi=epi)
