@@ -248,7 +248,36 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
                             watch_timeout=3600)
     rng = random.Random(7)
     n_total = args.warmup + args.steps
-    created = {}
+    created, detected = {}, {}
+    claim = sched._claim
+
+    def traced_claim(pod):   # detection time of every pod (the scheduler claims it on its first event)
+        key = f"{pod['metadata'].get('namespace', 'default')}/{pod['metadata']['name']}"
+        detected.setdefault(key, time.perf_counter())
+        return claim(pod)
+
+    sched._claim = traced_claim
+    # per-pod phase stamps inside the worker thread: start, decision call, decision return
+    phases = {}
+    run_claimed, decide = sched._schedule_claimed, sched.llm_client.get_scheduling_decision
+
+    def traced_run(pod, t0, revalidate):
+        key = f"{pod['metadata'].get('namespace', 'default')}/{pod['metadata']['name']}"
+        phases.setdefault(key, {})["start"] = time.perf_counter()
+        tls.key = key
+        return run_claimed(pod, t0, revalidate)
+
+    def traced_decide(prompt, spec, nodes):
+        ph = phases.setdefault(getattr(tls, "key", ""), {})
+        ph["call"] = time.perf_counter()
+        d = decide(prompt, spec, nodes)
+        ph["ret"] = time.perf_counter()
+        return d
+
+    import threading
+    tls = threading.local()
+    sched._schedule_claimed = traced_run
+    sched.llm_client.get_scheduling_decision = traced_decide
 
     async def main():
         task = asyncio.create_task(sched.start())
@@ -275,6 +304,18 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
     first = min(created[k] for k in keys)
     span = max(api.binding_times[k] for k in keys if k in api.binding_times) - first
     st = sched.get_stats()
+    c2d = sorted(detected[k] - created[k] for k in keys if k in detected) or [0.0]
+    d2b = sorted(api.binding_times[k] - detected[k] for k in keys if k in detected and k in api.binding_times) or [0.0]
+    def p50(vals):
+        vals = sorted(vals) or [0.0]
+        return round(1000 * vals[len(vals) // 2], 1)
+
+    ph = [(detected[k], phases[k], api.binding_times[k]) for k in keys
+          if k in detected and k in api.binding_times and {"start", "call", "ret"} <= set(phases.get(k, {}))]
+    phase_ms = {"detect_to_thread": p50([p["start"] - d for d, p, _ in ph]),
+                "thread_to_engine_call": p50([p["call"] - p["start"] for d, p, _ in ph]),
+                "decision_call": p50([p["ret"] - p["call"] for d, p, _ in ph]),
+                "decision_to_bind": p50([b - p["ret"] for d, p, b in ph])}
     fl = list(eng.finished_log)[args.warmup:]
     ttft = sorted(f - a for a, f, _, _ in fl) or [0.0]
     e2e = sorted(e - a for a, _, e, _ in fl) or [0.0]
@@ -302,6 +343,9 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
         "fallback_decisions": st["fallback_decisions"],
         "wall_s": round(time.perf_counter() - t0, 2),
         "init_s": round(init_s, 1),
+        "p50_phase_ms": phase_ms,
+        "p50_create_to_detect_ms": round(1000 * c2d[len(c2d) // 2], 1),
+        "p50_detect_to_bind_ms_scheduler": round(1000 * d2b[len(d2b) // 2], 1),
         "engine_p50_queue_to_first_token_ms": round(1000 * ttft[len(ttft) // 2], 1),
         "engine_p50_request_ms": round(1000 * e2e[len(e2e) // 2], 1),
         "engine_decode_steps": eng.stats["decode_steps"],

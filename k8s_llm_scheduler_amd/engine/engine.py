@@ -576,6 +576,9 @@ class LLMEngine:
         # (arrival, first token, finish, tokens) of the last requests: queueing vs service time
         self.finished_log.append((r.arrival, r.first_token_time or r.finish_time, r.finish_time, len(r.output_ids)))
         if r.done is not None:
+            # background-loop request: its caller holds the object, so drop it from the table here (the
+            # caller never waits for the engine lock, which the loop holds for a whole step)
+            self.requests.pop(r.rid, None)
             r.done.set()
         if r.slot >= 0:
             self.s_ctx[r.slot] = 0
@@ -658,6 +661,7 @@ class LLMEngine:
                     return
             try:
                 self.step()
+                time.sleep(0)   # let threads blocked on the GIL / engine lock in before the next step
             except Exception as e:  # noqa: BLE001 -- every pending request fails, the loop keeps serving
                 log.error(f"Engine step failed: {e!r}")
                 self._bg_error = e
@@ -719,22 +723,18 @@ class LLMEngine:
 
     def _generate_bg(self, prompts, params, deadline: Optional[float]) -> List[Output]:
         reqs = [self.add_request(p, sp) for p, sp in zip(prompts, params)]
-        try:
-            for r in reqs:
-                left = None if deadline is None else max(0.0, deadline - time.monotonic())
-                if not r.done.wait(timeout=left):
-                    for q in reqs:
-                        self.abort(q.rid)
-                    raise TimeoutError("decision engine deadline exceeded")
-            failed = next((r.error for r in reqs if r.error is not None), None)
-            if failed is not None:
-                raise RuntimeError(f"decision engine failure: {failed}") from failed
-            return [self.output(r) for r in reqs]
-        finally:
-            with self.lock:
-                for r in reqs:
-                    if r.finished:
-                        self.requests.pop(r.rid, None)
+        for r in reqs:
+            left = None if deadline is None else max(0.0, deadline - time.monotonic())
+            if not r.done.wait(timeout=left):
+                for q in reqs:
+                    q.aborted = True   # reaped (and finished) by the loop's next step; no engine lock here
+                with self._wake:
+                    self._wake.notify()
+                raise TimeoutError("decision engine deadline exceeded")
+        failed = next((r.error for r in reqs if r.error is not None), None)
+        if failed is not None:
+            raise RuntimeError(f"decision engine failure: {failed}") from failed
+        return [self.output(r) for r in reqs]
 
 
 class _PyBlockAllocator:
