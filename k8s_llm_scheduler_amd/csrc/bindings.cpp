@@ -50,6 +50,11 @@ int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const v
                                float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax,
                                hipStream_t s);
 long long k8s_decode_split_workspace(int B, int nq, int nkv, int pmax);
+int k8s_decode_attention_split_oproj(void* attn, void* part, uint32_t* counters, const void* qkv, const float* cos_sin,
+                                     void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
+                                     float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks,
+                                     int pmax, const void* wo, void* o_out, int N, uint32_t* sync, int delay,
+                                     int poll_sleep, hipStream_t s);
 int k8s_decode_attention_split(void* out, void* part, uint32_t* counters, const void* qkv, const float* cos_sin,
                                void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
                                float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax,
@@ -165,6 +170,17 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("decode_split_workspace", [](int B, int nq, int nkv, int pmax) {
     return k8s_decode_split_workspace(B, nq, nkv, pmax);
+  });
+  m.def("decode_attention_split_oproj", [](uintptr_t attn, uintptr_t part, uintptr_t counters, uintptr_t qkv,
+                                           uintptr_t cos_sin, uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx,
+                                           float scale, int B, int nq, int nkv, int D, int bs, int max_blocks,
+                                           int pmax, uintptr_t wo, uintptr_t o_out, int N, uintptr_t sync,
+                                           int delay, int poll_sleep, int64_t s) {
+    check(k8s_decode_attention_split_oproj(P(attn), P(part), P<uint32_t>(counters), P(qkv), P<float>(cos_sin),
+                                           P(kc), P(vc), P<int>(bt), P<int>(ctx), scale, B, nq, nkv, D, bs,
+                                           max_blocks, pmax, P(wo), P(o_out), N, P<uint32_t>(sync), delay,
+                                           poll_sleep, S(s)),
+          "decode_attention_split_oproj");
   });
   m.def("decode_attention_split", [](uintptr_t out, uintptr_t part, uintptr_t counters, uintptr_t qkv,
                                      uintptr_t cos_sin, uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx,

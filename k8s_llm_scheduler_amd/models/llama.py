@@ -341,9 +341,9 @@ class LlamaModel:
         x = h
         for l, w in enumerate(self.layers):
             qkv = ops.linear_norm(x, w.wqkv, g1(w) if g1 else None, c.rms_eps, None, None)
-            a = ops.decode_attention_fused(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
-                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
-            o = ops.linear(a, w.wo)
+            # attention + O projection: one launch (the W_o stream overlaps attention) where the shapes allow
+            o = ops.decode_attention_oproj(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
+                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D, w.wo)
             self.tp.all_reduce_(o, residual=x)                 # o = x + attention branch
             g = ops.linear_norm(o, w.wgu, g2(w) if g2 else None, c.rms_eps, None, None, epi=ops.EPI_SWIGLU)
             x = ops.linear(g, w.wdown)

@@ -664,6 +664,58 @@ def _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, contex
     return out
 
 
+# split attention + O projection in one launch (decode_split_oproj_kernel), opt-in with K8S_FUSE_ATTN_O=1:
+# correct (tests/test_kernels_gpu.py, test_model_gpu.py) but measured slower than the two launches it replaces
+# (profiles/kbench_attn_oproj_fusion.txt: 13.3-14.3 vs 12.0 us at TP=8, ctx 564; decode 4.49 vs 4.30 ms/token)
+FUSE_ATTN_O = os.environ.get("K8S_FUSE_ATTN_O", "0") == "1"
+ATTN_O_DELAY = int(os.environ.get("K8S_ATTN_O_DELAY", "0"))        # ~1.7 us units before the W_o loads
+ATTN_O_POLL = int(os.environ.get("K8S_ATTN_O_POLL", "1"))          # ~0.1 us units between polls
+
+
+def attn_oproj_fusable(B: int, wo, max_context: int, nq: int, nkv: int, D: int) -> bool:
+    """The fused kernel covers TP >= 4 decode shards of Llama-3.3-70B (o_proj K = nq * D of 1024 / 2048,
+    bf16 W_o) at <= 2 sequences on the split-attention path."""
+    return (FUSE_ATTN_O and not _is_fp8(wo) and wo.is_cuda and B <= 2 and D == 128 and nq * D in (1024, 2048)
+            and wo.shape[1] == nq * D and B * nkv <= SPLIT_MAX_PAIRS and max_context <= 64 * SPLIT_PARTITION)
+
+
+def decode_attention_oproj(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                           block_tables: torch.Tensor, context_lens: torch.Tensor, scale: float, block_size: int,
+                           max_context: int, nq: int, nkv: int, D: int, wo: torch.Tensor) -> torch.Tensor:
+    """linear(decode_attention_fused(...), wo) as one launch: the O-projection workgroups hold their W_o rows
+    in registers while the attention chunks run and start the moment the last (sequence, kv head) output is
+    published.  Returns o [B, N] bf16.  CPU / unsupported shapes: the two separate ops."""
+    B = qkv.shape[0]
+    if not (_gpu(qkv, k_cache) and block_size == 16 and attn_oproj_fusable(B, wo, max_context, nq, nkv, D)):
+        a = decode_attention_fused(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
+                                   max_context, nq, nkv, D)
+        return linear(a, wo)
+    N = wo.shape[0]
+    pmax = max(1, math.ceil(max_context / SPLIT_PARTITION))
+    attn = torch.empty(B, nq * D, dtype=BF16, device=qkv.device)
+    o = torch.empty(B, N, dtype=BF16, device=qkv.device)
+    part = None
+    if pmax > 1:
+        part = torch.empty(native().decode_split_workspace(B, nq, nkv, pmax), dtype=F32, device=qkv.device)
+    counters = _zeroed_scratch(qkv.device, "attn_split", B * nkv * 4)
+    sync = _zeroed_scratch(qkv.device, "attn_oproj_sync", 1280)
+    native().decode_attention_split_oproj(attn.data_ptr(), part.data_ptr() if part is not None else 0, counters,
+                                          _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"),
+                                          _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
+                                          _chk(block_tables, I32, "block_tables"),
+                                          _chk(context_lens, I32, "context_lens"), float(scale), B, nq, nkv, D,
+                                          block_size, block_tables.shape[1], pmax, _chk(wo, BF16, "wo"), o.data_ptr(),
+                                          N, sync, ATTN_O_DELAY, ATTN_O_POLL, -1)
+    del part
+    return o
+
+
+def attn_oproj_timeouts(dev) -> int:
+    """Non-zero if an O-projection workgroup of decode_attention_oproj ever gave up waiting (a bug signal)."""
+    buf = _SCRATCH.get(("attn_oproj_sync", dev.index if dev.index is not None else torch.cuda.current_device()))
+    return 0 if buf is None else int(buf[1152:1156].view(torch.int32).item())
+
+
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     """silu(x @ Wg.T) * (x @ Wu.T) with w_gate_up = [Wg; Wu] ([2I, K]); the SwiGLU is the GEMM's epilogue."""
     if not _gpu(x, w_gate_up):
