@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert(FM >= 1 && FN >= 1 && BM % (WM * 16) == 0 && BN % (WN * 16) == 0, "tile / wave split");
   static_assert(EPI != MG_SWIGLU || FN % 2 == 0, "SwiGLU pairs gate and up fragments");
   static_assert(S >= 2 && S <= 8, "ring depth");
+  static_assert(WN == 1 || WN == 2 || WN == 4, "the RMS prologue splits a fragment's 4 dot2 over WN waves");
   static_assert(RB == 64 || RB == 128 || RB == 256 || RB == 512, "row bytes per k-step");
   constexpr int CPR = RB / 16;                       // 16-byte chunks per staged row
   constexpr int KS = FP8 ? RB / 32 : RB / 64;        // k32 MFMA steps per k-step (RB = 64: one)
@@ -105,9 +106,9 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert((S - 2) * LPS <= 63, "vmcnt range");
   static_assert(WK == 1 || (WK - 1) * FN * FM * 64 * 16 * WM * WN <= S * STAGE_B, "LDS reduction space");
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the launch stub (its lambdas use device builtins)
-  __shared__ __attribute__((aligned(16))) char lds[S * STAGE_B + 16 + WK * BM * 4];
+  __shared__ __attribute__((aligned(16))) char lds[S * STAGE_B + 16 + WK * WN * BM * 4];
   unsigned* flag = reinterpret_cast<unsigned*>(lds + S * STAGE_B);
-  float* rss = reinterpret_cast<float*>(lds + S * STAGE_B + 16);   // [WK][BM] row sums of squares
+  float* rss = reinterpret_cast<float*>(lds + S * STAGE_B + 16);   // [WK * WN][BM] row sums of squares
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wk = wid % WK, wt = wid / WK;           // k-share, output sub-tile
@@ -221,13 +222,15 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
 #pragma unroll
             for (int j = 0; j < FM; ++j)
               acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], bfr[j], acc[f][j], 0, 0, 0);
-          if (do_rms && wn == 0) {   // the x rows are the same for every wn: count them once
+          if (do_rms) {   // the WN waves of a row block hold the same x fragments: each squares 1/WN of them
 #pragma unroll
             for (int j = 0; j < FM; ++j)
 #pragma unroll
               for (int e = 0; e < 4; ++e) {   // v_dot2_f32_bf16: two squares per instruction
-                const bf16x2 v2 = {bfr[j][2 * e], bfr[j][2 * e + 1]};
-                ss[j] = __builtin_amdgcn_fdot2_f32_bf16(v2, v2, ss[j], false);
+                if (WN == 1 || e % WN == wn % 4) {
+                  const bf16x2 v2 = {bfr[j][2 * e], bfr[j][2 * e + 1]};
+                  ss[j] = __builtin_amdgcn_fdot2_f32_bf16(v2, v2, ss[j], false);
+                }
               }
           }
         } else {
@@ -299,15 +302,15 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
         ss[j] += __shfl_xor(ss[j], 16, WAVE);
         ss[j] += __shfl_xor(ss[j], 32, WAVE);
       }
-      if (wn == 0 && g == 0) {
+      if (g == 0) {
 #pragma unroll
-        for (int j = 0; j < FM; ++j) rss[wk * BM + wm * (BM / WM) + j * 16 + li] = ss[j];
+        for (int j = 0; j < FM; ++j) rss[(wk * WN + wn) * BM + wm * (BM / WM) + j * 16 + li] = ss[j];
       }
       mg_barrier();
       if (threadIdx.x < BM) {
         float t = 0.f;
 #pragma unroll
-        for (int k2 = 0; k2 < WK; ++k2) t += rss[k2 * BM + threadIdx.x];
+        for (int k2 = 0; k2 < WK * WN; ++k2) t += rss[k2 * BM + threadIdx.x];
         rss[threadIdx.x] = t;   // row total of this segment (own thread reads / writes only)
       }
     }
@@ -514,7 +517,7 @@ extern "C" int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* ld
   *bm = c.bm;
   *bn = c.bn;
   *threads = 64 * c.wm * c.wn * c.wk;
-  *lds_bytes = c.s * (c.bm + c.bn) * c.rb + 16;
+  *lds_bytes = c.s * (c.bm + c.bn) * c.rb + 16 + c.wk * c.wn * c.bm * 4;
   *swiglu = (c.bn / (c.wn * 16)) % 2 == 0;
   *rb = c.rb;
   return 0;

@@ -462,10 +462,16 @@ def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
     return mgemm_heuristic(M, N, K, epi, fp8)
 
 
-def mgemm_preferred(M: int, N: int, K: int, epi: int, fp8: bool) -> bool:
+# what a fused mgemm saves over library GEMM + the separate kernel it absorbs (an RMSNorm or a residual add
+# at decode / prefill row counts, launch included: profiles/mgemm_fused_norm_residual_probe.txt)
+FUSION_CREDIT_US = 5.0
+
+
+def mgemm_preferred(M: int, N: int, K: int, epi: int, fp8: bool, fused: bool = False) -> bool:
     """K8S_GEMM=auto: the hand-written GEMM unless the tuned table measured the library GEMM more than 3 %
     faster at this shape (prefill-size row counts, where mgemm's tiles are not yet at the library's
-    MFMA efficiency: profiles/mgemm_vs_hipblaslt_bf16.txt)."""
+    MFMA efficiency: profiles/mgemm_vs_hipblaslt_bf16.txt).  ``fused``: the call carries the RMS prologue or
+    the residual epilogue, which the library route pays as one more kernel (FUSION_CREDIT_US)."""
     if GEMM_BACKEND == "mgemm":
         return True
     if GEMM_BACKEND == "library":
@@ -473,7 +479,7 @@ def mgemm_preferred(M: int, N: int, K: int, epi: int, fp8: bool) -> bool:
     pick = _mg_table_row(M, N, K, epi, fp8)
     if pick is None or not pick[4]:
         return M <= 128          # untuned shape: mgemm's streaming tiles are safe, its prefill tiles are not
-    return pick[3] <= 1.03 * pick[4]
+    return pick[3] <= 1.03 * pick[4] + (FUSION_CREDIT_US if fused else 0.0)
 
 
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
@@ -515,9 +521,10 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
     return out
 
 
-def _mgemm_route(M: int, w, K: int, epi: int) -> bool:
+def _mgemm_route(M: int, w, K: int, epi: int, fused: bool = False) -> bool:
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
-    return GEMM_BACKEND != "library" and _mgemm_ok(N, K, _is_fp8(w)) and mgemm_preferred(M, N, K, epi, _is_fp8(w))
+    return GEMM_BACKEND != "library" and _mgemm_ok(N, K, _is_fp8(w)) and \
+        mgemm_preferred(M, N, K, epi, _is_fp8(w), fused)
 
 
 def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Tensor:
@@ -525,7 +532,7 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
     load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
     copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM."""
     M, K = r.shape
-    if _gpu(r) and M > GEMV_MAX_M and not _is_fp8(w) and _mgemm_route(M, w, K, epi):
+    if _gpu(r) and M > GEMV_MAX_M and not _is_fp8(w) and _mgemm_route(M, w, K, epi, fused=True):
         return mgemm(r.contiguous(), w, epi, rms_eps=eps)
     ones = _ones(K, r.device)
     x = rmsnorm(r, ones, eps)
@@ -538,7 +545,7 @@ def linear_residual(x: torch.Tensor, w, res: torch.Tensor) -> torch.Tensor:
     """res + x @ w.T (bf16), written into ``res`` (the residual stream).  mgemm route: the add is the GEMM's
     epilogue; otherwise GEMM + add."""
     M, K = x.shape
-    if _gpu(x) and M > GEMV_MAX_M and _mgemm_route(M, w, K, EPI_BF16):
+    if _gpu(x) and M > GEMV_MAX_M and _mgemm_route(M, w, K, EPI_BF16, fused=True):
         return mgemm(x.contiguous(), w, EPI_BF16, res=res, out=res)
     y = linear(x, w)
     if y.is_cuda:

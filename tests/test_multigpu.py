@@ -110,7 +110,8 @@ def _model_and_engine(tp, res, preset="tiny-tp8"):
         res["argmax_equal"] = bool(torch.equal(full(lg).argmax(-1).cpu(), full(lg1).argmax(-1).cpu()))
         del m1
     del m
-    eng = build_engine(preset, tp=tp, device="cuda", max_batch=4, max_model_len=512, num_blocks=128, seed=1)
+    eng = build_engine(preset, tp=tp, device="cuda", max_batch=4, max_model_len=512, num_blocks=128, seed=1,
+                       capture_nucleus=True)   # a top_p < 1 request below: the graphs with the nucleus passes
     outs = eng.generate(["tensor parallel over xgmi", "second request", "third"],
                         [SamplingParams(max_tokens=12, temperature=0.8, seed=9, ignore_eos=True),
                          SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True),
