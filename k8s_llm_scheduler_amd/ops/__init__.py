@@ -452,7 +452,9 @@ def _mg_table_row(M: int, N: int, K: int, epi: int, fp8: bool):
     if not rows:
         return None
     mb = _mg_bucket(M)
-    return next((r for r in rows if r[0] >= mb), rows[-1])
+    # nearest tuned bucket at or above M; past the largest tuned bucket the shape counts as untuned (a plan
+    # tuned at 256 rows says nothing about an 8192-row prefill chunk)
+    return next((r for r in rows if r[0] >= mb), None)
 
 
 def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
@@ -462,9 +464,11 @@ def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
     return mgemm_heuristic(M, N, K, epi, fp8)
 
 
-# what a fused mgemm saves over library GEMM + the separate kernel it absorbs (an RMSNorm or a residual add
-# at decode / prefill row counts, launch included: profiles/mgemm_fused_norm_residual_probe.txt)
-FUSION_CREDIT_US = 5.0
+# routing credit for a fused mgemm (RMS prologue / residual epilogue) against library GEMM + the separate
+# kernel it absorbs.  0 by default: with 5 us the TP=1 B=64 decode moved QKV off the library and got slower
+# (30.6 -> 31.7 ms/step, profiles/bench_r2c_tp1_b64_credit5.json) -- the table's plain-GEMM times already
+# rank these shapes well
+FUSION_CREDIT_US = float(os.environ.get("K8S_FUSION_CREDIT_US", "0"))
 
 
 def mgemm_preferred(M: int, N: int, K: int, epi: int, fp8: bool, fused: bool = False) -> bool:
