@@ -1,4 +1,4 @@
-"""mgemm.hip (hand-written MFMA GEMM for M > 8 rows) against the fp32 PyTorch oracle of ops/reference.py:
+"""mgemm.hip (hand-written MFMA GEMM for batches of more than 2 rows) against the fp32 PyTorch oracle of ops/reference.py:
 every tile configuration x epilogue (bf16 / fp32 / SwiGLU) x weight dtype (bf16 / row-scaled e4m3) x split-K,
 partial tiles in M and N, plus the Llama-3.3-70B projection shapes at TP = 8 that the engine routes here."""
 
