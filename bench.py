@@ -144,6 +144,10 @@ def main() -> int:
         return items
 
     prompt_tokens = len(eng.render_chat(svc.system_message, make_items()[0][0]))
+    if prompt_tokens + args.gen_tokens > args.max_model_len:
+        # the engine would reject every request and the bench would time the fallback path instead
+        raise SystemExit(f"prompt ({prompt_tokens} tokens) + --gen-tokens {args.gen_tokens} exceeds --max-model-len "
+                         f"{args.max_model_len}: raise --max-model-len")
     if args.arrival_rate > 0:
         if world > 1 and not tp.simulate:
             raise SystemExit("--arrival-rate is a single-rank serving benchmark")

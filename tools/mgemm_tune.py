@@ -113,6 +113,7 @@ def main() -> int:
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
     a = ap.parse_args()
 
     if a.all_buckets:
@@ -143,6 +144,10 @@ def main() -> int:
                 best = (float("inf"), None)
                 for c, gr in candidates(M, N, K, epi, a.fp8):
                     us = time_graph(lambda i, c=c, gr=gr: ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr), copies)
+                    if a.verbose:
+                        bm, bn = ops.mgemm_configs()[c][:2]
+                        print(f"    cand tp{tp} {name} M={M} cfg {c:2d} ({bm}x{bn}) grid {gr:5d} "
+                              f"nwg {ops.mgemm_nwg(c, M, N, K, epi, a.fp8, gr):5d}: {us:8.2f} us", flush=True)
                     if us < best[0]:
                         best = (us, (c, gr))
                 gemv_us = None
