@@ -122,7 +122,11 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
   constexpr int GI = (1024 + NT - 1) / NT;  // norm-weight chunks per thread held in registers (xch <= 1024)
   const int nkc = K >> 3;
   u32x4 g[GI];
-  u32x4 pre[NL][M];
+  // the first pass's x (and residual) chunks: every load issued before any is consumed -- the add of
+  // x + res_in happens after the weight stream has been started (norm_row_chunk's own add would wait
+  // for each chunk in turn, a serial chain of L2 round trips ahead of the first weight load)
+  u32x4 pre[NL][M], preb[NL][M];
+  const bool has_res = res_in != nullptr;
   if (NORM != 0) {
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
@@ -134,7 +138,30 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
     for (int u = 0; u < NL; ++u) {
       const int c = min((int)threadIdx.x + u * (int)blockDim.x, nkc - 1);
 #pragma unroll
-      for (int m = 0; m < M; ++m) norm_row_chunk<M>(x, res_in, m, K, c, pre[u][m]);
+      for (int m = 0; m < M; ++m) pre[u][m] = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + c * 8);
+    }
+    if (has_res) {
+#pragma unroll
+      for (int u = 0; u < NL; ++u) {
+        const int c = min((int)threadIdx.x + u * (int)blockDim.x, nkc - 1);
+#pragma unroll
+        for (int m = 0; m < M; ++m) preb[u][m] = *reinterpret_cast<const u32x4*>(res_in + (size_t)m * K + c * 8);
+      }
+    }
+  }
+  // plain input: the first 4 x chunks per thread (a whole 8192-wide row at 256 threads) are loaded
+  // BEFORE the weight stream too, so staging them into LDS waits for x only, not for the first
+  // weight block (loads retire in order: a wait for x issued after the weights is a wait for both)
+  constexpr int XP = 4;
+  u32x4 px[XP][M];
+  if (NORM == 0) {
+#pragma unroll
+    for (int p = 0; p < XP; ++p) {
+      const int i = (int)threadIdx.x + p * NT;
+      if (i < xch) {   // no redundant loads ahead of the weights (o_proj at TP = 8: 128 chunks)
+#pragma unroll
+        for (int m = 0; m < M; ++m) px[p][m] = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + kb + i * 8);
+      }
     }
   }
   // weights do not depend on x: start streaming them before the x staging / norm prologue
@@ -155,23 +182,11 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
     float ss[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = 0.f;
-    // NL row chunks per thread per pass, all loaded before any is consumed (the first pass was
-    // issued before the weight stream): at K = 8192 and M <= 2 the whole row is ONE pass
-    for (int c0 = threadIdx.x; c0 < nkc; c0 += blockDim.x * NL) {
-      u32x4 r[NL][M];
-      if (c0 == (int)threadIdx.x) {
-#pragma unroll
-        for (int u = 0; u < NL; ++u)
-#pragma unroll
-          for (int m = 0; m < M; ++m) r[u][m] = pre[u][m];
-      } else {
-#pragma unroll
-        for (int u = 0; u < NL; ++u) {
-          const int c = min(c0 + u * (int)blockDim.x, nkc - 1);
-#pragma unroll
-          for (int m = 0; m < M; ++m) norm_row_chunk<M>(x, res_in, m, K, c, r[u][m]);
-        }
-      }
+    // NL row chunks per thread per pass, all loaded before any is consumed.  The first pass was issued
+    // before the weight stream and is consumed here in straight-line code, so the compiler's wait
+    // counts only its own loads (inside a loop the header wait would be vmcnt(0), i.e. also wait for
+    // the first weight block); at K = 8192 and M <= 2 the whole row is this one pass.
+    auto consume = [&](int c0, u32x4 (&r)[NL][M]) {
 #pragma unroll
       for (int u = 0; u < NL; ++u) {
         const int c = c0 + u * (int)blockDim.x;
@@ -187,6 +202,29 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
             ss[m] += l * l + h * h;
           }
         }
+      }
+    };
+    if (has_res) {
+#pragma unroll
+      for (int u = 0; u < NL; ++u)
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            pre[u][m][j] = pack_bf2(lo_bf(pre[u][m][j]) + lo_bf(preb[u][m][j]),
+                                    hi_bf(pre[u][m][j]) + hi_bf(preb[u][m][j]));
+    }
+    consume((int)threadIdx.x, pre);
+    if (nkc > (int)blockDim.x * NL) {   // rows longer than one pass (K > 8192 at M <= 2)
+      for (int c0 = threadIdx.x + blockDim.x * NL; c0 < nkc; c0 += blockDim.x * NL) {
+        u32x4 r[NL][M];
+#pragma unroll
+        for (int u = 0; u < NL; ++u) {
+          const int c = min(c0 + u * (int)blockDim.x, nkc - 1);
+#pragma unroll
+          for (int m = 0; m < M; ++m) norm_row_chunk<M>(x, res_in, m, K, c, r[u][m]);
+        }
+        consume(c0, r);
       }
     }
 #pragma unroll
@@ -231,10 +269,19 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
       }
     }
   } else if (NORM == 0) {
-    // stage x[:, kb:kb+klen] into LDS
-    for (int i = threadIdx.x; i < M * xch; i += blockDim.x) {
-      const int m = i / xch, c = i - m * xch;
-      xs[m * (KS >> 3) + c] = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + kb + c * 8);
+    // stage x[:, kb:kb+klen] into LDS: the chunks loaded ahead of the weights, then any remainder
+#pragma unroll
+    for (int p = 0; p < XP; ++p) {
+      const int i = (int)threadIdx.x + p * NT;
+      if (i < xch) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) xs[m * (KS >> 3) + i] = px[p][m];
+      }
+    }
+    for (int i = threadIdx.x + XP * NT; i < xch; i += NT) {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        xs[m * (KS >> 3) + i] = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + kb + i * 8);
     }
   }
   __syncthreads();
