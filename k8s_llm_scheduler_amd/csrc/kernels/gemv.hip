@@ -155,13 +155,16 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
   constexpr int XP = 4;
   u32x4 px[XP][M];
   if (NORM == 0) {
+    // unconditional buffer loads bounded by the slice: a chunk past it reads 0 without a memory access
+    // (a branch per chunk made the compiler copy the whole array per branch and wait on each load)
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x + kb), 0,
+                                                     (M - 1) * K * 2 + xch * 16, 0x00020000);
 #pragma unroll
     for (int p = 0; p < XP; ++p) {
       const int i = (int)threadIdx.x + p * NT;
-      if (i < xch) {   // no redundant loads ahead of the weights (o_proj at TP = 8: 128 chunks)
 #pragma unroll
-        for (int m = 0; m < M; ++m) px[p][m] = *reinterpret_cast<const u32x4*>(x + (size_t)m * K + kb + i * 8);
-      }
+      for (int m = 0; m < M; ++m)
+        px[p][m] = __builtin_amdgcn_raw_buffer_load_b128(xr, m * K * 2 + i * 16, 0, 0);
     }
   }
   // weights do not depend on x: start streaming them before the x staging / norm prologue
@@ -171,6 +174,9 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
 #pragma unroll
     for (int r = 0; r < NR; ++r)
       wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r]) + min(cb + lane + 64 * u, clast));
+  // keep the x staging below the weight issue: the compiler would otherwise merge each x chunk's
+  // `if (i < xch)` load and LDS store into one block ahead of the weights and wait per chunk
+  asm volatile("" ::: "memory");
 
   float inv[M];
   if (NORM != 0) {
