@@ -1,4 +1,4 @@
-// K3 / K8 / K9(+K10) / K11 / K15: hand-written MFMA GEMM for projections with more than 8 rows
+// K3 / K8 / K9(+K10) / K11 / K15: hand-written MFMA GEMM for projections with more than 2 rows
 // (prefill chunks, batched decode), bf16 or OCP-e4m3 weights, fp32 accumulate (gfx950).
 //
 //     out[M, N] = epi( x[M, K] . W[N, K]^T )        epi: bf16 | fp32 | SwiGLU (silu(g) * u)

@@ -5,9 +5,10 @@ fused into one weight each: ``wqkv`` = [q; k; v] rows, ``wgu`` = [gate; up] rows
 row-parallel (followed by an all-reduce), the LM head is vocabulary-parallel (fp32 logits are
 all-gathered shard-major), the embedding is replicated (no collective on the input side).
 
-Every op on a CUDA tensor is a hand-written gfx950 kernel from ``ops`` except the prefill
-projections with more than 8 rows, which are plain library GEMMs (hipBLASLt).  The same code
-runs on CPU through the fp32 reference ops, which is how TP=k == TP=1 is tested with gloo.
+Every op on a CUDA tensor is a hand-written gfx950 kernel from ``ops``; projections with more than
+``ops.GEMV_MAX_M`` rows run the hand-written MFMA GEMM except the prefill-size shapes where its tuned
+plan table measured hipBLASLt faster.  The same code runs on CPU through the fp32 reference ops, which
+is how TP=k == TP=1 is tested with gloo.
 
 Weights: deterministic hash-uniform random init (identical global tensors for every TP degree
 and device; BASELINE allows random-init weights) or a HuggingFace safetensors checkpoint,

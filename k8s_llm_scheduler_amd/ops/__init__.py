@@ -332,7 +332,7 @@ def _lib_linear(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return torch.nn.functional.linear(xp, w)[:M]
 
 
-# ----------------------------------------------------------------------------- MFMA GEMM (M > 8)
+# ----------------------------------------------------------------------------- MFMA GEMM (M > GEMV_MAX_M)
 # A plan is (cfg, grid): cfg indexes mgemm.hip's tile configurations; grid > 0 launches grid workgroups
 # per output tile (split-K), grid < 0 launches min(-grid, work items) workgroups that stream equal shares
 # of the (tile, k-step) items (stream-K: balanced whatever the tile count).
@@ -489,7 +489,7 @@ def mgemm_preferred(M: int, N: int, K: int, epi: int, fp8: bool, fused: bool = F
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
           grid: Optional[int] = None, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
           out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Hand-written MFMA GEMM (mgemm.hip): epi(x[M, K] @ w[N, K].T) for M > 8 rows.  ``w``: bf16 or
+    """Hand-written MFMA GEMM (mgemm.hip): epi(x[M, K] @ w[N, K].T), any M (routed for M > GEMV_MAX_M).  ``w``: bf16 or
     Fp8Weight (activations are then quantized per token by quantize_act_fp8).  SwiGLU: w = [Wg; Wu].
     ``rms_eps``: RMSNorm prologue -- the result is scaled by 1/rms(x row) (the norm gamma must be folded into
     ``w``), so the un-normalised residual stream feeds the GEMM directly.  ``res``: residual epilogue
@@ -532,7 +532,7 @@ def _mgemm_route(M: int, w, K: int, epi: int, fused: bool = False) -> bool:
 
 
 def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Tensor:
-    """epi(rmsnorm(r) @ w.T) for M > 8 rows with the norm gamma folded into ``w`` (LlamaModel folds it at
+    """epi(rmsnorm(r) @ w.T) for M > GEMV_MAX_M rows with the norm gamma folded into ``w`` (LlamaModel folds it at
     load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
     copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM."""
     M, K = r.shape
@@ -578,7 +578,7 @@ if GEMM_BACKEND not in ("mgemm", "library", "auto"):
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
-    """y = x @ w.T with w [N, K] (bf16 or Fp8Weight).  M <= 8 rows: hand-written HBM-streaming GEMV;
+    """y = x @ w.T with w [N, K] (bf16 or Fp8Weight).  M <= GEMV_MAX_M rows: hand-written HBM-streaming GEMV;
     more rows (batched decode, prefill): hand-written MFMA GEMM (mgemm.hip)."""
     if not _gpu(x, w):
         return ref.linear(_ref_act_quant(x, w), w, out_dtype)
