@@ -32,8 +32,14 @@ FUSED_PARTITION = 1024
 SPLIT_PARTITION = 64
 # Decode attention with at most this many (sequence, kv head) pairs uses the small-grid kernel
 # (attn_decode_split.hip: one wave per 64-token chunk, in-kernel merge); more pairs fill the chip
-# with the one-workgroup-per-pair kernel (attn_decode_fused.hip).  K8S_ATTN_SPLIT_PAIRS overrides.
-SPLIT_MAX_PAIRS = int(os.environ.get("K8S_ATTN_SPLIT_PAIRS", "64"))
+# with the one-workgroup-per-pair kernel (attn_decode_fused.hip).  Measured crossover at ctx 564
+# (profiles/kbench_attn_split_vs_onewg.txt): split 11.7 vs 14.9 us at 32 pairs, 17.4 vs 14.9 at 64; in the
+# 4096-token graph class the split grid is 4x larger and the crossover halves.  K8S_ATTN_SPLIT_PAIRS overrides.
+SPLIT_MAX_PAIRS = int(os.environ.get("K8S_ATTN_SPLIT_PAIRS", "32"))
+
+
+def _split_pairs_limit(max_context: int) -> int:
+    return SPLIT_MAX_PAIRS if max_context <= 1024 else SPLIT_MAX_PAIRS // 2
 
 
 def native():
@@ -639,7 +645,7 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
                           block_tables=block_tables, block_size=block_size)
         return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, context_lens, scale,
                                           block_size).view(B, nq * D)
-    if B * nkv <= SPLIT_MAX_PAIRS and max_context <= 64 * SPLIT_PARTITION:
+    if B * nkv <= _split_pairs_limit(max_context) and max_context <= 64 * SPLIT_PARTITION:
         return _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
                                        max_context, nq, nkv, D)
     pmax = max(1, math.ceil(max_context / FUSED_PARTITION))
@@ -687,7 +693,8 @@ def attn_oproj_fusable(B: int, wo, max_context: int, nq: int, nkv: int, D: int) 
     """The fused kernel covers TP >= 4 decode shards of Llama-3.3-70B (o_proj K = nq * D of 1024 / 2048,
     bf16 W_o) at <= 2 sequences on the split-attention path."""
     return (FUSE_ATTN_O and not _is_fp8(wo) and wo.is_cuda and B <= 2 and D == 128 and nq * D in (1024, 2048)
-            and wo.shape[1] == nq * D and B * nkv <= SPLIT_MAX_PAIRS and max_context <= 64 * SPLIT_PARTITION)
+            and wo.shape[1] == nq * D and B * nkv <= _split_pairs_limit(max_context)
+            and max_context <= 64 * SPLIT_PARTITION)
 
 
 def decode_attention_oproj(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,

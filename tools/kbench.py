@@ -94,7 +94,7 @@ def main():
     qkv = torch.randn(M, (nq + 2 * nkv) * D, device=dev).to(bf)
     cs = ref.rope_table(D, 4096, 500000.0, None).to(dev)
     default_pairs = ops.SPLIT_MAX_PAIRS
-    for pairs, tag in ((0, "one-wg"), (default_pairs, "split")):
+    for pairs, tag in ((0, "one-wg"), (default_pairs, "split"), (1 << 20, "split-any")):
         ops.SPLIT_MAX_PAIRS = pairs
         for mc in (1024, 4096):
             us = timeit(lambda: ops.decode_attention_fused(qkv, cs, kc, vc, bt, cl, 0.088, bs, mc, nq, nkv, D), a.iters)
