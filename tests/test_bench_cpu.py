@@ -1,0 +1,47 @@
+"""The bench.py contract the driver depends on (README / task): one JSON line on stdout with the headline metric and
+config, here on CPU with the tiny preset; the Poisson-arrival serving mode; and the refusal of prompts that do not fit
+--max-model-len (which would otherwise time the fallback path)."""
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args, timeout=300):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_json_line_contract():
+    p = _run("--preset", "tiny", "--steps", "2", "--warmup", "1", "--gen-tokens", "8")
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["metric"] == "scheduling_decisions_per_sec" and d["higher_is_better"] is True
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+    assert d["dtype"] == "bf16" and "synthetic" in d["data"]
+    assert d["config"]["parallelism"] == "tp1" and d["config"]["global_batch"] == 1
+    assert abs(d["vs_baseline"] - d["value"] / 0.3) < 0.01 * d["vs_baseline"] + 1e-3
+
+
+def test_bench_arrival_mode():
+    p = _run("--preset", "tiny", "--arrival-rate", "20", "--steps", "6", "--warmup", "1", "--batch", "4",
+             "--gen-tokens", "8")
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["bound"] == 6 and d["config"]["scheduler_mode"] == "continuous"
+    assert d["p50_detect_to_bind_ms"] > 0 and set(d["p50_phase_ms"]) == {
+        "detect_to_thread", "thread_to_engine_call", "decision_call", "decision_to_bind"}
+
+
+def test_bench_refuses_prompt_longer_than_max_model_len():
+    p = _run("--preset", "tiny", "--nodes", "64", "--max-model-len", "2048", "--steps", "1", "--warmup", "0")
+    assert p.returncode != 0 and "max-model-len" in (p.stderr + p.stdout)
