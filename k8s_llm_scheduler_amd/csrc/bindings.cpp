@@ -47,7 +47,7 @@ int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M,
                   const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
 int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const void* qkv, const float* cos_sin,
                                void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
-                               float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax,
+                               float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax, int part,
                                hipStream_t s);
 long long k8s_decode_split_workspace(int B, int nq, int nkv, int pmax);
 int k8s_decode_attention_split_oproj(void* attn, void* part, uint32_t* counters, const void* qkv, const float* cos_sin,
@@ -163,9 +163,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("decode_attention_fused", [](uintptr_t out, uintptr_t pacc, uintptr_t pml, uintptr_t qkv, uintptr_t cos_sin,
                                      uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx, float scale, int B, int nq,
-                                     int nkv, int D, int bs, int max_blocks, int pmax, int64_t s) {
+                                     int nkv, int D, int bs, int max_blocks, int pmax, int part, int64_t s) {
     check(k8s_decode_attention_fused(P(out), P(pacc), P(pml), P(qkv), P<float>(cos_sin), P(kc), P(vc), P<int>(bt),
-                                     P<int>(ctx), scale, B, nq, nkv, D, bs, max_blocks, pmax, S(s)),
+                                     P<int>(ctx), scale, B, nq, nkv, D, bs, max_blocks, pmax, part, S(s)),
           "decode_attention_fused");
   });
   m.def("decode_split_workspace", [](int B, int nq, int nkv, int pmax) {

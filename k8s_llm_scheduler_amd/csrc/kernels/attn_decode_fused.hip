@@ -28,14 +28,14 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
 
 __device__ __forceinline__ int vswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
-template <int D, int G, int PART>
-__global__ void __launch_bounds__(1024) decode_fused_kernel(
+template <int D, int G, int PART, int NW>
+__global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_acc, float* __restrict__ part_ml, const bf16_t* __restrict__ qkv,
     const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ context_lens, float scale, int block_size,
     int max_blocks, int nkv, int pmax) {
   static_assert(D == 128 && G <= 16, "head_dim 128, group <= 16");
-  constexpr int NW = 16;
+  static_assert(PART / NW == 64, "64 tokens per wave");
   constexpr int NT = NW * WAVE;
   constexpr int TW = PART / NW;   // tokens per wave (64)
   constexpr int NTILE = TW / 16;  // 16-token tiles per wave
@@ -304,32 +304,43 @@ __global__ void __launch_bounds__(D) decode_merge_kernel(bf16_t* __restrict__ ou
 
 using namespace k8sllm;
 
-// part_acc [B, nq, pmax, D] f32 / part_ml [B, nq, pmax, 2] f32 (needed when pmax > 1)
+// part_acc [B, nq, pmax, D] f32 / part_ml [B, nq, pmax, 2] f32 (needed when pmax > 1).
+// part: context tokens per workgroup, 1024 (16 waves, ~137 KB of LDS: one workgroup per CU) or 512 (8 waves,
+// ~73 KB: two per CU -- for batches whose (sequence, kv head) pairs outnumber the CUs, where the 16-wave
+// workgroups would run in two rounds).  pmax = ceil(max context / part).
 extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const void* qkv,
                                           const float* cos_sin, void* k_cache, void* v_cache, const int* block_tables,
                                           const int* context_lens, float scale, int B, int nq, int nkv, int D,
-                                          int block_size, int max_blocks, int pmax, hipStream_t stream) {
+                                          int block_size, int max_blocks, int pmax, int part, hipStream_t stream) {
   if (B <= 0) return 0;
   if (D != 128 || nq % nkv != 0) return -1;
   if (block_size != 16) return -4;  // the speculative K loads assume one 16-token block per tile
   if (pmax > 1 && (part_acc == nullptr || part_ml == nullptr)) return -3;
+  if (part != 1024 && part != 512) return -5;
   const int G = nq / nkv;
   dim3 grid(pmax, nkv, B);
-#define L(GG)                                                                                               \
-  decode_fused_kernel<128, GG, 1024><<<grid, 1024, 0, stream>>>(                                             \
+#define L(GG, PP, WW)                                                                                       \
+  decode_fused_kernel<128, GG, PP, WW><<<grid, WW * 64, 0, stream>>>(                                        \
       (bf16_t*)out, (float*)part_acc, (float*)part_ml, (const bf16_t*)qkv, cos_sin, (bf16_t*)k_cache,       \
       (bf16_t*)v_cache, block_tables, context_lens, scale, block_size, max_blocks, nkv, pmax)
-  switch (G) {
-    case 1: L(1); break;
-    case 2: L(2); break;
-    case 4: L(4); break;
-    case 8: L(8); break;
-    case 16: L(16); break;
-    default: return -2;
+#define LG(PP, WW)                 \
+  switch (G) {                     \
+    case 1: L(1, PP, WW); break;   \
+    case 2: L(2, PP, WW); break;   \
+    case 4: L(4, PP, WW); break;   \
+    case 8: L(8, PP, WW); break;   \
+    case 16: L(16, PP, WW); break; \
+    default: return -2;            \
   }
+  if (part == 1024) {
+    LG(1024, 16)
+  } else {
+    LG(512, 8)
+  }
+#undef LG
 #undef L
   if (pmax > 1)
     decode_merge_kernel<128><<<dim3(nq, B), 128, 0, stream>>>((bf16_t*)out, (const float*)part_acc,
-                                                              (const float*)part_ml, context_lens, 1024, pmax, nq);
+                                                              (const float*)part_ml, context_lens, part, pmax, nq);
   return (int)hipGetLastError();
 }

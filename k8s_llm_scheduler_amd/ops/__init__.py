@@ -648,7 +648,8 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
     if B * nkv <= _split_pairs_limit(max_context) and max_context <= 64 * SPLIT_PARTITION:
         return _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
                                        max_context, nq, nkv, D)
-    pmax = max(1, math.ceil(max_context / FUSED_PARTITION))
+    part = fused_partition(B * nkv)
+    pmax = max(1, math.ceil(max_context / part))
     out = torch.empty(B, nq * D, dtype=BF16, device=qkv.device)
     if pmax > 1:
         pacc = torch.empty(B * nq * pmax * D, dtype=F32, device=qkv.device)
@@ -659,8 +660,19 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
     native().decode_attention_fused(out.data_ptr(), pa, pm, _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"),
                                     _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
                                     _chk(block_tables, I32, "block_tables"), _chk(context_lens, I32, "context_lens"),
-                                    float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], pmax, -1)
+                                    float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], pmax, part, -1)
     return out
+
+
+# Context tokens per workgroup of the one-workgroup-per-pair decode attention: 1024 (16 waves, one workgroup per CU
+# by LDS).  K8S_ATTN_FUSED_PART=512 selects 8-wave workgroups (two per CU): faster for short contexts at TP = 1 with
+# 64 sequences (ctx 256: 30.1 vs 32.3 us) but slower at the bench's ~0.5k contexts, which then take two partitions
+# and the merge kernel (40.8 vs 36.1 us, decode 31.1 vs 30.6 ms/step; profiles/kbench_attn_split_vs_onewg.txt).
+FUSED_PART_ENV = int(os.environ.get("K8S_ATTN_FUSED_PART", "1024"))
+
+
+def fused_partition(pairs: int) -> int:
+    return FUSED_PART_ENV if FUSED_PART_ENV in (512, 1024) else FUSED_PARTITION
 
 
 def _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,

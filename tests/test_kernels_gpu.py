@@ -309,11 +309,14 @@ def test_linear_norm_fused(M, epi, with_res):
     close(got, want, 3e-2 if epi != 1 else 2e-2)
 
 
-@pytest.mark.parametrize("split_pairs", [0, 64], ids=["one-wg-per-pair", "small-grid-split"])
+@pytest.mark.parametrize("variant", ["one-wg-1024", "one-wg-512", "small-grid-split"])
 @pytest.mark.parametrize("nq,nkv", [(8, 1), (64, 8), (32, 8), (4, 2), (16, 1)])
 @pytest.mark.parametrize("ctxs", [[1, 37, 600], [1024, 1025], [3000], [64, 65, 128]])
-def test_decode_attention_fused(nq, nkv, ctxs, split_pairs, monkeypatch):
-    monkeypatch.setattr(ops, "SPLIT_MAX_PAIRS", split_pairs)
+def test_decode_attention_fused(nq, nkv, ctxs, variant, monkeypatch):
+    """The one-workgroup-per-pair kernel at both partition sizes (16 waves x 1024 tokens, 8 waves x 512 tokens with
+    the merge kernel from 513 tokens on) and the small-grid split kernel."""
+    monkeypatch.setattr(ops, "SPLIT_MAX_PAIRS", 64 if variant == "small-grid-split" else 0)
+    monkeypatch.setattr(ops, "FUSED_PART_ENV", 512 if variant == "one-wg-512" else 1024)
     D, bs = 128, 16
     B = len(ctxs)
     maxb = (max(ctxs) + bs - 1) // bs
