@@ -235,7 +235,7 @@ class LLMEngine:
                     self.graphs[(B, mc, nuc)] = g
         if self.prefill_graphs_enabled():
             for Tb in PREFILL_GRAPH_BUCKETS:
-                if Tb in self.prefill_graphs:
+                if Tb in self.prefill_graphs or not self._prefill_bucket_capturable(Tb):
                     continue
                 # a harmless chunk: Tb tokens of one sequence over block 0 whose K/V all go to the
                 # scratch block (block 0 is only read)
@@ -254,14 +254,24 @@ class LLMEngine:
         torch.cuda.synchronize(self.device)
 
     def prefill_graphs_enabled(self) -> bool:
-        """Single-rank engines only by default: a TP > 1 prefill carries 4-8 MiB all-reduces that
-        may leave the xGMI kernels for RCCL (or gloo in the 1-GPU rehearsal, which cannot be
-        captured); ``K8S_PREFILL_GRAPHS=1`` opts a multi-rank RCCL engine in."""
-        tp = self.model.tp
-        single = tp.world <= 1 or tp.simulate
+        """Prefill chunks of one sequence replay captured graphs (``K8S_PREFILL_GRAPHS=0`` turns them off).
+        Multi-rank engines capture only the buckets whose collectives all stay on xGMI
+        (``_prefill_bucket_capturable``); ``K8S_PREFILL_GRAPHS=1`` captures every bucket (RCCL included)."""
         env = os.environ.get("K8S_PREFILL_GRAPHS", "")
-        on = env == "1" or (env == "" and single)
-        return on and self.use_graphs and PREFILL_GRAPH_BUCKETS[-1] <= self.max_prefill_tokens
+        return env != "0" and self.use_graphs and PREFILL_GRAPH_BUCKETS[-1] <= self.max_prefill_tokens
+
+    def _prefill_bucket_capturable(self, Tb: int) -> bool:
+        """TP > 1: a chunk of Tb tokens all-reduces Tb x hidden bf16 twice per layer and all-gathers one row of
+        fp32 logits; both must fit the xGMI transports, because a gloo collective cannot be captured (the 1-GPU
+        rehearsals) and RCCL capture stays opt-in until it has run on a multi-GPU node."""
+        tp = self.model.tp
+        if tp.world <= 1 or tp.simulate or os.environ.get("K8S_PREFILL_GRAPHS", "") == "1":
+            return True
+        if tp.xgmi is None:
+            return False
+        ar_bytes = Tb * self.model.cfg.hidden * 2
+        gather_bytes = self.model.lm_head.shape[0] * 4
+        return ar_bytes <= (tp.xgmi_max_ar or tp.xgmi.max_allreduce_bytes) and gather_bytes <= tp.xgmi.slot_bytes
 
     def _p_views(self, Tb: int):
         Tm = PREFILL_GRAPH_BUCKETS[-1]

@@ -116,8 +116,13 @@ def _model_and_engine(tp, res, preset="tiny-tp8"):
                         [SamplingParams(max_tokens=12, temperature=0.8, seed=9, ignore_eos=True),
                          SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True),
                          SamplingParams(max_tokens=12, temperature=0.3, top_p=0.9, seed=4, ignore_eos=True)])
-    res["tokens"] = [o.token_ids for o in outs]
+    # one request alone: its prefill chunk replays a prefill graph (xGMI-only buckets at TP > 1)
+    solo = eng.generate(["a single prompt prefilled by a graph"], [SamplingParams(max_tokens=4, temperature=0.0,
+                                                                                  ignore_eos=True)])
+    res["tokens"] = [o.token_ids for o in outs] + [solo[0].token_ids]
     res["graph_replays"] = eng.stats["graph_replays"]
+    res["prefill_graph_replays"] = eng.stats["prefill_graph_replays"]
+    res["prefill_graphs"] = sorted(eng.prefill_graphs)
 
 
 def _rehearsal_rank(rank, world):
@@ -145,6 +150,7 @@ def _assert_model(res, world):
     assert r0["decode_err"] < 0.03 * r0["logit_scale"] + 0.03, r0
     assert all(res[r]["tokens"] == r0["tokens"] for r in range(world)), "ranks drew different tokens"
     assert r0["graph_replays"] > 0
+    assert r0["prefill_graph_replays"] > 0, r0["prefill_graphs"]
 
 
 @pytest.mark.parametrize("world", [8, 4])
