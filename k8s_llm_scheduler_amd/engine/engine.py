@@ -54,6 +54,25 @@ BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
 # either way -- the chunk is GEMM-bound, profiles/rocprof_prefill_tp8.txt).  The padding tokens
 # belong to no sequence (cu_q stops at the real length) and write their K/V into a scratch block.
 PREFILL_GRAPH_BUCKETS = (64, 128, 192, 256, 320, 384, 448, 512)
+_P_SPLIT = 6   # packed prefill-graph inputs of the two micro-batch halves: cu_q0 (2), ctx0, cu_q1 (2), ctx1
+
+
+def split_prefill_meta(cu: Sequence[int], ctx: Sequence[int], T0: int) -> tuple:
+    """Split a varlen prefill chunk at token ``T0`` into two micro-batches (``LlamaModel.forward_prefill``
+    ``split``).  ``cu`` are the chunk's query offsets, ``ctx[s]`` sequence s's context length after the chunk.
+    A sequence straddling T0 contributes its first part to half 0 (whose context then ends where that part
+    ends) and the rest to half 1.  Returns ``((cu0, ctx0, seqs0), (cu1, ctx1, seqs1))`` with ``seqs`` the
+    chunk-local sequence indices of each half (rows of the block table)."""
+    halves = (([0], [], []), ([0], [], []))
+    for s in range(len(cu) - 1):
+        a, b = cu[s], cu[s + 1]
+        for h, (lo, hi) in enumerate(((a, min(b, T0)), (max(a, T0), b))):
+            if hi > lo:
+                c, cx, sq = halves[h]
+                c.append(c[-1] + hi - lo)
+                cx.append(ctx[s] - (b - hi))
+                sq.append(s)
+    return halves
 
 
 @dataclass
@@ -161,7 +180,8 @@ class LLMEngine:
         self._bg_error: Optional[BaseException] = None
         self.finished_log: Deque[tuple] = deque(maxlen=4096)
         self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
-                      "graph_replays": 0, "prefill_graph_replays": 0, "prefill_time": 0.0, "decode_time": 0.0}
+                      "graph_replays": 0, "prefill_graph_replays": 0, "prefill_overlap_chunks": 0, "prefill_time": 0.0,
+                      "decode_time": 0.0}
 
     # ------------------------------------------------------------------ device state
     def _alloc_state(self) -> None:
@@ -176,9 +196,10 @@ class LLMEngine:
         self.s_steps = torch.zeros(B, **i32)
         self.s_hist = torch.zeros(B, self.max_new_cap, **i32)
         # prefill-graph inputs, one packed buffer filled by one host->device copy per chunk:
-        # [ids | positions | slots] x Tmax, then cu_q (2), context_lens (1), last_idx (1)
+        # [ids | positions | slots] x Tmax, then cu_q (2), context_lens (1), last_idx (1), then the two
+        # micro-batch halves' cu_q / context_lens (_P_SPLIT)
         Tm = PREFILL_GRAPH_BUCKETS[-1]
-        self.p_packed = torch.zeros(3 * Tm + 4, **i32)
+        self.p_packed = torch.zeros(3 * Tm + 4 + _P_SPLIT, **i32)
         self.p_bt = torch.zeros(1, self.max_blocks_per_seq, **i32)
 
     def _ctx_classes(self) -> List[int]:
@@ -279,16 +300,31 @@ class LLMEngine:
         return (pk[:Tb], pk[Tm:Tm + Tb], pk[2 * Tm:2 * Tm + Tb], pk[3 * Tm:3 * Tm + 2], pk[3 * Tm + 2:3 * Tm + 3],
                 pk[3 * Tm + 3:3 * Tm + 4])
 
+    def _overlap_split_at(self, T: int) -> int:
+        """Token at which a TP > 1 prefill chunk of T tokens splits into two micro-batches (0: no split)."""
+        if T < self.model.PREFILL_OVERLAP_MIN or not self.model.prefill_overlap:
+            return 0
+        return max(16, T // 2 // 16 * 16)
+
     def _prefill_graph_body(self, Tb: int) -> torch.Tensor:
         ids, pos, slots, cu, ctx, last = self._p_views(Tb)
-        return self.model.forward_prefill(ids, pos, slots, cu, ctx, self.p_bt, Tb, last)
+        split = None
+        T0 = self._overlap_split_at(Tb)
+        if T0:
+            o = 3 * PREFILL_GRAPH_BUCKETS[-1] + 4
+            pk = self.p_packed
+            split = (T0, (pk[o:o + 2], pk[o + 2:o + 3], self.p_bt, T0),
+                     (pk[o + 3:o + 5], pk[o + 5:o + 6], self.p_bt, Tb - T0))
+        return self.model.forward_prefill(ids, pos, slots, cu, ctx, self.p_bt, Tb, last, split=split)
 
     def _fill_prefill_state(self, ids, pos, slots, ctx_len: int, blocks, Tb: int) -> None:
         """One chunk of ONE sequence into the graph's static inputs; positions Tb-T.. are padding
-        (token 0 at position 0, K/V into the scratch slot, outside cu_q)."""
+        (token 0 at position 0, K/V into the scratch slot, outside cu_q).  The micro-batch halves (tokens
+        [0, T0) and [T0, Tb), ``_overlap_split_at``) get their own cu_q / context length: a half holding
+        only padding has no query tokens."""
         T, Tm = len(ids), PREFILL_GRAPH_BUCKETS[-1]
         pad = Tb - T
-        host = torch.zeros(3 * Tm + 4, dtype=torch.int32)
+        host = torch.zeros(3 * Tm + 4 + _P_SPLIT, dtype=torch.int32)
         host[:T] = torch.tensor(ids, dtype=torch.int32)
         host[Tm:Tm + T] = torch.tensor(pos, dtype=torch.int32)
         host[2 * Tm:2 * Tm + T] = torch.tensor(slots, dtype=torch.int32)
@@ -296,6 +332,12 @@ class LLMEngine:
         host[3 * Tm + 1] = T
         host[3 * Tm + 2] = ctx_len
         host[3 * Tm + 3] = T - 1
+        T0 = self._overlap_split_at(Tb)
+        if T0:
+            n0, n1 = min(T, T0), max(0, T - T0)
+            o = 3 * Tm + 4
+            host[o + 1], host[o + 2] = n0, ctx_len - n1
+            host[o + 4], host[o + 5] = n1, ctx_len
         bt = torch.zeros(1, self.max_blocks_per_seq, dtype=torch.int32)
         bt[0, :len(blocks)] = torch.tensor(blocks, dtype=torch.int32)
         self.p_packed.copy_(host.to(self.device, non_blocking=True))
@@ -466,9 +508,21 @@ class LLMEngine:
             graph, logits = self.prefill_graphs[Tb]
             graph.replay()
             self.stats["prefill_graph_replays"] += 1
+            self.stats["prefill_overlap_chunks"] += bool(self._overlap_split_at(Tb))
         else:
-            logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx), bt.to(dev, non_blocking=True),
-                                                max(e - s for _, s, e in chunk), t(last))
+            bt_d = bt.to(dev, non_blocking=True)
+            split = None
+            T0 = self._overlap_split_at(len(ids))
+            if T0:
+                halves = []
+                for c_h, x_h, seqs in split_prefill_meta(cu, ctx, T0):
+                    idx = torch.tensor(seqs, dtype=torch.long, device=dev)
+                    halves.append((t(c_h), t(x_h), bt_d.index_select(0, idx),
+                                   max(b - a for a, b in zip(c_h, c_h[1:]))))
+                split = (T0, halves[0], halves[1])
+                self.stats["prefill_overlap_chunks"] += 1
+            logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx), bt_d,
+                                                max(e - s for _, s, e in chunk), t(last), split=split)
         self.stats["prefill_tokens"] += len(ids)
         done = [(i, r) for i, (r, s, e) in enumerate(chunk) if e == len(r.prompt_ids)]
         for r, s, e in chunk:

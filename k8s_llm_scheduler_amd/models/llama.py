@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import json
 import math
+import os
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Dict, List, Optional
@@ -228,6 +229,81 @@ class LlamaModel:
                 r = d
         return r
 
+    # ------------------------------------------------------------------ prefill all-reduce overlap
+    PREFILL_OVERLAP_MIN = 128   # tokens per chunk below which a half's GEMMs are too short to hide an all-reduce
+    _comm_stream: Optional[torch.cuda.Stream] = None
+
+    @property
+    def prefill_overlap(self) -> bool:
+        """TP > 1 prefill runs as two token halves whose all-reduces overlap the other half's GEMMs
+        (``K8S_PREFILL_OVERLAP=0`` turns it off; ``=cpu`` also splits on CPU, for the gloo tests)."""
+        env = os.environ.get("K8S_PREFILL_OVERLAP", "1")
+        if self.tp.world <= 1 or self.tp.simulate or env == "0" or not self.norm_folded:
+            return False
+        return self.device.type == "cuda" or env == "cpu"
+
+    def _layers_folded_overlap(self, h: torch.Tensor, attn, T0: int) -> torch.Tensor:
+        """``_layers_folded`` for TP > 1 prefill as two micro-batches (tokens [0, T0) and [T0, T)) on one
+        compute stream, with every all-reduce on a comm stream.  Per layer the compute stream issues
+        [QKV, attention, O] of half 0, then of half 1, then [gate/up, down] of half 0, then of half 1; each
+        branch's all-reduce (residual fused, as in ``_layers_folded``) waits only for its own O / down GEMM, so
+
+            AR(O0)    runs under  QKV1 + attention1 + O1
+            AR(O1)    runs under  gate/up0 + down0
+            AR(down0) runs under  gate/up1 + down1
+            AR(down1) runs under  QKV0 + attention0 + O0 of the next layer.
+
+        Half 1's attention reads the K/V half 0 wrote at the same layer (the compute stream orders them).
+        The collectives stay in one fixed order on one stream (every rank issues the same sequence, as one
+        communicator needs); nothing is allocated on the comm stream, and a tensor the comm stream touches
+        is released only after the compute stream has waited for that collective, so the caching allocator
+        cannot hand its memory to a later kernel early.  Captures into the prefill hipGraphs as a fork/join.
+        (SURVEY 2.6 P-COMM / north star "all-reduce overlapped with GEMMs".)"""
+        eps = self.cfg.rms_eps
+        gpu = h.is_cuda
+        if gpu:
+            cs = torch.cuda.current_stream(self.device)
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.Stream(self.device)
+            ms = self._comm_stream
+
+        def all_reduce(t: torch.Tensor, res: torch.Tensor):
+            if not gpu:
+                self.tp.all_reduce_(t, residual=res)
+                return None
+            ms.wait_stream(cs)
+            with torch.cuda.stream(ms):
+                self.tp.all_reduce_(t, residual=res)
+            ev = torch.cuda.Event()
+            ev.record(ms)
+            return ev
+
+        def wait(ev) -> None:
+            if ev is not None:
+                cs.wait_event(ev)
+
+        r = [h[:T0].clone(), h[T0:].clone()]
+        o: List[Optional[torch.Tensor]] = [None, None]
+        pend: list = [None, None]          # event after which r[i] holds the layer's output on the comm stream
+        for l, w in enumerate(self.layers):
+            ev_o = [None, None]
+            for i in (0, 1):
+                wait(pend[i])
+                o[i] = None                # the previous layer's o[i] was the residual of AR(down_i): released now
+                qkv = ops.linear_rms(r[i], w.wqkv, eps)
+                a = attn(l, qkv, i)
+                o[i] = ops.linear(a, w.wo)
+                ev_o[i] = all_reduce(o[i], r[i])     # o_i = r_i + attention branch
+            for i in (0, 1):
+                wait(ev_o[i])
+                g = ops.linear_rms(o[i], w.wgu, eps, ops.EPI_SWIGLU)
+                d = ops.linear(g, w.wdown)
+                pend[i] = all_reduce(d, o[i])        # d_i = o_i + MLP branch
+                r[i] = d                   # the old r[i] was read by AR(O_i), which the wait above covered
+        wait(pend[0])
+        wait(pend[1])
+        return torch.cat(r)
+
     def _logits_folded(self, r: torch.Tensor) -> torch.Tensor:
         logits = ops.linear_rms(r, self.lm_head, self.cfg.rms_eps, ops.EPI_F32)   # final norm folded: [S, Vs]
         return self.tp.all_gather_shards(logits)                               # [tp, S, Vs]
@@ -257,9 +333,13 @@ class LlamaModel:
 
     def forward_prefill(self, ids: torch.Tensor, positions: torch.Tensor, slot_mapping: torch.Tensor,
                         cu_q: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
-                        max_qlen: int, last_idx: torch.Tensor) -> torch.Tensor:
+                        max_qlen: int, last_idx: torch.Tensor, split: Optional[tuple] = None) -> torch.Tensor:
         """Varlen prefill (chunks of several sequences).  Returns gathered logits [tp, S, Vs] for
-        the token at ``last_idx`` of each sequence."""
+        the token at ``last_idx`` of each sequence.
+
+        ``split`` = ``(T0, half0, half1)`` with ``half = (cu_q, context_lens, block_tables, max_qlen)`` of the
+        tokens [0, T0) / [T0, T) (``split_prefill_meta``): TP > 1 runs the two halves as micro-batches whose
+        all-reduces overlap the other half's GEMMs (``_layers_folded_overlap``)."""
         T = ids.shape[0]
         kv = self.kv_cache
 
@@ -271,6 +351,21 @@ class LlamaModel:
             return a.view(T, self.nq * self.D)
 
         li = last_idx.long()
+        if split is not None and self.prefill_overlap:
+            T0 = split[0]
+            pieces = ((slice(0, T0), split[1]), (slice(T0, T), split[2]))
+
+            def attn_half(l: int, qkv: torch.Tensor, i: int) -> torch.Tensor:
+                sl, (cu, ctx, bt, mq) = pieces[i]
+                n = qkv.shape[0]
+                q = ops.rope_kv_write(qkv, self.cos_sin, kv[l, 0], kv[l, 1], self.nq, self.nkv, self.D,
+                                      positions=positions[sl], slot_mapping=slot_mapping[sl])
+                a = ops.paged_prefill_attention(q, kv[l, 0], kv[l, 1], cu, ctx, bt, self.scale, self.block_size,
+                                                max(1, mq))
+                return a.view(n, self.nq * self.D)
+
+            r = self._layers_folded_overlap(ops.embedding(ids, self.embed), attn_half, T0)
+            return self._logits_folded(r.index_select(0, li).contiguous())
         if self.norm_folded:
             r = self._layers_folded(ops.embedding(ids, self.embed), attn)
             return self._logits_folded(r.index_select(0, li).contiguous())

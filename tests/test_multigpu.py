@@ -109,6 +109,16 @@ def _model_and_engine(tp, res, preset="tiny-tp8"):
         res["logit_scale"] = float(full(lg1).float().abs().max())
         res["argmax_equal"] = bool(torch.equal(full(lg).argmax(-1).cpu(), full(lg1).argmax(-1).cpu()))
         del m1
+    # prefill as two micro-batches whose all-reduces run on the comm stream under the other half's GEMMs
+    # (a two-sequence chunk split inside sequence 0) against the same chunk unsplit
+    from test_prefill_overlap import _run_chunk
+
+    assert m.prefill_overlap
+    lg_a, kv_a = _run_chunk(m, 0)
+    lg_b, kv_b = _run_chunk(m, 80)
+    res["split_err"] = float((lg_a.float() - lg_b.float()).abs().max())
+    res["split_kv_err"] = float((kv_a.float() - kv_b.float()).abs().max())
+    res["split_scale"] = float(lg_a.float().abs().max())
     del m
     eng = build_engine(preset, tp=tp, device="cuda", max_batch=4, max_model_len=512, num_blocks=128, seed=1,
                        capture_nucleus=True)   # a top_p < 1 request below: the graphs with the nucleus passes
@@ -119,7 +129,20 @@ def _model_and_engine(tp, res, preset="tiny-tp8"):
     # one request alone: its prefill chunk replays a prefill graph (xGMI-only buckets at TP > 1)
     solo = eng.generate(["a single prompt prefilled by a graph"], [SamplingParams(max_tokens=4, temperature=0.0,
                                                                                   ignore_eos=True)])
-    res["tokens"] = [o.token_ids for o in outs] + [solo[0].token_ids]
+    # prompts of >= 128 tokens prefill as two overlapped micro-batches: alone (a prefill graph with the
+    # fork / join captured) and two at once (the eager varlen split)
+    long_p = " ".join(f"node-{i} cpu {i % 7} mem {i % 5}" for i in range(13))
+    assert len(eng.tok.encode(long_p)) >= 128
+    greedy = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    replays = eng.stats["prefill_graph_replays"]
+    lone = eng.generate([long_p], [greedy])
+    res["long_graph_replayed"] = eng.stats["prefill_graph_replays"] > replays
+    split_chunks = eng.stats["prefill_overlap_chunks"]
+    pair = eng.generate([" ".join(f"pod-{i} gpu {i % 3}" for i in range(12)),
+                         " ".join(f"rack-{i} disk {i % 9}" for i in range(12))], [greedy, greedy])
+    res["tokens"] = [o.token_ids for o in outs] + [solo[0].token_ids] + [lone[0].token_ids] + \
+        [o.token_ids for o in pair]
+    res["overlap_chunks"] = (split_chunks, eng.stats["prefill_overlap_chunks"])
     res["graph_replays"] = eng.stats["graph_replays"]
     res["prefill_graph_replays"] = eng.stats["prefill_graph_replays"]
     res["prefill_graphs"] = sorted(eng.prefill_graphs)
@@ -151,6 +174,11 @@ def _assert_model(res, world):
     assert all(res[r]["tokens"] == r0["tokens"] for r in range(world)), "ranks drew different tokens"
     assert r0["graph_replays"] > 0
     assert r0["prefill_graph_replays"] > 0, r0["prefill_graphs"]
+    assert r0["split_kv_err"] < 0.03, r0
+    assert r0["split_err"] < 0.02 * r0["split_scale"] + 0.02, r0
+    assert r0["long_graph_replayed"], r0["prefill_graphs"]
+    a, b = r0["overlap_chunks"]
+    assert a >= 1 and b >= a + 1, r0["overlap_chunks"]   # the graph chunk and the eager pair chunk were split
 
 
 @pytest.mark.parametrize("world", [8, 4])
