@@ -36,10 +36,6 @@ int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const f
 int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s);
 int k8s_quantize_act_fp8(void* q, float* scale, const void* x, int T, int K, hipStream_t s);
 int k8s_dequant_fp8_rows(void* w, const void* q, const float* scale, int N, int K, hipStream_t s);
-int k8s_skinny_supported(int M, int N_out, int K);
-long long k8s_skinny_workspace(int M, int N_out, int epi);
-int k8s_skinny_gemm(void* out, void* workspace, const void* x, const void* W, int M, int N_out, int K, int epi,
-                    int num_cus, hipStream_t s);
 int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi, hipStream_t s);
 int k8s_gemv_rms(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out, int K,
                  int epi, const void* res_in, void* res_out, float eps, hipStream_t s);
@@ -142,12 +138,6 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("dequant_fp8_rows", [](uintptr_t w, uintptr_t q, uintptr_t scale, int N, int K, int64_t s) {
     check(k8s_dequant_fp8_rows(P(w), P(q), P<float>(scale), N, K, S(s)), "dequant_fp8_rows");
-  });
-  m.def("skinny_supported", [](int M, int N, int K) { return k8s_skinny_supported(M, N, K) != 0; });
-  m.def("skinny_workspace", [](int M, int N, int epi) { return k8s_skinny_workspace(M, N, epi); });
-  m.def("skinny_gemm", [](uintptr_t out, uintptr_t ws, uintptr_t x, uintptr_t W, int M, int N, int K, int epi,
-                          int num_cus, int64_t s) {
-    check(k8s_skinny_gemm(P(out), P(ws), P(x), P(W), M, N, K, epi, num_cus, S(s)), "skinny_gemm");
   });
   m.def("gemv", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, int M, int N, int K, int epi,
                    int64_t s) { check(k8s_gemv(P(out), P(partial), P(x), P(W), M, N, K, epi, S(s)), "gemv"); });

@@ -258,7 +258,6 @@ GEMV_KERNEL_MAX_M = 8   # rows the GEMV kernels (gemv.hip) accept
 GEMV_MAX_M = int(os.environ.get("K8S_GEMV_MAX_M", "2"))
 if not 1 <= GEMV_MAX_M <= GEMV_KERNEL_MAX_M:
     raise ValueError(f"K8S_GEMV_MAX_M must be 1..{GEMV_KERNEL_MAX_M}")
-SKINNY_MAX_M = 64
 
 
 def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0, res_in=None,
@@ -290,35 +289,6 @@ def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0
     return out
 
 
-_NUM_CUS = {}
-
-
-def _num_cus(dev: torch.device) -> int:
-    i = dev.index if dev.index is not None else torch.cuda.current_device()
-    if i not in _NUM_CUS:
-        _NUM_CUS[i] = torch.cuda.get_device_properties(i).multi_processor_count
-    return _NUM_CUS[i]
-
-
-def _skinny(x: torch.Tensor, w: torch.Tensor, epi: int, out_dtype) -> torch.Tensor:
-    M, K = x.shape
-    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
-    out = torch.empty(M, N, dtype=out_dtype, device=x.device)
-    n_ws = native().skinny_workspace(M, N, epi)
-    ws = torch.empty(n_ws, dtype=F32, device=x.device) if n_ws else None
-    native().skinny_gemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, _chk(x, BF16, "x"),
-                         _chk(w, BF16, "w"), M, N, K, epi, _num_cus(x.device), -1)
-    del ws
-    return out
-
-
-# The MFMA skinny GEMM is opt-in until it beats hipBLASLt at every batched-decode shape
-# (profiles/kbench_skinny_*.txt); K8S_SKINNY=1 routes 8 < M <= 64 through it.
-SKINNY_ENABLED = os.environ.get("K8S_SKINNY", "0") == "1"
-
-
-def _use_skinny(M: int, w, K: int) -> bool:
-    return SKINNY_ENABLED and not _is_fp8(w) and GEMV_MAX_M < M <= SKINNY_MAX_M and K % 256 == 0
 
 
 # Row counts of the library GEMMs in the tuned table (engine/assets/tunableop_gfx950.csv, written by
@@ -595,8 +565,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
     elif GEMM_BACKEND != "library" and _mgemm_ok(w.shape[0], x2.shape[1], _is_fp8(w)) and out_dtype in (None, BF16, F32) \
             and mgemm_preferred(x2.shape[0], w.shape[0], x2.shape[1], epi, _is_fp8(w)):
         y = mgemm(x2.contiguous(), w, epi)
-    elif _use_skinny(x2.shape[0], w, x2.shape[1]):
-        y = _skinny(x2.contiguous(), w, epi, out_dtype or BF16)
     elif _is_fp8(w):
         y = _fp8_gemm(x2, w, out_dtype)
     else:
@@ -756,8 +724,6 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     elif GEMM_BACKEND != "library" and _mgemm_ok(w_gate_up.shape[0] // 2, x2.shape[1], _is_fp8(w_gate_up)) \
             and mgemm_preferred(x2.shape[0], w_gate_up.shape[0] // 2, x2.shape[1], EPI_SWIGLU, _is_fp8(w_gate_up)):
         y = mgemm(x2.contiguous(), w_gate_up, EPI_SWIGLU)
-    elif _use_skinny(x2.shape[0], w_gate_up, x2.shape[1]):
-        y = _skinny(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
     elif _is_fp8(w_gate_up):
         y = silu_mul(_fp8_gemm(x2, w_gate_up))
     else:

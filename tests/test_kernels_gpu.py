@@ -156,23 +156,6 @@ def test_gemv_swiglu(M, I, K):
     close(ops.linear_swiglu(x, w), want, 3e-2)
 
 
-@pytest.mark.parametrize("M", [9, 16, 17, 40, 64])
-@pytest.mark.parametrize("N,K", [(1280, 8192), (10240, 8192), (8192, 3584), (100, 256), (16032, 8192)])
-def test_skinny_mfma_gemm(M, N, K, monkeypatch):
-    """The opt-in MFMA skinny GEMM kernel (skinny_mfma.hip: stream-K, fp32 atomics; K8S_SKINNY=1, superseded by
-    mgemm on the default route), called directly, all epilogues."""
-    x, w = rnd(M, K), rnd(N, K, scale=0.05)
-    close(ops._skinny(x, w, ops.EPI_BF16, torch.bfloat16), ref.linear(x.cpu(), w.cpu()), 3e-2)
-    close(ops._skinny(x, w, ops.EPI_F32, torch.float32), ref.linear(x.cpu(), w.cpu(), torch.float32), 1e-2, 1e-3)
-
-
-@pytest.mark.parametrize("M", [12, 64])
-@pytest.mark.parametrize("I,K", [(3584, 8192), (128, 512), (28672, 8192)])
-def test_skinny_mfma_swiglu(M, I, K, monkeypatch):
-    x, w = rnd(M, K), rnd(2 * I, K, scale=0.05)
-    close(ops._skinny(x, w, ops.EPI_SWIGLU, torch.bfloat16), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)
-
-
 def test_prefill_linear_and_silu_mul():
     x, w = rnd(300, 1024), rnd(2 * 512, 1024, scale=0.05)
     close(ops.linear_swiglu(x, w), ref.linear_swiglu(x.cpu(), w.cpu()), 3e-2)

@@ -51,7 +51,6 @@ def main():
     dev = "cuda"
     H, I, V, nq, nkv, D = 8192, 28672 // a.tp, 128256 // a.tp, 64 // a.tp, max(1, 8 // a.tp), 128
     M = a.M
-    ops.SKINNY_ENABLED = True  # compare the MFMA skinny GEMM against hipBLASLt at M > 8
     bf = torch.bfloat16
     res = []
 
