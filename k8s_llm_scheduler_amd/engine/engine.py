@@ -302,7 +302,7 @@ class LLMEngine:
 
     def _overlap_split_at(self, T: int) -> int:
         """Token at which a TP > 1 prefill chunk of T tokens splits into two micro-batches (0: no split)."""
-        if T < self.model.PREFILL_OVERLAP_MIN or not self.model.prefill_overlap:
+        if T < self.model.prefill_overlap_min or not self.model.prefill_overlap:
             return 0
         return max(16, T // 2 // 16 * 16)
 

@@ -230,15 +230,23 @@ class LlamaModel:
         return r
 
     # ------------------------------------------------------------------ prefill all-reduce overlap
-    PREFILL_OVERLAP_MIN = 128   # tokens per chunk below which a half's GEMMs are too short to hide an all-reduce
+    # Chunks shorter than this many tokens are not split (``K8S_PREFILL_OVERLAP_MIN``).  Splitting streams every
+    # weight twice: at TP = 8 a 256-token chunk's four projections take 119 us per layer, its two 128-token halves
+    # 2 x 87 us (profiles/mgemm_vs_hipblaslt_*.txt), more than the two ~2 MiB all-reduces they would hide.  From about
+    # a thousand tokens up the all-reduces (16 MiB+ per projection) outweigh the extra weight pass.
     _comm_stream: Optional[torch.cuda.Stream] = None
+
+    @property
+    def prefill_overlap_min(self) -> int:
+        return int(os.environ.get("K8S_PREFILL_OVERLAP_MIN", "1024"))
 
     @property
     def prefill_overlap(self) -> bool:
         """TP > 1 prefill runs as two token halves whose all-reduces overlap the other half's GEMMs
-        (``K8S_PREFILL_OVERLAP=0`` turns it off; ``=cpu`` also splits on CPU, for the gloo tests)."""
+        (``K8S_PREFILL_OVERLAP=0`` turns it off; ``=cpu`` also splits on CPU, for the gloo tests; ``=sim`` also
+        splits a simulated TP rank, whose skipped collectives leave the split's own cost: tools/overlap_probe.py)."""
         env = os.environ.get("K8S_PREFILL_OVERLAP", "1")
-        if self.tp.world <= 1 or self.tp.simulate or env == "0" or not self.norm_folded:
+        if self.tp.world <= 1 or env == "0" or not self.norm_folded or (self.tp.simulate and env != "sim"):
             return False
         return self.device.type == "cuda" or env == "cpu"
 

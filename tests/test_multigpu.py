@@ -119,6 +119,7 @@ def _model_and_engine(tp, res, preset="tiny-tp8"):
     res["split_err"] = float((lg_a.float() - lg_b.float()).abs().max())
     res["split_kv_err"] = float((kv_a.float() - kv_b.float()).abs().max())
     res["split_scale"] = float(lg_a.float().abs().max())
+    res["split_kv_scale"] = float(kv_a.float().abs().max())
     del m
     eng = build_engine(preset, tp=tp, device="cuda", max_batch=4, max_model_len=512, num_blocks=128, seed=1,
                        capture_nucleus=True)   # a top_p < 1 request below: the graphs with the nucleus passes
@@ -174,7 +175,8 @@ def _assert_model(res, world):
     assert all(res[r]["tokens"] == r0["tokens"] for r in range(world)), "ranks drew different tokens"
     assert r0["graph_replays"] > 0
     assert r0["prefill_graph_replays"] > 0, r0["prefill_graphs"]
-    assert r0["split_kv_err"] < 0.03, r0
+    # the halves' GEMMs have other row counts (other tiles / k-split orders): bf16 rounding, not a layout error
+    assert r0["split_kv_err"] < 0.02 * r0["split_kv_scale"] + 0.02, r0
     assert r0["split_err"] < 0.02 * r0["split_scale"] + 0.02, r0
     assert r0["long_graph_replayed"], r0["prefill_graphs"]
     a, b = r0["overlap_chunks"]
@@ -186,11 +188,14 @@ def test_tp_rehearsal_ranks_share_one_gpu(world):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = run_ranks(_rehearsal_rank, world, env={"K8S_TP_BACKEND": "gloo", "K8S_TP_COMM": "xgmi",
-                                                 "K8S_TEST_MODEL": "1" if world == 8 else "0"}, timeout_s=480)
+                                                 "K8S_TEST_MODEL": "1" if world == 8 else "0",
+                                                 "K8S_PREFILL_OVERLAP_MIN": "128"}, timeout_s=480)
     _assert_model(res, world)
     if world == 8:
         print(f"TP=8 rehearsal (8 ranks, one GPU): max |d logit| prefill {res[0]['prefill_err']:.3g} "
-              f"decode {res[0]['decode_err']:.3g} (scale {res[0]['logit_scale']:.3g}), tokens equal on all ranks")
+              f"decode {res[0]['decode_err']:.3g} (scale {res[0]['logit_scale']:.3g}), tokens equal on all ranks; "
+              f"overlapped prefill vs unsplit: max |d logit| {res[0]['split_err']:.3g}, |d kv| {res[0]['split_kv_err']:.3g} "
+              f"(kv scale {res[0]['split_kv_scale']:.3g}), overlapped chunks {res[0]['overlap_chunks']}")
 
 
 def _multi_gpu_rank(rank, world):
@@ -218,5 +223,5 @@ def _multi_gpu_rank(rank, world):
 def test_multi_gpu_tp_rccl_and_xgmi(world):
     if not torch.cuda.is_available() or torch.cuda.device_count() < world:
         pytest.skip(f"needs {world} GPUs (found {torch.cuda.device_count() if torch.cuda.is_available() else 0})")
-    res = run_ranks(_multi_gpu_rank, world, timeout_s=600)
+    res = run_ranks(_multi_gpu_rank, world, env={"K8S_PREFILL_OVERLAP_MIN": "128"}, timeout_s=600)
     _assert_model(res, world)

@@ -97,7 +97,7 @@ def _cpu_rank(rank, world):
 
 
 def test_split_prefill_matches_unsplit_tp2_gloo():
-    res = run_ranks(_cpu_rank, 2, env={"K8S_PREFILL_OVERLAP": "cpu"}, timeout_s=300)
+    res = run_ranks(_cpu_rank, 2, env={"K8S_PREFILL_OVERLAP": "cpu", "K8S_PREFILL_OVERLAP_MIN": "128"}, timeout_s=300)
     for r in range(2):
         (d_lg, d_kv, scale), (split_toks, plain_toks) = res[r]
         assert d_kv <= 1e-2, res[r]                     # every token's K/V written once, at its own slot

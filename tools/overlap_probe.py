@@ -62,6 +62,47 @@ def _rank(rank, world):
     return {k: min(v) for k, v in out.items()}
 
 
+def simulated(a):
+    """One TP rank's shapes in this process, collectives skipped: what splitting a chunk costs by itself
+    (two half-size passes over every weight, the comm-stream fork / join), per chunk length."""
+    import torch
+
+    from k8s_llm_scheduler_amd.engine.engine import split_prefill_meta
+    from k8s_llm_scheduler_amd.models.config import PRESETS
+    from k8s_llm_scheduler_amd.models.llama import LlamaModel
+    from k8s_llm_scheduler_amd.parallel import TPGroup
+
+    os.environ["K8S_PREFILL_OVERLAP"] = "sim"
+    cfg = dataclasses.replace(PRESETS["llama-3.3-70b"], num_layers=a.layers)
+    tmax = max(a.sweep)
+    m = LlamaModel(cfg, TPGroup(0, a.simulate_tp, None, "none", simulate=True), device="cuda", seed=1,
+                   max_model_len=max(4096, tmax))
+    bs = 16
+    m.allocate_kv(tmax // bs + 2, bs)
+    i32 = lambda x: torch.tensor(x, dtype=torch.int32, device="cuda")   # noqa: E731
+    rows = []
+    for T in a.sweep:
+        ids, pos, slots = i32([(7 * i) % 120000 + 5 for i in range(T)]), i32(list(range(T))), i32(list(range(T)))
+        bt = i32([list(range(T // bs + 1))])
+        halves = [(i32(c), i32(x), bt, max(q - p for p, q in zip(c, c[1:])))
+                  for c, x, _ in split_prefill_meta([0, T], [T], T // 2)]
+        res = {}
+        for name, sp in (("unsplit", None), ("split", (T // 2, halves[0], halves[1]))) * 2:
+            ts = []
+            for it in range(a.reps + 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                m.forward_prefill(ids, pos, slots, i32([0, T]), i32([T]), bt, T, i32([T - 1]), split=sp)
+                torch.cuda.synchronize()
+                if it:
+                    ts.append((time.perf_counter() - t0) * 1e3)
+            res[name] = min(res.get(name, 1e9), statistics.median(ts))
+        rows.append({"tokens": T, "ms_unsplit": round(res["unsplit"], 3), "ms_split": round(res["split"], 3),
+                     "split_cost_us_per_layer": round((res["split"] - res["unsplit"]) * 1e3 / a.layers, 1)})
+        print(json.dumps({"probe": "prefill_split_cost_simulated", "tp": a.simulate_tp, "layers": a.layers, **rows[-1]}),
+              flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=2)
@@ -69,10 +110,15 @@ def main():
     ap.add_argument("--tokens", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--modes", default="unsplit,split", help="comma list of unsplit / split")
+    ap.add_argument("--simulate-tp", type=int, default=0, help="one rank of this TP degree, no collectives")
+    ap.add_argument("--sweep", type=int, nargs="+", default=[256, 1024, 2048, 4096, 8192])
     a = ap.parse_args()
+    if a.simulate_tp:
+        return simulated(a)
     from mp_harness import run_ranks
 
     res = run_ranks(_rank, a.world, env={"K8S_TP_BACKEND": "gloo", "K8S_TP_COMM": "xgmi", "K8S_XGMI_MAX_BYTES": str(4 << 20),
+                                         "K8S_PREFILL_OVERLAP_MIN": "0",
                                          "OVERLAP_PROBE_ARGS": json.dumps(vars(a))}, timeout_s=600)
     worst = {k: round(max(res[r][k] for r in res), 3) for k in res[0]}
     print(json.dumps({"probe": "prefill_allreduce_overlap", "world": a.world, "layers": a.layers, "tokens": a.tokens,
