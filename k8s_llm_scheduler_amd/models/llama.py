@@ -230,15 +230,15 @@ class LlamaModel:
         return r
 
     # ------------------------------------------------------------------ prefill all-reduce overlap
-    # Chunks shorter than this many tokens are not split (``K8S_PREFILL_OVERLAP_MIN``).  Splitting streams every
-    # weight twice: at TP = 8 a 256-token chunk's four projections take 119 us per layer, its two 128-token halves
-    # 2 x 87 us (profiles/mgemm_vs_hipblaslt_*.txt), more than the two ~2 MiB all-reduces they would hide.  From about
-    # a thousand tokens up the all-reduces (16 MiB+ per projection) outweigh the extra weight pass.
+    # Chunks shorter than this many tokens are not split (``K8S_PREFILL_OVERLAP_MIN``).  Splitting costs a second,
+    # half-size pass over every weight: measured at one TP = 8 rank's shapes (profiles/prefill_split_cost_tp8sim.jsonl)
+    # +112 us per layer at 256 tokens, +172 at 2048, +28 at 8192, while the two all-reduces it hides grow with the
+    # chunk (2 x 4 MiB two-shot xGMI at 256 tokens: well under the cost; 2 x 32 MiB RCCL at 2048: several times it).
     _comm_stream: Optional[torch.cuda.Stream] = None
 
     @property
     def prefill_overlap_min(self) -> int:
-        return int(os.environ.get("K8S_PREFILL_OVERLAP_MIN", "1024"))
+        return int(os.environ.get("K8S_PREFILL_OVERLAP_MIN", "2048"))
 
     @property
     def prefill_overlap(self) -> bool:
