@@ -219,6 +219,7 @@ def main() -> int:
         "prefill_ms_per_decision": round(1000 * st["prefill_time"] / max(1, args.steps * args.batch), 2),
         "prefill_tokens_per_decision": round(st["prefill_tokens"] / max(1, args.steps * args.batch), 1),
         "prefill_graph_replays": st.get("prefill_graph_replays", 0),
+        "prefill_overlap_chunks": st.get("prefill_overlap_chunks", 0),
         "fallback_rate": round(fallbacks / (args.steps * args.batch), 3),
         "init_s": round(init_s, 1),
         "tp_comm": tp.comm_info,
