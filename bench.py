@@ -65,6 +65,8 @@ def main() -> int:
                     help="serving mode: pods arrive as a Poisson process at this rate (pods/s) into the scheduler "
                          "in continuous mode on an in-memory apiserver; reports detect->bind latency "
                          "(--steps pods after --warmup pods; single rank)")
+    ap.add_argument("--speculative", type=int, default=0,
+                    help="prompt-lookup speculative decoding: drafted tokens per step (engine.speculative_tokens)")
     ap.add_argument("--top-p", type=float, default=1.0,
                     help="nucleus sampling (the reference sends no top_p: provider default 1.0); < 1 captures the "
                          "decode graphs with the top-p passes")
@@ -113,7 +115,7 @@ def main() -> int:
                        num_blocks=max(args.batch, 2) * (per_seq // bs + 2) + 64,
                        max_model_len=args.max_model_len, cuda_graphs=not args.no_graphs,
                        prefix_caching=not args.no_prefix_cache, capture=False, decode_chunk=8,
-                       weight_dtype=args.dtype)
+                       weight_dtype=args.dtype, speculative_tokens=args.speculative)
     progress("engine built")
     if eng.use_graphs:
         eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= max(1, args.batch)] or [1],
@@ -220,6 +222,8 @@ def main() -> int:
         "prefill_tokens_per_decision": round(st["prefill_tokens"] / max(1, args.steps * args.batch), 1),
         "prefill_graph_replays": st.get("prefill_graph_replays", 0),
         "prefill_overlap_chunks": st.get("prefill_overlap_chunks", 0),
+        "speculative": {"tokens": args.speculative, "steps": st.get("spec_steps", 0),
+                        "drafted": st.get("spec_drafted", 0), "accepted": st.get("spec_accepted", 0)},
         "fallback_rate": round(fallbacks / (args.steps * args.batch), 3),
         "init_s": round(init_s, 1),
         "tp_comm": tp.comm_info,

@@ -108,6 +108,7 @@ class EngineSection:
     max_prefill_tokens: int = 8192     # chunked-prefill token budget per step
     cuda_graphs: bool = True
     prefix_caching: bool = True
+    speculative_tokens: int = 0        # prompt-lookup speculative decoding: draft tokens per step (0 = off)
     ignore_eos: bool = False
     stop_on_json_close: bool = True
     fault_injection: str = "none"      # chaos hook: none | raise:<rate> | hang:<rate> | garbage:<rate>

@@ -468,19 +468,12 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
   if (splits > 1 && partial == nullptr) return -3;
   float* part = splits > 1 ? (float*)partial : nullptr;
   const int rpw = gemv_rpw(M, N_out, epi, mode);
-  // KW: waves per row set.  Split a row set's K over 2 or 4 waves while N alone leaves fewer
-  // than ~1024 workgroups and every wave keeps >= 2 chunks per lane (K8S_GEMV_KW overrides).
+  // KW: waves per row set (K8S_GEMV_KW = 2 / 4 splits a row set's K over that many waves).  One wave per row
+  // set is the default: the two-wave split the small-N projections (TP = 8 QKV, LM head) used to take measured
+  // slower end to end (TP = 8 shapes 4.28 -> 4.26 ms/token with one wave, 8B and TP = 1 unchanged,
+  // profiles/gemv_kw_ab.txt).
   static const int kw_env = [] { const char* e = getenv("K8S_GEMV_KW"); return e ? atoi(e) : 0; }();
-  const int nch_split = ks / (fp8 ? 16 : 8);
-  int kw = 1;
-  if (kw_env == 1 || kw_env == 2 || kw_env == 4) {
-    kw = kw_env;
-  } else {
-    // small N: two waves per row set (one weight round trip per wave); the norm variants then
-    // run 8-wave workgroups so the prologue is not repeated per extra workgroup
-    const int wg1 = (N_out + 4 * rpw - 1) / (4 * rpw) * splits;
-    if (wg1 < 512 && nch_split >= 256 && (mode == 0 || M <= 4)) kw = 2;
-  }
+  const int kw = (kw_env == 2 || kw_env == 4) ? kw_env : 1;
   // The norm variants keep 4 row sets per workgroup when they split K (8 waves, 512 threads):
   // the per-workgroup norm prologue is then shared by twice the waves instead of being repeated.
   const int nt = (mode != 0 && kw == 2 && M <= 4) ? 512 : 256;

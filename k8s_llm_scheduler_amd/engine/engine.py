@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import itertools
 import logging
+from array import array
 import math
 import os
 import random
@@ -75,6 +76,32 @@ def split_prefill_meta(cu: Sequence[int], ctx: Sequence[int], T0: int) -> tuple:
     return halves
 
 
+SPEC_MAX_BATCH = 8   # speculative steps only while at most this many sequences decode (drafting and the eager
+                     # verify forward are per-step host work; larger batches keep the captured decode graphs)
+
+
+def ngram_draft(seq: Sequence[int], k: int, n_max: int = 3) -> List[int]:
+    """Prompt-lookup draft: the up to ``k`` tokens that followed the most recent earlier occurrence of the
+    sequence's last n tokens (n = n_max .. 1, longest match first).  The search runs over the int32 bytes of the
+    sequence (``bytes.rfind``), so drafting a 700-token context costs microseconds, not a Python scan."""
+    L = len(seq)
+    if k <= 0 or L < 2:
+        return []
+    buf = array("i", seq).tobytes()
+    for n in range(min(n_max, L - 1), 0, -1):
+        pat = buf[(L - n) * 4:]           # the last n tokens
+        end = (L - 1) * 4                 # a match must leave at least one token after it
+        while end >= len(pat):
+            at = buf.rfind(pat, 0, end)
+            if at < 0:
+                break
+            if at % 4 == 0:               # token-aligned
+                s0 = at // 4 + n
+                return list(seq[s0:s0 + k])
+            end = at + len(pat) - 1       # misaligned hit: look further left
+    return []
+
+
 @dataclass
 class Request:
     rid: int
@@ -113,8 +140,10 @@ class LLMEngine:
                  num_blocks: Optional[int] = None, kv_cache_gb: float = 0.0, kv_cache_fraction: float = 0.85,
                  max_model_len: Optional[int] = None, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
                  prefix_caching: bool = True, decode_chunk: int = 4, seed: int = 0, metrics=None,
-                 control=None, capture_nucleus: bool = False):
+                 control=None, capture_nucleus: bool = False, speculative_tokens: int = 0):
         self.model = model
+        # prompt-lookup speculative decoding (_spec_decode): drafted tokens per step, 0 = off
+        self.speculative_tokens = max(0, int(speculative_tokens))
         # also capture decode graphs with the top-p passes (config llm.top_p < 1); otherwise chunks
         # holding a top_p < 1 request decode eagerly
         self.capture_nucleus = capture_nucleus
@@ -181,7 +210,7 @@ class LLMEngine:
         self.finished_log: Deque[tuple] = deque(maxlen=4096)
         self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "graph_replays": 0, "prefill_graph_replays": 0, "prefill_overlap_chunks": 0, "prefill_time": 0.0,
-                      "decode_time": 0.0}
+                      "decode_time": 0.0, "spec_steps": 0, "spec_drafted": 0, "spec_accepted": 0}
 
     # ------------------------------------------------------------------ device state
     def _alloc_state(self) -> None:
@@ -560,12 +589,12 @@ class LLMEngine:
             self.model.tp.check_health()
         self.stats["prefill_time"] += time.perf_counter() - t0
 
-    def _decode(self) -> List[Request]:
+    def _decode(self, max_steps: Optional[int] = None) -> List[Request]:
         if not self.running:
             return []
         remaining = min(r.params.max_tokens - len(r.output_ids) - (1 if not r.output_ids else 0)
                         for r in self.running.values())
-        steps = max(1, min(self.decode_chunk, remaining))
+        steps = max(1, min(self.decode_chunk if max_steps is None else max_steps, remaining))
         B = self._bucket(max(self.running) + 1)
         # context length reached by the end of this chunk decides the graph variant
         top = max(len(r.prompt_ids) + max(len(r.output_ids), 1) for r in self.running.values()) + steps
@@ -604,6 +633,105 @@ class LLMEngine:
             elif len(r.output_ids) >= r.params.max_tokens:
                 self._finish(r, "length")
                 finished.append(r)
+        if self.metrics is not None:
+            self.metrics.engine_tokens(sum(len(r.output_ids) for r in finished), self.kv_utilization())
+        return finished
+
+    # ------------------------------------------------------------------ speculative decoding
+    def _spec_ok(self) -> bool:
+        return (self.speculative_tokens > 0 and 0 < len(self.running) <= SPEC_MAX_BATCH
+                and all(r.params.forced_output_ids is None for r in self.running.values()))
+
+    def _emit(self, r: Request, tkn: int) -> None:
+        """Append one generated token to ``r`` with the stop checks of the decode path."""
+        r.output_ids.append(tkn)
+        self.stats["decode_tokens"] += 1
+        if not self._stopped(r, tkn) and len(r.output_ids) >= r.params.max_tokens:
+            self._finish(r, "length")
+
+    def _spec_decode(self) -> List[Request]:
+        """One prompt-lookup speculative step for every running sequence (no counterpart in the reference, whose
+        provider decodes; SURVEY 3.6 decode loop).  Each sequence feeds its last token plus up to
+        ``speculative_tokens`` drafted ones (``ngram_draft`` over prompt + answer) through ONE varlen forward over
+        the paged cache (``forward_prefill`` with logits at every row), the sampler draws the token after every
+        row with the counter of that position -- exactly what the one-token decode step would draw there -- and
+        the longest prefix of drafts equal to those draws is accepted, plus the first draw that differs.  So the
+        answer is the non-speculative answer (up to the kernels' rounding), in fewer forwards when the drafts hit:
+        JSON keys and node names the model copies from the prompt.  K/V written for rejected drafts lies beyond
+        the new context length and is overwritten by the next step.  Every TP rank drafts from the same host
+        state and draws the same tokens, so the ranks stay in lock-step without an exchange."""
+        t0 = time.perf_counter()
+        finished: List[Request] = []
+        dev = self.device
+        fresh = [r for r in self.running.values() if not r.output_ids]
+        if fresh:                         # first tokens, sampled by the prefill
+            first = self.s_hist[:, 0].cpu()
+            for r in fresh:
+                self._emit(r, int(first[r.slot]))
+                if r.finished:
+                    finished.append(r)
+        rows = []
+        for r in list(self.running.values()):
+            seq = r.prompt_ids + r.output_ids
+            p = len(seq) - 1              # position of the last token, whose K/V is not in the cache yet
+            k = min(self.speculative_tokens, r.params.max_tokens - len(r.output_ids) - 1,
+                    self.max_model_len - len(seq))
+            rows.append((r, [seq[-1]] + ngram_draft(seq, k), p))
+        if rows and all(len(fed) == 1 for _, fed, _ in rows):
+            # nothing to verify: one step of the captured decode graph (the host stays current for drafting)
+            self.stats["decode_time"] += time.perf_counter() - t0
+            return finished + self._decode(max_steps=1)
+        if rows:
+            bs = self.block_size
+            ids, pos, slots, cu, ctx = [], [], [], [0], []
+            temp, top_p, seeds, ctr = [], [], [], []
+            bt = torch.zeros(len(rows), self.max_blocks_per_seq, dtype=torch.int32)
+            for i, (r, toks, p) in enumerate(rows):
+                n = len(toks)
+                ids += toks
+                pos += range(p, p + n)
+                slots += [r.blocks[q // bs] * bs + q % bs for q in range(p, p + n)]
+                cu.append(cu[-1] + n)
+                ctx.append(p + n)
+                bt[i, :len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
+                temp += [r.params.temperature] * n
+                top_p += [r.params.top_p] * n
+                seeds += [r.seed] * n
+                ctr += range(p + 1, p + n + 1)     # the decode step's sampler counter: the context length
+            t = lambda x, dt=torch.int32: torch.tensor(x, dtype=dt).to(dev, non_blocking=True)   # noqa: E731
+            logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx), bt.to(dev, non_blocking=True),
+                                                max(len(x[1]) for x in rows), t(list(range(len(ids)))))
+            toks = ops.sample(logits, t(temp, torch.float32), t(top_p, torch.float32), t(seeds), t(ctr),
+                              shards=logits.shape[0], nucleus=self._wants_nucleus(r for r, _, _ in rows))
+            self.model.tp.snapshot_health()
+            drawn = toks.cpu().tolist()   # syncs the stream
+            self.model.tp.check_health()
+            self.stats["spec_steps"] += 1
+            i = 0
+            for r, fed, p in rows:
+                n = len(fed)
+                emit = []
+                for j in range(n):
+                    emit.append(drawn[i + j])
+                    if j + 1 >= n or fed[j + 1] != drawn[i + j]:
+                        break
+                i += n
+                self.stats["spec_drafted"] += n - 1
+                self.stats["spec_accepted"] += len(emit) - 1
+                for tkn in emit:
+                    self._emit(r, tkn)
+                    if r.finished:
+                        break
+                if r.finished:
+                    finished.append(r)
+                    continue
+                # device decode state of the slot, as the one-token decode path leaves it
+                slot = r.slot
+                self.s_tokens[slot] = r.output_ids[-1]
+                self.s_ctx[slot] = len(r.prompt_ids) + len(r.output_ids)
+                self.s_steps[slot] = len(r.output_ids)
+        self.stats["decode_steps"] += 1
+        self.stats["decode_time"] += time.perf_counter() - t0
         if self.metrics is not None:
             self.metrics.engine_tokens(sum(len(r.output_ids) for r in finished), self.kv_utilization())
         return finished
@@ -674,6 +802,8 @@ class LLMEngine:
                 # first decode, so the batch decodes in lock-step (no extra tail of decode steps)
                 return []
             with trace("engine.decode"):
+                if self._spec_ok():
+                    return self._spec_decode()
                 return self._decode()
 
     def serve_worker(self) -> None:
