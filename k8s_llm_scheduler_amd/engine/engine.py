@@ -76,6 +76,7 @@ def split_prefill_meta(cu: Sequence[int], ctx: Sequence[int], T0: int) -> tuple:
     return halves
 
 
+SPEC_GRAPH_T = 8     # rows of the captured single-sequence verify forward (last token + up to 7 drafts)
 SPEC_MAX_BATCH = 8   # speculative steps only while at most this many sequences decode (drafting and the eager
                      # verify forward are per-step host work; larger batches keep the captured decode graphs)
 
@@ -210,7 +211,8 @@ class LLMEngine:
         self.finished_log: Deque[tuple] = deque(maxlen=4096)
         self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "graph_replays": 0, "prefill_graph_replays": 0, "prefill_overlap_chunks": 0, "prefill_time": 0.0,
-                      "decode_time": 0.0, "spec_steps": 0, "spec_drafted": 0, "spec_accepted": 0}
+                      "decode_time": 0.0, "spec_steps": 0, "spec_graph_replays": 0, "spec_drafted": 0,
+                      "spec_accepted": 0}
 
     # ------------------------------------------------------------------ device state
     def _alloc_state(self) -> None:
@@ -230,6 +232,7 @@ class LLMEngine:
         Tm = PREFILL_GRAPH_BUCKETS[-1]
         self.p_packed = torch.zeros(3 * Tm + 4 + _P_SPLIT, **i32)
         self.p_bt = torch.zeros(1, self.max_blocks_per_seq, **i32)
+        self.v_last = torch.arange(SPEC_GRAPH_T, **i32)       # the verify graph's logits rows: all of them
 
     def _ctx_classes(self) -> List[int]:
         """Context-length classes with their own decode graph: contexts <= 1024 tokens (one
@@ -301,6 +304,22 @@ class LLMEngine:
                 if self._graph_pool is None:
                     self._graph_pool = g.pool()
                 self.prefill_graphs[Tb] = (g, logits)
+        if self.speculative_tokens and self.speculative_tokens < SPEC_GRAPH_T and self.spec_graph is None \
+                and self._prefill_bucket_capturable(SPEC_GRAPH_T):
+            # one sequence's verify forward (_spec_decode): SPEC_GRAPH_T rows, logits at every row
+            Tb = SPEC_GRAPH_T
+            self._fill_prefill_state([0] * Tb, list(range(Tb)), [self.scratch_slot] * Tb, Tb, [0], Tb)
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(stream):
+                self._spec_graph_body()
+            torch.cuda.current_stream(self.device).wait_stream(stream)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._graph_pool, stream=stream):
+                logits = self._spec_graph_body()
+            if self._graph_pool is None:
+                self._graph_pool = g.pool()
+            self.spec_graph = (g, logits)
         torch.cuda.synchronize(self.device)
 
     def prefill_graphs_enabled(self) -> bool:
@@ -334,6 +353,12 @@ class LLMEngine:
         if T < self.model.prefill_overlap_min or not self.model.prefill_overlap:
             return 0
         return max(16, T // 2 // 16 * 16)
+
+    spec_graph: Optional[tuple] = None   # (graph, logits [tp, SPEC_GRAPH_T, Vs]) of the single-sequence verify forward
+
+    def _spec_graph_body(self) -> torch.Tensor:
+        ids, pos, slots, cu, ctx, _ = self._p_views(SPEC_GRAPH_T)
+        return self.model.forward_prefill(ids, pos, slots, cu, ctx, self.p_bt, SPEC_GRAPH_T, self.v_last)
 
     def _prefill_graph_body(self, Tb: int) -> torch.Tensor:
         ids, pos, slots, cu, ctx, last = self._p_views(Tb)
@@ -699,8 +724,21 @@ class LLMEngine:
                 seeds += [r.seed] * n
                 ctr += range(p + 1, p + n + 1)     # the decode step's sampler counter: the context length
             t = lambda x, dt=torch.int32: torch.tensor(x, dtype=dt).to(dev, non_blocking=True)   # noqa: E731
-            logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx), bt.to(dev, non_blocking=True),
-                                                max(len(x[1]) for x in rows), t(list(range(len(ids)))))
+            if len(rows) == 1 and self.spec_graph is not None and len(ids) <= SPEC_GRAPH_T:
+                # one sequence: replay the captured verify forward (padding rows write K/V to the scratch slot
+                # and their draws are ignored)
+                r0, fed0, p0 = rows[0]
+                pad = SPEC_GRAPH_T - len(ids)
+                self._fill_prefill_state(ids, pos, slots, ctx[0], r0.blocks, SPEC_GRAPH_T)
+                graph, logits = self.spec_graph
+                graph.replay()
+                self.stats["spec_graph_replays"] += 1
+                temp, top_p, seeds, ctr = temp + temp[-1:] * pad, top_p + top_p[-1:] * pad, seeds + seeds[-1:] * pad, \
+                    ctr + [1] * pad
+            else:
+                logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx),
+                                                    bt.to(dev, non_blocking=True), max(len(x[1]) for x in rows),
+                                                    t(list(range(len(ids)))))
             toks = ops.sample(logits, t(temp, torch.float32), t(top_p, torch.float32), t(seeds), t(ctr),
                               shards=logits.shape[0], nucleus=self._wants_nucleus(r for r, _, _ in rows))
             self.model.tp.snapshot_health()

@@ -38,3 +38,20 @@ def test_speculative_gpu_matches_graph_decode(temperature):
     assert got == want
     st = spec.stats
     assert st["spec_accepted"] >= 60 and st["spec_steps"] <= 20, st   # 120 tokens in <= 20 verify forwards
+
+
+def test_speculative_gpu_single_sequence_replays_verify_graph():
+    """One sequence: the verify forward replays its captured graph (SPEC_GRAPH_T rows, padding to the scratch
+    slot) and the answer still equals the decode graphs' answer."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_scheduler_amd.engine import SamplingParams
+
+    params = SamplingParams(max_tokens=37, temperature=0.0, ignore_eos=True)
+    want = [o.token_ids for o in _engine(0, True).generate([[3, 4, 5, 6, 7]], params)]
+    spec = _engine(4, True)
+    assert spec.spec_graph is not None
+    got = [o.token_ids for o in spec.generate([[3, 4, 5, 6, 7]], params)]
+    assert got == want
+    st = spec.stats
+    assert st["spec_graph_replays"] >= 5 and st["spec_accepted"] >= 20, st

@@ -58,7 +58,7 @@ def main():
             st = eng.stats
             row = {"probe": "speculative", "preset": a.preset, "workload": workload, "spec_tokens": spec,
                    "ms_per_answer": round(best * 1e3, 1), "tokens": len(toks),
-                   "verify_forwards": st["spec_steps"], "drafted": st["spec_drafted"], "accepted": st["spec_accepted"]}
+                   "verify_forwards": st["spec_steps"], "verify_graph_replays": st["spec_graph_replays"], "drafted": st["spec_drafted"], "accepted": st["spec_accepted"]}
             out.append((workload, spec, toks))
             print(json.dumps(row), flush=True)
             del eng
