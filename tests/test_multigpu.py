@@ -147,6 +147,19 @@ def _model_and_engine(tp, res, preset="tiny-tp8"):
     res["graph_replays"] = eng.stats["graph_replays"]
     res["prefill_graph_replays"] = eng.stats["prefill_graph_replays"]
     res["prefill_graphs"] = sorted(eng.prefill_graphs)
+    del eng
+    # speculative decoding at TP > 1: every rank drafts from the same host state, verifies through the captured
+    # verify graph (its all-reduces on xGMI) and must accept the same drafts
+    from k8s_llm_scheduler_amd.engine.engine import LLMEngine
+    from k8s_llm_scheduler_amd.engine.tokenizer import Tokenizer
+    from test_speculative_cpu import CycleModel
+
+    cm = CycleModel(PRESETS[preset], tp, device="cuda", seed=1, max_model_len=512)
+    seng = LLMEngine(cm, Tokenizer(None, model_vocab=cm.cfg.vocab), max_batch=4, num_blocks=64, max_model_len=512,
+                     seed=1, speculative_tokens=4)
+    seng.capture_graphs()
+    sp = seng.generate([[3, 4, 5, 6, 7]], SamplingParams(max_tokens=30, temperature=0.0, ignore_eos=True))
+    res["spec"] = (sp[0].token_ids, seng.stats["spec_graph_replays"], seng.stats["spec_accepted"])
 
 
 def _rehearsal_rank(rank, world):
@@ -179,6 +192,9 @@ def _assert_model(res, world):
     assert r0["split_kv_err"] < 0.02 * r0["split_kv_scale"] + 0.02, r0
     assert r0["split_err"] < 0.02 * r0["split_scale"] + 0.02, r0
     assert r0["long_graph_replayed"], r0["prefill_graphs"]
+    toks, replays, accepted = r0["spec"]
+    assert all(res[r]["spec"] == r0["spec"] for r in range(world)), "ranks diverged under speculative decoding"
+    assert toks[:6] == [10, 11, 12, 13, 14, 10] and replays > 0 and accepted >= 15, r0["spec"]
     a, b = r0["overlap_chunks"]
     assert a >= 1 and b >= a + 1, r0["overlap_chunks"]   # the graph chunk and the eager pair chunk were split
 
