@@ -149,6 +149,9 @@ def cmd_run(args, cfg: Config) -> int:
 
         api = RestKubeAPI(KubeConnection.auto(args.kubeconfig))
     sched = build_scheduler(cfg, api, backend, metrics)
+    if engine is not None:
+        metrics.add_health_source("engine", engine.health_probe)
+    metrics.add_health_source("scheduler", lambda: (True, bool(sched.running), {"stats": sched.get_stats()}))
 
     async def main():
         task = asyncio.create_task(sched.start())

@@ -109,6 +109,9 @@ class EngineSection:
     cuda_graphs: bool = True
     prefix_caching: bool = True
     speculative_tokens: int = 0        # prompt-lookup speculative decoding: draft tokens per step (0 = off)
+    decode_chunk: int = 4              # decode graph replays per engine step (stops are detected on the device)
+    watchdog_s: float = 0.0            # bound on any host wait for device results; 0 == llm.timeout
+    on_unrecoverable: str = "exit"     # exit (pod restarts, code 70) | stay (not ready) when recovery fails
     ignore_eos: bool = False
     stop_on_json_close: bool = True
     fault_injection: str = "none"      # chaos hook: none | raise:<rate> | hang:<rate> | garbage:<rate>

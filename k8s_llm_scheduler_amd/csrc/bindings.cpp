@@ -71,6 +71,18 @@ int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, int cfg, int 
 int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs, const float* wsc,
               int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax, const void* res, int rms,
               float eps, hipStream_t s);
+int k8s_pgemm4_num_configs();
+int k8s_pgemm4_config(int cfg, int* bp, int* bq, int* lds_bytes);
+int k8s_pgemm4_plan(int M, int N_out, int K, int epi, int cfg, int splits, int* nwg, long long* slab_elems);
+int k8s_pgemm4(void* out, float* slab, const void* x, const void* W, int M, int N_out, int K, int epi, int cfg,
+               int splits, int group_m, const void* res, int rms, float eps, hipStream_t s);
+int k8s_pgemm_num_configs();
+int k8s_pgemm_config(int cfg, int* bp, int* bq, int* lds_bytes);
+int k8s_pgemm_plan(int M, int N_out, int K, int epi, int fp8, int cfg, int splits, int* nwg, long long* ws_elems,
+                   int* tickets);
+int k8s_pgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs, const float* wsc,
+              int M, int N_out, int K, int epi, int fp8, int cfg, int splits, int group_m, const void* res, int rms,
+              float eps, hipStream_t s);
 }
 
 namespace {
@@ -225,6 +237,51 @@ PYBIND11_MODULE(_C, m) {
           "mgemm");
   });
 
+  m.def("pgemm4_configs", []() {
+    py::list out;
+    for (int c = 0; c < k8s_pgemm4_num_configs(); ++c) {
+      int bp = 0, bq = 0, lds = 0;
+      k8s_pgemm4_config(c, &bp, &bq, &lds);
+      out.append(py::make_tuple(bp, bq, lds));
+    }
+    return out;
+  });
+  m.def("pgemm4_plan", [](int M, int N, int K, int epi, int cfg, int splits) {
+    int nwg = 0;
+    long long slab = 0;
+    if (k8s_pgemm4_plan(M, N, K, epi, cfg, splits, &nwg, &slab) != 0)
+      throw std::invalid_argument("pgemm4_plan: invalid plan");
+    return py::make_tuple(nwg, slab);
+  });
+  m.def("pgemm4", [](uintptr_t out, uintptr_t slab, uintptr_t x, uintptr_t W, int M, int N, int K, int epi, int cfg,
+                     int splits, int group_m, uintptr_t res, int rms, float eps, int64_t s) {
+    check(k8s_pgemm4(P(out), P<float>(slab), P(x), P(W), M, N, K, epi, cfg, splits, group_m, P(res), rms, eps, S(s)),
+          "pgemm4");
+  });
+  m.def("pgemm_configs", []() {
+    py::list out;
+    for (int c = 0; c < k8s_pgemm_num_configs(); ++c) {
+      int bp = 0, bq = 0, lds = 0;
+      k8s_pgemm_config(c, &bp, &bq, &lds);
+      out.append(py::make_tuple(bp, bq, lds));
+    }
+    return out;
+  });
+  m.def("pgemm_plan", [](int M, int N, int K, int epi, int fp8, int cfg, int splits) {
+    int nwg = 0, tickets = 0;
+    long long ws = 0;
+    if (k8s_pgemm_plan(M, N, K, epi, fp8, cfg, splits, &nwg, &ws, &tickets) != 0)
+      throw std::invalid_argument("pgemm_plan: invalid plan");
+    return py::make_tuple(nwg, ws, tickets);
+  });
+  m.def("pgemm", [](uintptr_t out, uintptr_t ws, uintptr_t tickets, uintptr_t x, uintptr_t W, uintptr_t xs,
+                    uintptr_t wsc, int M, int N, int K, int epi, int fp8, int cfg, int splits, int group_m,
+                    uintptr_t res, int rms, float eps, int64_t s) {
+    check(k8s_pgemm(P(out), P<float>(ws), P<unsigned>(tickets), P(x), P(W), P<float>(xs), P<float>(wsc), M, N, K,
+                    epi, fp8, cfg, splits, group_m, P(res), rms, eps, S(s)),
+          "pgemm");
+  });
+
   using k8sllm::RcclComm;
   py::class_<RcclComm>(m, "RcclComm")
       .def_static("unique_id", []() {
@@ -244,6 +301,8 @@ PYBIND11_MODULE(_C, m) {
         c.broadcast(P(buf), count, dtype, root, S(s));
       })
       .def("async_error", &RcclComm::async_error)
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("aborted", &RcclComm::aborted)
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("rank", &RcclComm::rank);
 
@@ -270,6 +329,7 @@ PYBIND11_MODULE(_C, m) {
       .def("snapshot_error", [](XgmiComm& c, int64_t s) { c.snapshot_error(S(s)); }, py::arg("stream") = -1)
       .def("last_error", &XgmiComm::last_error)
       .def("reset_error", &XgmiComm::reset_error)
+      .def("reset", &XgmiComm::reset, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("world", &XgmiComm::world)
       .def_property_readonly("rank", &XgmiComm::rank)
       .def_property_readonly("slot_bytes", &XgmiComm::slot_bytes)

@@ -1,0 +1,496 @@
+// K3 / K8 / K9(+K10) / K11 / K12 at prefill row counts, bf16: the 4-wave big-tile MFMA GEMM.
+//
+//     out[M, N_out] = epi( x[M, K] . W[N, K]^T )      epi: bf16 (+ residual) | fp32 | SwiGLU, optional RMS prologue
+//
+// Why 4 waves (and not pgemm.hip's 8-wave ping-pong): PMC on the 2048 x 8192 x 8192 projection showed the
+// 8-wave 128 x 64-per-wave schedule parked 31 % of its wave cycles at barriers (SQ_WAIT_ANY) and issued 1.5x
+// the LDS instructions of the library's 256 x 256 kernel, which runs 4 waves of 128 x 128
+// (profiles/pmc_pgemm_vs_hipblaslt_M2048_oproj_tp1.txt).  Here every wave owns a 128 x 128 output (64
+// fragments of v_mfma_f32_16x16x32_bf16, 256 accumulator registers: the AGPR half of the unified file at one
+// wave per SIMD), so per 32-deep k-step a wave issues 16 fragment reads for 64 MFMAs.
+//
+//  * ring of 4 LDS k-steps (BP + BQ rows x 64 bytes each, 128 KiB at 256 x 256) filled by LDS-DMA
+//    (global_load_lds_dwordx4); k-step s+3 is issued right after the barrier of iteration s into the slot
+//    k-step s-1 vacated, so three k-steps (two MFMA blocks, ~2k cycles) of DMA are in flight across the raw
+//    s_barriers; the one wait per k-step is a counted `s_waitcnt vmcnt` (never 0 in the steady state).
+//  * register double buffer: the fragments of k-step s+1 are read (ds_read_b128) before the 64 MFMAs of
+//    k-step s, so the LDS latency hides under the matrix pipe of the same wave.
+//  * DMA image lane-linear, XOR swizzle on the per-lane global source (16-byte chunk c of row r in slot
+//    c ^ ((r >> 2) & 3)): the 16-row fragment reads are conflict-free on 64-byte rows.
+//  * swapped orientation C^T = W . x^T: every lane ends with 4 consecutive features of one token (gate/up
+//    rows of one feature sit in the same lane for the SwiGLU epilogue).
+//  * XCD-aware bijective block remap, group_m m-tiles per n-column group, k-slices of a tile adjacent.
+//  * split-K: every slice stores fp32 partial sums into its own slab [M][W rows] (plus the RMS row sums) and
+//    pgemm_reduce_kernel sums the slabs in slice order (deterministic) and applies the epilogue -- a
+//    parallel reduction over the whole chip instead of one last-arriving workgroup reading every slab.
+#include <type_traits>
+
+#include "common.h"
+
+namespace k8sllm {
+
+namespace {
+enum { P4_BF16 = 0, P4_F32 = 1, P4_SWIGLU = 2 };
+typedef __attribute__((ext_vector_type(2))) uint32_t p4_u32x2;
+
+template <int N>
+__device__ __forceinline__ void p4_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void p4_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ float p4_silu(float g) { return g / (1.f + __expf(-g)); }
+}  // namespace
+
+struct P4Args {
+  void* out;
+  const bf16_t* res;     // optional residual (bf16 [M][N_out], may alias out)
+  float* slab;           // split-K: [splits][M][W rows] fp32 partial sums, then [splits][M] row sums of squares
+  const uint8_t* x;      // [M][K] bf16
+  const uint8_t* W;      // [rows][K] bf16
+  uint32_t kbytes;       // bytes per row of x and W
+  int M, N_out, half_rows, wrows, K;
+  int m_tiles, n_tiles, ks, splits, group_m, nwg;
+  float eps;
+};
+
+template <int FP, int FQ, int EPI, bool RMS>
+__global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
+  constexpr int BP = 32 * FP, BQ = 32 * FQ;          // weight rows, tokens per tile (2 x 2 waves)
+  constexpr int ROWS = BP + BQ;
+  constexpr int SUB = ROWS * 64;                     // one 32-deep k-step of both operands
+  constexpr int G = ROWS / 64;                       // 16-byte DMA instructions per thread per k-step
+  constexpr int NSLOT = 4;
+  static_assert(ROWS % 64 == 0 && G >= 1, "tile shape");
+#if defined(__HIP_DEVICE_COMPILE__)
+  __shared__ __attribute__((aligned(16))) char lds[NSLOT * SUB + BQ * 8];
+  float* rss = reinterpret_cast<float*>(lds + NSLOT * SUB);   // [2][BQ] row sums of squares (wave rows)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int li = lane & 15, g = lane >> 4;
+
+  // ---- block -> (tile, k-slice)
+  const int bid = blockIdx.x, q8 = a.nwg >> 3, r8 = a.nwg & 7, xcd = bid & 7, loc = bid >> 3;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tile = lid / a.splits, slice = lid - tile * a.splits;
+  int mt, nt;
+  {
+    const int per = a.group_m * a.n_tiles, gi = tile / per, m0 = gi * a.group_m;
+    const int gm = min(a.m_tiles - m0, a.group_m), in = tile - gi * per;
+    mt = m0 + in % gm;
+    nt = in / gm;
+  }
+  const int ks0 = 2 * (int)((long long)slice * (a.ks / 2) / a.splits);
+  const int n = 2 * (int)((long long)(slice + 1) * (a.ks / 2) / a.splits) - ks0;   // even, >= 2
+
+  // ---- per-thread DMA sources: chunk p = j * 256 + tid of the k-step image (rows 0..BP-1 weights, then x);
+  // instructions j < GW cover weight rows only, the rest x rows only
+  constexpr int GW = BP / 64;
+  uint32_t off[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int p = j * 256 + tid, r = p >> 2, c = (p & 3) ^ ((r >> 2) & 3);
+    const uint32_t col = (uint32_t)(c * 16 + ks0 * 64);
+    if (j < GW) {
+      const int w = r / (BP / 2), q = r % (BP / 2);
+      int row;
+      if constexpr (EPI == P4_SWIGLU) {   // wave rows: BP/4 gate rows then the matching BP/4 up rows
+        const int f = min(nt * (BP / 2) + w * (BP / 4) + (q % (BP / 4)), a.N_out - 1);
+        row = q < BP / 4 ? f : a.half_rows + f;
+      } else {
+        row = min(nt * BP + r, a.N_out - 1);
+      }
+      off[j] = (uint32_t)row * a.kbytes + col;
+    } else {
+      off[j] = (uint32_t)min(mt * BQ + (r - BP), a.M - 1) * a.kbytes + col;
+    }
+  }
+  auto issue = [&](int u) {   // k-step u of this slice into slot u % 4
+    char* dst = lds + (u & (NSLOT - 1)) * SUB + wid * 1024;
+    const uint32_t kb = (uint32_t)u * 64u;
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      __builtin_amdgcn_global_load_lds((j < GW ? a.W : a.x) + (off[j] + kb),
+                                       (__attribute__((address_space(3))) void*)(dst + j * 4096), 16, 0, 0);
+  };
+
+  // ---- fragment reads: row li of a 16-row fragment, chunk g (k 8g .. 8g+7), swizzled
+  const int lo = li * 64 + ((g ^ (li >> 2)) << 4);
+  const int pb = (wr * (BP / 2)) * 64 + lo, qb = (BP + wc * (BQ / 2)) * 64 + lo;
+  bf16x8 A0[FP], B0[FQ], A1[FP], B1[FQ];
+  auto rd = [&](int u, bf16x8* A, bf16x8* B) {
+    const char* sb = lds + (u & (NSLOT - 1)) * SUB;
+#pragma unroll
+    for (int f = 0; f < FP; ++f) A[f] = *reinterpret_cast<const bf16x8*>(sb + pb + f * 1024);
+#pragma unroll
+    for (int f = 0; f < FQ; ++f) B[f] = *reinterpret_cast<const bf16x8*>(sb + qb + f * 1024);
+  };
+
+  f32x4 acc[FP][FQ];
+#pragma unroll
+  for (int i = 0; i < FP; ++i)
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[FQ];
+#pragma unroll
+  for (int f = 0; f < FQ; ++f) ss[f] = 0.f;
+
+  auto mma = [&](const bf16x8* A, const bf16x8* B, bool sq) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FP; ++i)
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (RMS) {
+      if (sq) {   // the two wave rows hold the same x fragments: each squares every other k-step
+#pragma unroll
+        for (int f = 0; f < FQ; ++f)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bf16x2 v2 = {B[f][2 * e], B[f][2 * e + 1]};
+            ss[f] = __builtin_amdgcn_fdot2_f32_bf16(v2, v2, ss[f], false);
+          }
+      }
+    }
+  };
+  // one k-step s: make s+1 visible, refill the slot of s-1 with s+3, read s+1, MFMA on s.  The steady-state
+  // loop runs the unconditional form (every k-step it touches exists); the last 2-4 k-steps are peeled
+  auto step_full = [&](int s, bf16x8* Ac, bf16x8* Bc, bf16x8* An, bf16x8* Bn) {
+    p4_vmcnt<G>();
+    p4_sync();
+    issue(s + 3);
+    rd(s + 1, An, Bn);
+    mma(Ac, Bc, (s & 1) == wr);
+  };
+  auto step_tail = [&](int s, bf16x8* Ac, bf16x8* Bc, bf16x8* An, bf16x8* Bn) {
+    if (s + 1 < n) {
+      if (s + 2 < n) p4_vmcnt<G>(); else p4_vmcnt<0>();
+      p4_sync();
+      if (s + 3 < n) issue(s + 3);
+      rd(s + 1, An, Bn);
+    }
+    mma(Ac, Bc, (s & 1) == wr);
+  };
+
+  // n is even (the host splits K in 64-deep units): the loop body is two k-steps with fixed register sets
+  issue(0);
+  issue(1);
+  if (n > 2) issue(2);
+  if (n > 2) p4_vmcnt<2 * G>(); else p4_vmcnt<G>();
+  p4_sync();
+  rd(0, A0, B0);
+  int s = 0;
+  for (; s + 4 < n; s += 2) {
+    step_full(s, A0, B0, A1, B1);
+    step_full(s + 1, A1, B1, A0, B0);
+  }
+  if (s + 2 < n) {
+    step_tail(s, A0, B0, A1, B1);
+    step_tail(s + 1, A1, B1, A0, B0);
+    s += 2;
+  }
+  step_tail(s, A0, B0, A1, B1);
+  step_tail(s + 1, A1, B1, A0, B0);
+  p4_vmcnt<0>();
+
+  if constexpr (RMS) {
+#pragma unroll
+    for (int f = 0; f < FQ; ++f) {
+      ss[f] += __shfl_xor(ss[f], 16, WAVE);
+      ss[f] += __shfl_xor(ss[f], 32, WAVE);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int f = 0; f < FQ; ++f) rss[wr * BQ + wc * (BQ / 2) + f * 16 + li] = ss[f];
+    }
+    __syncthreads();
+    if (tid < BQ) rss[tid] += rss[BQ + tid];
+    __syncthreads();
+  }
+
+  // ---- split-K: raw partial sums into this slice's slab (natural [M][W rows] layout)
+  if (a.splits > 1) {
+    float* sl = a.slab + (size_t)slice * a.M * a.wrows;
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) {
+      const int m = mt * BQ + wc * (BQ / 2) + j * 16 + li;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int i = 0; i < FP; ++i) {
+        int r0;
+        if constexpr (EPI == P4_SWIGLU) {
+          const int hf = i / (FP / 2), f = nt * (BP / 2) + wr * (BP / 4) + (i % (FP / 2)) * 16 + 4 * g;
+          if (f >= a.N_out) continue;
+          r0 = hf ? a.half_rows + f : f;
+        } else {
+          r0 = nt * BP + wr * (BP / 2) + i * 16 + 4 * g;
+          if (r0 >= a.N_out) continue;
+        }
+        *reinterpret_cast<f32x4*>(sl + (size_t)m * a.wrows + r0) = acc[i][j];
+      }
+    }
+    if (RMS && tid < BQ && mt * BQ + tid < a.M)
+      a.slab[(size_t)a.splits * a.M * a.wrows + (size_t)slice * a.M + mt * BQ + tid] = rss[tid];
+    return;
+  }
+
+  // ---- epilogue: lane holds out[token li of fragment j][features 4 g .. 4 g + 3 of fragment i]
+#pragma unroll
+  for (int j = 0; j < FQ; ++j) {
+    const int mloc = wc * (BQ / 2) + j * 16 + li;
+    const int m = mt * BQ + mloc;
+    if (m >= a.M) continue;
+    float sx = 1.f;
+    if constexpr (RMS) sx = rsqrtf(rss[mloc] / (float)a.K + a.eps);
+    if constexpr (EPI == P4_SWIGLU) {
+#pragma unroll
+      for (int i = 0; i < FP / 2; ++i) {
+        const int f0 = nt * (BP / 2) + wr * (BP / 4) + i * 16 + 4 * g;
+        if (f0 >= a.N_out) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = p4_silu(acc[i][j][e] * sx) * (acc[FP / 2 + i][j][e] * sx);
+        const p4_u32x2 o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+        *reinterpret_cast<p4_u32x2*>(reinterpret_cast<bf16_t*>(a.out) + (size_t)m * a.N_out + f0) = o;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < FP; ++i) {
+        const int n0 = nt * BP + wr * (BP / 2) + i * 16 + 4 * g;
+        if (n0 >= a.N_out) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * sx;
+        if constexpr (EPI == P4_F32) {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + (size_t)m * a.N_out + n0) =
+              f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          if (a.res != nullptr) {
+            const p4_u32x2 rr = *reinterpret_cast<const p4_u32x2*>(a.res + (size_t)m * a.N_out + n0);
+            v[0] += lo_bf(rr[0]);
+            v[1] += hi_bf(rr[0]);
+            v[2] += lo_bf(rr[1]);
+            v[3] += hi_bf(rr[1]);
+          }
+          const p4_u32x2 o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+          *reinterpret_cast<p4_u32x2*>(reinterpret_cast<bf16_t*>(a.out) + (size_t)m * a.N_out + n0) = o;
+        }
+      }
+    }
+  }
+#endif
+}
+
+// Split-K combine: out[m, 4 q .. 4 q + 3] = epi(sum over slices of the slabs), slices in order.  One thread per
+// 4 output features of one token; x scaling (RMS) and the residual as in the main kernel's epilogue.
+template <int EPI, bool RMS, bool FP8>
+__global__ void __launch_bounds__(256) pgemm_reduce_kernel(void* __restrict__ out, const bf16_t* res,
+                                                           const float* __restrict__ slab, int splits, int M,
+                                                           int N_out, int half_rows, int wrows, int K, float eps,
+                                                           const float* __restrict__ xs,
+                                                           const float* __restrict__ wsc) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int qn = N_out / 4;
+  if (idx >= (long long)M * qn) return;
+  const int m = (int)(idx / qn), n0 = (int)(idx - (long long)m * qn) * 4;
+  const size_t stride = (size_t)M * wrows;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < splits; ++k) {
+    const float* p = slab + (size_t)k * stride + (size_t)m * wrows;
+    s += *reinterpret_cast<const f32x4*>(p + n0);
+    if (EPI == P4_SWIGLU) u += *reinterpret_cast<const f32x4*>(p + half_rows + n0);
+  }
+  float sx = 1.f;
+  if (RMS) {
+    float t = 0.f;
+    for (int k = 0; k < splits; ++k) t += slab[(size_t)splits * stride + (size_t)k * M + m];
+    sx = rsqrtf(t / (float)K + eps);
+  }
+  if (FP8) sx *= xs[m];
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (EPI == P4_SWIGLU) {
+      float gt = s[e] * sx, up = u[e] * sx;
+      if (FP8) {
+        gt *= wsc[n0 + e];
+        up *= wsc[half_rows + n0 + e];
+      }
+      v[e] = p4_silu(gt) * up;
+    } else {
+      v[e] = s[e] * sx * (FP8 ? wsc[n0 + e] : 1.f);
+    }
+  }
+  if (EPI == P4_F32) {
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + (size_t)m * N_out + n0) = f32x4{v[0], v[1], v[2], v[3]};
+  } else {
+    if (EPI == P4_BF16 && res != nullptr) {
+      const p4_u32x2 rr = *reinterpret_cast<const p4_u32x2*>(res + (size_t)m * N_out + n0);
+      v[0] += lo_bf(rr[0]);
+      v[1] += hi_bf(rr[0]);
+      v[2] += lo_bf(rr[1]);
+      v[3] += hi_bf(rr[1]);
+    }
+    const p4_u32x2 o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+    *reinterpret_cast<p4_u32x2*>(reinterpret_cast<bf16_t*>(out) + (size_t)m * N_out + n0) = o;
+  }
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+namespace {
+struct P4Cfg {
+  int fp, fq;
+};
+// tile configurations: BP = 32 FP weight rows x BQ = 32 FQ tokens, 4 waves of (BP / 2) x (BQ / 2)
+constexpr P4Cfg kP4Cfgs[] = {
+    {8, 8},   // 0: 256 x 256
+    {8, 4},   // 1: 256 x 128
+    {4, 8},   // 2: 128 x 256
+    {4, 4},   // 3: 128 x 128
+};
+constexpr int kP4NumCfgs = sizeof(kP4Cfgs) / sizeof(kP4Cfgs[0]);
+
+template <int C, int EPI, bool RMS>
+int p4_launch(const P4Args& a, hipStream_t s) {
+  hipLaunchKernelGGL((pgemm4_kernel<kP4Cfgs[C].fp, kP4Cfgs[C].fq, EPI, RMS>), dim3(a.nwg), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+template <int C>
+int p4_epi(const P4Args& a, int epi, int rms, hipStream_t s) {
+  if (rms) {
+    switch (epi) {
+      case P4_BF16: return p4_launch<C, P4_BF16, true>(a, s);
+      case P4_F32: return p4_launch<C, P4_F32, true>(a, s);
+      case P4_SWIGLU: return p4_launch<C, P4_SWIGLU, true>(a, s);
+    }
+  } else {
+    switch (epi) {
+      case P4_BF16: return p4_launch<C, P4_BF16, false>(a, s);
+      case P4_F32: return p4_launch<C, P4_F32, false>(a, s);
+      case P4_SWIGLU: return p4_launch<C, P4_SWIGLU, false>(a, s);
+    }
+  }
+  return -2;
+}
+template <int C = 0>
+int p4_cfg(const P4Args& a, int cfg, int epi, int rms, hipStream_t s) {
+  if constexpr (C < kP4NumCfgs) {
+    if (cfg == C) return p4_epi<C>(a, epi, rms, s);
+    return p4_cfg<C + 1>(a, cfg, epi, rms, s);
+  } else {
+    return -4;
+  }
+}
+
+template <int EPI, bool RMS, bool FP8>
+int reduce_launch(void* out, const void* res, const float* slab, int splits, int M, int N_out, int half_rows,
+                  int wrows, int K, float eps, const float* xs, const float* wsc, hipStream_t s) {
+  const long long items = (long long)M * (N_out / 4);
+  hipLaunchKernelGGL((pgemm_reduce_kernel<EPI, RMS, FP8>), dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s,
+                     out, static_cast<const bf16_t*>(res), slab, splits, M, N_out, half_rows, wrows, K, eps, xs, wsc);
+  return (int)hipGetLastError();
+}
+}  // namespace
+
+// Split-K combine of pgemm slabs (also used by the fp8 kernel): slab = [splits][M][wrows] fp32, then (rms)
+// [splits][M] row sums of squares.
+extern "C" int k8s_pgemm_reduce(void* out, const void* res, const float* slab, int splits, int M, int N_out, int K,
+                                int epi, int rms, float eps, const float* xs, const float* wsc, hipStream_t s) {
+  if (splits < 1 || M <= 0 || N_out <= 0 || N_out % 4) return -1;
+  const int half = epi == P4_SWIGLU ? N_out : 0, wrows = epi == P4_SWIGLU ? 2 * N_out : N_out;
+  const bool fp8 = xs != nullptr;
+  if (rms && fp8) return -6;
+#define K8S_RED(E, R, F) return reduce_launch<E, R, F>(out, res, slab, splits, M, N_out, half, wrows, K, eps, xs, wsc, s)
+  if (fp8) {
+    switch (epi) {
+      case P4_BF16: K8S_RED(P4_BF16, false, true);
+      case P4_F32: K8S_RED(P4_F32, false, true);
+      case P4_SWIGLU: K8S_RED(P4_SWIGLU, false, true);
+    }
+  } else if (rms) {
+    switch (epi) {
+      case P4_BF16: K8S_RED(P4_BF16, true, false);
+      case P4_F32: K8S_RED(P4_F32, true, false);
+      case P4_SWIGLU: K8S_RED(P4_SWIGLU, true, false);
+    }
+  } else {
+    switch (epi) {
+      case P4_BF16: K8S_RED(P4_BF16, false, false);
+      case P4_F32: K8S_RED(P4_F32, false, false);
+      case P4_SWIGLU: K8S_RED(P4_SWIGLU, false, false);
+    }
+  }
+#undef K8S_RED
+  return -2;
+}
+
+extern "C" int k8s_pgemm4_num_configs() { return kP4NumCfgs; }
+
+extern "C" int k8s_pgemm4_config(int cfg, int* bp, int* bq, int* lds_bytes) {
+  if (cfg < 0 || cfg >= kP4NumCfgs) return -1;
+  *bp = 32 * kP4Cfgs[cfg].fp;
+  *bq = 32 * kP4Cfgs[cfg].fq;
+  *lds_bytes = 4 * (*bp + *bq) * 64 + *bq * 8;
+  return 0;
+}
+
+// Launch facts: workgroups and split-K slab elements (0 without split-K).
+extern "C" int k8s_pgemm4_plan(int M, int N_out, int K, int epi, int cfg, int splits, int* nwg, long long* slab_elems) {
+  if (cfg < 0 || cfg >= kP4NumCfgs || M <= 0 || N_out <= 0 || K <= 0 || splits < 1) return -1;
+  if (K % 64 != 0 || N_out % 4 != 0) return -1;
+  const int bp = 32 * kP4Cfgs[cfg].fp, bq = 32 * kP4Cfgs[cfg].fq;
+  const int feat = epi == P4_SWIGLU ? bp / 2 : bp;
+  const int ks = K / 32;
+  if (splits > ks / 2) return -1;
+  const long long tiles = (long long)((M + bq - 1) / bq) * ((N_out + feat - 1) / feat);
+  if (tiles * splits > (1LL << 30)) return -1;
+  const long long wrows = epi == P4_SWIGLU ? 2LL * N_out : N_out;
+  *nwg = (int)(tiles * splits);
+  *slab_elems = splits > 1 ? (long long)splits * M * wrows + (long long)splits * M : 0;
+  return 0;
+}
+
+extern "C" int k8s_pgemm4(void* out, float* slab, const void* x, const void* W, int M, int N_out, int K, int epi,
+                          int cfg, int splits, int group_m, const void* res, int rms, float eps, hipStream_t stream) {
+  int nwg;
+  long long nsl;
+  if (k8s_pgemm4_plan(M, N_out, K, epi, cfg, splits, &nwg, &nsl) != 0) return -1;
+  if (splits > 1 && slab == nullptr) return -3;
+  const long long kbytes = (long long)K * 2;
+  const long long wrows = epi == P4_SWIGLU ? 2LL * N_out : (long long)N_out;
+  if (wrows * kbytes >= (1LL << 32) || (long long)M * kbytes >= (1LL << 32)) return -5;   // 32-bit DMA offsets
+  if (res != nullptr && epi != P4_BF16) return -6;
+  const int bp = 32 * kP4Cfgs[cfg].fp, bq = 32 * kP4Cfgs[cfg].fq;
+  const int feat = epi == P4_SWIGLU ? bp / 2 : bp;
+  P4Args a;
+  a.out = out;
+  a.res = static_cast<const bf16_t*>(res);
+  a.slab = slab;
+  a.x = static_cast<const uint8_t*>(x);
+  a.W = static_cast<const uint8_t*>(W);
+  a.kbytes = (uint32_t)kbytes;
+  a.M = M;
+  a.N_out = N_out;
+  a.half_rows = epi == P4_SWIGLU ? N_out : 0;
+  a.wrows = (int)wrows;
+  a.K = K;
+  a.m_tiles = (M + bq - 1) / bq;
+  a.n_tiles = (N_out + feat - 1) / feat;
+  a.ks = K / 32;
+  a.splits = splits;
+  a.group_m = group_m > 0 ? group_m : 1;
+  a.nwg = nwg;
+  a.eps = eps;
+  int rc = p4_cfg(a, cfg, epi, rms, stream);
+  if (rc != 0 || splits == 1) return rc;
+  return k8s_pgemm_reduce(out, res, slab, splits, M, N_out, K, epi, rms, eps, nullptr, nullptr, stream);
+}

@@ -306,23 +306,29 @@ __host__ __device__ inline int grid_x(int shards) { return shards * ((NB + shard
 
 using namespace k8sllm;
 
-// row_key [B] u64 + row_cnt [B] u32: zero-initialised scratch owned by the caller (one per
-// concurrently captured sampler), restored to zero by every launch.  nuc_scratch (or null: top_p
-// ignored): k8s_sample_nucleus_bytes(B, shards) bytes, zero before the first call and left zero.
+// Scratch layouts do not depend on B, so one buffer serves every batch size (decode graph buckets,
+// prefill rows, speculative verify rows) in any order:
+//   scratch:     row_key [SAMPLE_ROW_CAP] u64 | row_cnt [SAMPLE_ROW_CAP] u32 -- zero-initialised, owned by
+//                the caller (one per concurrently captured sampler), restored to zero by every launch.
+//   nuc_scratch: (or null: top_p ignored) NucRow [SAMPLE_ROW_CAP] | histograms [B][grid][256] u64 --
+//                the row states zero before the first call and left zero; the histograms are fully
+//                rewritten by every launch before they are read.
+constexpr int SAMPLE_ROW_CAP = 4096;
 extern "C" int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
                           const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist,
                           int hist_stride, int* steps, void* scratch, void* nuc_scratch, hipStream_t stream) {
   if (B <= 0) return 0;
+  if (B > SAMPLE_ROW_CAP) return -2;
   if (hist != nullptr && steps == nullptr) return -1;
   if (scratch == nullptr) return -3;
   if (shards < 1 || Vs < 1) return -2;
   auto* key = static_cast<unsigned long long*>(scratch);
-  auto* cnt = reinterpret_cast<uint32_t*>(key + B);
+  auto* cnt = reinterpret_cast<uint32_t*>(key + SAMPLE_ROW_CAP);
   const dim3 grid(grid_x(shards), B);
   NucRow* st = nullptr;
   if (nuc_scratch != nullptr) {
     st = static_cast<NucRow*>(nuc_scratch);
-    auto* ws = reinterpret_cast<unsigned long long*>(st + B);
+    auto* ws = reinterpret_cast<unsigned long long*>(st + SAMPLE_ROW_CAP);
     nuc_max_kernel<<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, st);
     nuc_hist_kernel<0><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, st, ws);
     nuc_hist_kernel<1><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, st, ws);
@@ -332,9 +338,12 @@ extern "C" int k8s_sample(int* tokens, const float* logits, int B, int Vs, int s
   return (int)hipGetLastError();
 }
 
-extern "C" long long k8s_sample_scratch_bytes(int B) { return (long long)B * 12; }
+extern "C" long long k8s_sample_scratch_bytes(int B) {
+  (void)B;
+  return (long long)SAMPLE_ROW_CAP * 12;
+}
 
 extern "C" long long k8s_sample_nucleus_bytes(int B, int shards) {
   if (B <= 0 || shards < 1) return 0;
-  return (long long)B * (long long)sizeof(NucRow) + (long long)B * grid_x(shards) * 256 * 8;
+  return (long long)SAMPLE_ROW_CAP * (long long)sizeof(NucRow) + (long long)B * grid_x(shards) * 256 * 8;
 }

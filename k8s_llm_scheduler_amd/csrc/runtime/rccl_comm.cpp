@@ -53,25 +53,34 @@ RcclComm::RcclComm(int world, int rank, const std::vector<uint8_t>& id) : world_
   comm_ = c;
 }
 
+void RcclComm::abort() {
+  if (comm_) (void)ncclCommAbort(static_cast<ncclComm_t>(comm_));
+  comm_ = nullptr;
+}
+
 RcclComm::~RcclComm() {
   if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
 }
 
 void RcclComm::all_reduce(const void* send, void* recv, size_t count, int dtype, int red, hipStream_t s) {
+  if (!comm_) throw std::runtime_error("RCCL communicator aborted");
   ck(ncclAllReduce(send, recv, count, dt(dtype), op(red), static_cast<ncclComm_t>(comm_), s), "ncclAllReduce");
 }
 
 void RcclComm::all_gather(const void* send, void* recv, size_t count, int dtype, hipStream_t s) {
+  if (!comm_) throw std::runtime_error("RCCL communicator aborted");
   ck(ncclAllGather(send, recv, count, dt(dtype), static_cast<ncclComm_t>(comm_), s), "ncclAllGather");
 }
 
 std::string RcclComm::async_error() const {
+  if (!comm_) return "communicator aborted";
   ncclResult_t r = ncclSuccess;
   if (ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
   return r == ncclSuccess ? std::string() : std::string(ncclGetErrorString(r));
 }
 
 void RcclComm::broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s) {
+  if (!comm_) throw std::runtime_error("RCCL communicator aborted");
   ck(ncclBroadcast(buf, buf, count, dt(dtype), root, static_cast<ncclComm_t>(comm_), s), "ncclBroadcast");
 }
 

@@ -21,6 +21,10 @@ class RcclComm {
   void broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s);
   // ncclCommGetAsyncError: "" when healthy, else the error text (a peer died, a transport failed)
   std::string async_error() const;
+  // ncclCommAbort: pending operations of this communicator error out (so a stream blocked on a dead
+  // peer drains) and the communicator is unusable afterwards; the engine then builds a new one.
+  void abort();
+  bool aborted() const { return comm_ == nullptr; }
   int world() const { return world_; }
   int rank() const { return rank_; }
 

@@ -125,6 +125,14 @@ void XgmiComm::snapshot_error(hipStream_t s) {
 
 uint32_t XgmiComm::last_error() const { return *reinterpret_cast<volatile uint32_t*>(host_err_); }
 
+void XgmiComm::reset() {
+  ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  ck(hipMemset(region_, 0, region_bytes_), "hipMemset(region)");
+  ck(hipMemset(counters_, 0, (k8s_xgmi_max_blocks() + 1) * sizeof(uint32_t)), "hipMemset(counters)");
+  *host_err_ = 0;
+  ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+}
+
 void XgmiComm::reset_error() {
   ck(hipMemset(counters_ + k8s_xgmi_max_blocks(), 0, sizeof(uint32_t)), "hipMemset");
 }

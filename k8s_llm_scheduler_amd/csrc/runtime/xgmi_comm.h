@@ -28,6 +28,10 @@ class XgmiComm {
   void snapshot_error(hipStream_t s);
   uint32_t last_error() const;
   void reset_error();
+  // Back to the freshly-constructed protocol state: zero this rank's region (flags, LL rows, slots),
+  // the per-workgroup epochs and the error word.  Recovery after a stall: every rank calls it with its
+  // device drained, then the ranks pass a barrier before the next collective.
+  void reset();
 
   int world() const { return world_; }
   int rank() const { return rank_; }

@@ -42,6 +42,7 @@ import torch
 from .. import ops
 from ..control.jsonextract import json_object_closed
 from ..models.llama import LlamaModel
+from ..parallel.comm import CollectiveError
 from .sampling import SamplingParams
 from .tokenizer import Tokenizer
 from ..utils.tracing import trace
@@ -103,6 +104,23 @@ def ngram_draft(seq: Sequence[int], k: int, n_max: int = 3) -> List[int]:
     return []
 
 
+class EngineStalled(TimeoutError):
+    """Device work of an engine step did not complete within the call deadline or the engine watchdog (a
+    hung collective or kernel).  The engine stops accepting work until :meth:`LLMEngine.recover` succeeds."""
+
+
+class EngineUnavailable(RuntimeError):
+    """The engine is not ready: an earlier collective failure or stall has not been recovered yet."""
+
+
+class RequestRejected(RuntimeError):
+    """One request cannot be served (e.g. it does not fit in an empty KV cache); only that request fails."""
+
+    def __init__(self, request, msg: str):
+        super().__init__(msg)
+        self.request = request
+
+
 @dataclass
 class Request:
     rid: int
@@ -141,8 +159,23 @@ class LLMEngine:
                  num_blocks: Optional[int] = None, kv_cache_gb: float = 0.0, kv_cache_fraction: float = 0.85,
                  max_model_len: Optional[int] = None, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
                  prefix_caching: bool = True, decode_chunk: int = 4, seed: int = 0, metrics=None,
-                 control=None, capture_nucleus: bool = False, speculative_tokens: int = 0):
+                 control=None, capture_nucleus: bool = False, speculative_tokens: int = 0,
+                 watchdog_s: float = 60.0, on_unrecoverable: str = "stay"):
         self.model = model
+        # Bounded device waits: every host wait for device results polls an event against
+        # min(call deadline, step start + watchdog_s) instead of blocking in a synchronize, so a hung collective
+        # surfaces as EngineStalled inside llm.timeout.  ``on_unrecoverable``: "exit" ends the process (exit code
+        # 70) when recovery cannot drain the device, so the Deployment restarts the pod; "stay" keeps it
+        # not-ready (tests, single-process runs).
+        self.watchdog_s = float(watchdog_s)
+        if on_unrecoverable not in ("exit", "stay"):
+            raise ValueError("on_unrecoverable must be 'exit' or 'stay'")
+        self.on_unrecoverable = on_unrecoverable
+        self._call_deadline: Optional[float] = None
+        self._step_t0 = time.monotonic()
+        self._last_event = None
+        self._pinned: Dict[tuple, torch.Tensor] = {}
+        self.health = {"ready": True, "reason": "", "failures": 0, "recoveries": 0, "since": time.time()}
         # prompt-lookup speculative decoding (_spec_decode): drafted tokens per step, 0 = off
         self.speculative_tokens = max(0, int(speculative_tokens))
         # also capture decode graphs with the top-p passes (config llm.top_p < 1); otherwise chunks
@@ -212,7 +245,151 @@ class LLMEngine:
         self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "graph_replays": 0, "prefill_graph_replays": 0, "prefill_overlap_chunks": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "spec_steps": 0, "spec_graph_replays": 0, "spec_drafted": 0,
-                      "spec_accepted": 0}
+                      "spec_accepted": 0, "stalls": 0}
+
+    # ------------------------------------------------------------------ bounded device waits / health
+    def _wait_limit(self) -> Optional[float]:
+        lim = self._step_t0 + self.watchdog_s if self.watchdog_s > 0 else None
+        if self._call_deadline is not None:
+            lim = self._call_deadline if lim is None else min(lim, self._call_deadline)
+        return lim
+
+    def _wait_device(self, what: str) -> None:
+        """Wait for the work enqueued so far on the engine's stream: an event polled against the call deadline
+        and the watchdog (never a blocking synchronize, so a hung collective cannot block the host forever)."""
+        if not self.gpu:
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._last_event = ev
+        limit = self._wait_limit()
+        spins = 0
+        while not ev.query():
+            if limit is not None and time.monotonic() > limit:
+                self.stats["stalls"] += 1
+                msg = f"engine stalled: {what} did not complete within the deadline (rank {self.model.tp.rank})"
+                self._fail(msg)
+                raise EngineStalled(msg)
+            spins += 1
+            time.sleep(0 if spins < 200 else 2e-5)
+
+    def _fetch(self, *ts: torch.Tensor, what: str = "step") -> List[torch.Tensor]:
+        """Small device tensors -> host, through reused pinned buffers and one bounded wait.  The returned
+        tensors are overwritten by the next fetch: read them right away."""
+        if not self.gpu:
+            return [t.clone() for t in ts]
+        outs = []
+        for i, t in enumerate(ts):
+            key = (i, t.dtype, tuple(t.shape))
+            buf = self._pinned.get(key)
+            if buf is None:
+                buf = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                self._pinned[key] = buf
+            buf.copy_(t, non_blocking=True)
+            outs.append(buf)
+        self._wait_device(what)
+        return outs
+
+    def _fail(self, reason: str) -> None:
+        if self.health["ready"]:
+            log.error(f"Decision engine not ready: {reason}")
+        self.health.update(ready=False, reason=reason, failures=self.health["failures"] + 1, since=time.time())
+        if self.metrics is not None and hasattr(self.metrics, "engine_health"):
+            self.metrics.engine_health(False)
+
+    @property
+    def ready(self) -> bool:
+        return bool(self.health["ready"])
+
+    def health_probe(self):
+        """(live, ready, detail) for /healthz and /readyz: live while the serving loop (if started) runs."""
+        t = self._bg_thread
+        live = t is None or t.is_alive()
+        return live, self.ready, {"reason": self.health["reason"], "failures": self.health["failures"],
+                                  "recoveries": self.health["recoveries"], "stalls": self.stats["stalls"]}
+
+    def _drained(self, timeout_s: float) -> bool:
+        """True once every piece of device work this engine enqueued has completed (bounded poll)."""
+        if not self.gpu:
+            return True
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        end = time.monotonic() + max(0.0, timeout_s)
+        while not ev.query():
+            if time.monotonic() > end:
+                return False
+            time.sleep(1e-3)
+        return True
+
+    def recover(self, drain_timeout: float = 0.0) -> bool:
+        """Bring a failed engine back.  The device must drain within ``drain_timeout`` s (a
+        stalled peer that resumes lets the parked collectives finish; an RCCL communicator is aborted so its
+        parked operations error out).  Then every rank of the replica -- told through the control channel --
+        resets its collectives (xGMI protocol state zeroed, a broken RCCL communicator rebuilt, bounded
+        barrier) and drops all in-flight requests and cached prefixes.  Returns True when ready again."""
+        with self.lock:
+            if self.ready:
+                return True
+            tp = self.model.tp
+            if not self._drained(drain_timeout):
+                if tp.rccl is not None and not tp.rccl.aborted:
+                    tp.abort_rccl()
+                    if self._drained(min(5.0, max(drain_timeout, 0.5))):
+                        return self._reset_all(announce=True)
+                return False
+            return self._reset_all(announce=True)
+
+    def _reset_all(self, announce: bool) -> bool:
+        """Every rank: end all requests, free every slot, drop the prefix cache (an abandoned step may have
+        committed KV that was never written), reset the collectives.  ``announce``: rank 0 first tells the
+        other ranks of the replica to do the same."""
+        tp = self.model.tp
+        try:
+            if announce and self.control is not None and self.control.rank == 0:
+                self.control.exchange({"new": [], "abort": [], "stop": False, "reset": True})
+            err = EngineUnavailable(self.health["reason"] or "engine reset")
+            for r in list(self.requests.values()) + list(self.waiting) + list(self.prefilling) + \
+                    list(self.running.values()):
+                if not r.finished:
+                    r.error = r.error or err
+                    self._finish(r, "error")
+            with self._inbox_lock:
+                pending, self._inbox = self._inbox, []
+            for r in pending:
+                r.error = err
+                r.finished, r.finish_reason = True, "error"
+                if r.done is not None:
+                    r.done.set()
+            self.requests.clear()
+            self.waiting.clear()
+            self.prefilling.clear()
+            self.running.clear()
+            self._outbox = []
+            self.free_slots = list(range(self.max_batch - 1, -1, -1))
+            self.allocator = ops.native().BlockAllocator(self.num_blocks, self.block_size, self.prefix_caching) \
+                if ops.available() else _PyBlockAllocator(self.num_blocks, self.block_size, self.prefix_caching)
+            if self.gpu:
+                self.s_ctx.zero_()
+                self.s_steps.zero_()
+                tp.reset_collectives(self.control, timeout_s=max(10.0, self.watchdog_s))
+                torch.cuda.synchronize(self.device)
+            else:
+                tp.reset_collectives(self.control, timeout_s=max(10.0, self.watchdog_s))
+        except Exception as e:  # noqa: BLE001 -- recovery failed: stay (or exit) not ready
+            self._fail(f"recovery failed: {e!r}")
+            self._unrecoverable(f"recovery failed: {e!r}")
+            return False
+        self.health.update(ready=True, reason="", recoveries=self.health["recoveries"] + 1, since=time.time())
+        if self.metrics is not None and hasattr(self.metrics, "engine_health"):
+            self.metrics.engine_health(True)
+        log.warning(f"Decision engine recovered (rank {tp.rank}; recoveries {self.health['recoveries']})")
+        return True
+
+    def _unrecoverable(self, why: str) -> None:
+        if self.on_unrecoverable == "exit":
+            log.critical(f"Decision engine cannot recover ({why}); exiting so the pod restarts")
+            logging.shutdown()
+            os._exit(70)
 
     # ------------------------------------------------------------------ device state
     def _alloc_state(self) -> None:
@@ -305,7 +482,7 @@ class LLMEngine:
                     self._graph_pool = g.pool()
                 self.prefill_graphs[Tb] = (g, logits)
         if self.speculative_tokens and self.speculative_tokens < SPEC_GRAPH_T and self.spec_graph is None \
-                and self._prefill_bucket_capturable(SPEC_GRAPH_T):
+                and self._prefill_bucket_capturable(SPEC_GRAPH_T, logits_rows=SPEC_GRAPH_T):
             # one sequence's verify forward (_spec_decode): SPEC_GRAPH_T rows, logits at every row
             Tb = SPEC_GRAPH_T
             self._fill_prefill_state([0] * Tb, list(range(Tb)), [self.scratch_slot] * Tb, Tb, [0], Tb)
@@ -329,17 +506,19 @@ class LLMEngine:
         env = os.environ.get("K8S_PREFILL_GRAPHS", "")
         return env != "0" and self.use_graphs and PREFILL_GRAPH_BUCKETS[-1] <= self.max_prefill_tokens
 
-    def _prefill_bucket_capturable(self, Tb: int) -> bool:
-        """TP > 1: a chunk of Tb tokens all-reduces Tb x hidden bf16 twice per layer and all-gathers one row of
-        fp32 logits; both must fit the xGMI transports, because a gloo collective cannot be captured (the 1-GPU
-        rehearsals) and RCCL capture stays opt-in until it has run on a multi-GPU node."""
+    def _prefill_bucket_capturable(self, Tb: int, logits_rows: int = 1) -> bool:
+        """TP > 1: a chunk of Tb tokens all-reduces Tb x hidden bf16 twice per layer and all-gathers
+        ``logits_rows`` rows of fp32 logits (one for a prefill chunk, every row for the speculative verify
+        forward); both must fit the xGMI transports, because a gloo collective cannot be captured (the 1-GPU
+        rehearsals) and RCCL capture stays opt-in until it has run on a multi-GPU node.  A verify forward that
+        does not fit runs eagerly."""
         tp = self.model.tp
         if tp.world <= 1 or tp.simulate or os.environ.get("K8S_PREFILL_GRAPHS", "") == "1":
             return True
         if tp.xgmi is None:
             return False
         ar_bytes = Tb * self.model.cfg.hidden * 2
-        gather_bytes = self.model.lm_head.shape[0] * 4
+        gather_bytes = logits_rows * self.model.lm_head.shape[0] * 4
         return ar_bytes <= (tp.xgmi_max_ar or tp.xgmi.max_allreduce_bytes) and gather_bytes <= tp.xgmi.slot_bytes
 
     def _p_views(self, Tb: int):
@@ -435,21 +614,32 @@ class LLMEngine:
         for r in new:
             self._enqueue(r)
 
-    def _sync(self) -> bool:
-        """Replicate rank 0's new requests and aborts to every rank.  Returns False on a stop
-        command (worker shutdown)."""
+    def _sync(self):
+        """Replicate rank 0's new requests and aborts to every rank, and collect every rank's health.  Returns
+        False on a stop command (worker shutdown), "reset" after a recovery reset (workers), else True.  A worker
+        that reports a failure makes rank 0 fail this step before it launches anything."""
         if self.control is None:
             return True
+        status = None if self.ready and not self.model.tp.failed else (self.health["reason"] or self.model.tp.failed)
         if self.control.rank == 0:
             msg = {"new": [(r.rid, r.prompt_ids, r.params.__dict__, r.seed) for r in self._outbox],
                    "abort": sorted(r.rid for r in self.requests.values() if r.aborted and not r.finished),
                    "stop": False}
             self._outbox = []
-            self.control.exchange(msg)
+            _, statuses = self.control.exchange(msg, status)
+            bad = [(i, st) for i, st in enumerate(statuses) if st and i != 0]
+            if bad:
+                raise CollectiveError(f"TP rank(s) {[i for i, _ in bad]} failed: {bad[0][1]}")
             return True
-        msg = self.control.exchange(None)
+        msg, _ = self.control.exchange(None, status)
         if msg.get("stop"):
             return False
+        if msg.get("reset"):
+            if not self._drained(max(5.0, self.watchdog_s)):
+                self._fail("reset: device did not drain")
+                self._unrecoverable("device did not drain for the reset")
+            self._reset_all(announce=False)
+            return "reset"
         for rid, ids, pd, seed in msg["new"]:
             r = Request(rid, list(ids), SamplingParams(**pd), seed)
             self.requests[rid] = r
@@ -520,7 +710,8 @@ class LLMEngine:
             total = len(r.prompt_ids) + r.params.max_tokens
             if not self.allocator.can_allocate(r.prompt_ids, total):
                 if not self.running and not self.prefilling:
-                    raise RuntimeError("request does not fit in an empty KV cache")
+                    self.waiting.popleft()
+                    raise RequestRejected(r, "request does not fit in an empty KV cache")
                 break
             self.waiting.popleft()
             a = self.allocator.allocate(r.prompt_ids, total)
@@ -610,7 +801,7 @@ class LLMEngine:
                 self.running[r.slot] = r
         if self.gpu:
             self.model.tp.snapshot_health()
-            torch.cuda.synchronize(self.device)
+            self._wait_device("prefill")
             self.model.tp.check_health()
         self.stats["prefill_time"] += time.perf_counter() - t0
 
@@ -635,9 +826,8 @@ class LLMEngine:
                 self._decode_step(B, mc, nuc)
         self.stats["decode_steps"] += steps
         tp = self.model.tp
-        tp.snapshot_health()             # rides on the sync below
-        hist = self.s_hist[:B].cpu()     # syncs the stream
-        nsteps = self.s_steps[:B].cpu()
+        tp.snapshot_health()             # rides on the bounded wait below
+        hist, nsteps = self._fetch(self.s_hist[:B], self.s_steps[:B], what="decode")
         tp.check_health()                # a failed collective raises into the decision service
         self.stats["decode_time"] += time.perf_counter() - t0
         finished = []
@@ -690,7 +880,7 @@ class LLMEngine:
         dev = self.device
         fresh = [r for r in self.running.values() if not r.output_ids]
         if fresh:                         # first tokens, sampled by the prefill
-            first = self.s_hist[:, 0].cpu()
+            first = self._fetch(self.s_hist[:, 0].contiguous(), what="first tokens")[0].clone()
             for r in fresh:
                 self._emit(r, int(first[r.slot]))
                 if r.finished:
@@ -742,7 +932,7 @@ class LLMEngine:
             toks = ops.sample(logits, t(temp, torch.float32), t(top_p, torch.float32), t(seeds), t(ctr),
                               shards=logits.shape[0], nucleus=self._wants_nucleus(r for r, _, _ in rows))
             self.model.tp.snapshot_health()
-            drawn = toks.cpu().tolist()   # syncs the stream
+            drawn = self._fetch(toks, what="speculative verify")[0].tolist()
             self.model.tp.check_health()
             self.stats["spec_steps"] += 1
             i = 0
@@ -825,33 +1015,51 @@ class LLMEngine:
 
     def step(self) -> List[Request]:
         with self.lock:
+            self._step_t0 = time.monotonic()
+            worker = self.control is not None and self.control.rank != 0
+            if not worker and not self.ready:
+                raise EngineUnavailable(self.health["reason"] or "decision engine not ready")
+            try:
+                return self._step(worker)
+            except (CollectiveError, EngineStalled) as e:
+                self._fail(str(e))
+                raise
+
+    def _step(self, worker: bool) -> List[Request]:
+        if not worker:
             self.model.tp.ensure_healthy()
-            self._drain_inbox()
-            if not self._sync():
-                raise StopIteration("engine stopped by rank 0")
-            self._reap_aborted()
-            self._share_deferred = False
-            self._admit()
-            if self.prefilling or self.waiting:
-                with trace("engine.prefill"):
-                    self._prefill()
-            if self._share_deferred and not any(r.output_ids for r in self.running.values()):
-                # requests are waiting for a prefix this step published: admit them before the
-                # first decode, so the batch decodes in lock-step (no extra tail of decode steps)
-                return []
-            with trace("engine.decode"):
-                if self._spec_ok():
-                    return self._spec_decode()
-                return self._decode()
+        self._drain_inbox()
+        sync = self._sync()
+        if sync is False:
+            raise StopIteration("engine stopped by rank 0")
+        if sync == "reset":
+            return []
+        self._reap_aborted()
+        self._share_deferred = False
+        self._admit()
+        if self.prefilling or self.waiting:
+            with trace("engine.prefill"):
+                self._prefill()
+        if self._share_deferred and not any(r.output_ids for r in self.running.values()):
+            # requests are waiting for a prefix this step published: admit them before the
+            # first decode, so the batch decodes in lock-step (no extra tail of decode steps)
+            return []
+        with trace("engine.decode"):
+            if self._spec_ok():
+                return self._spec_decode()
+            return self._decode()
 
     def serve_worker(self) -> None:
-        """Non-zero TP ranks: follow rank 0's schedule until it sends stop."""
+        """Non-zero TP ranks: follow rank 0's schedule until it sends stop.  A collective failure or stall seen
+        here is reported to rank 0 with the next exchange; rank 0's reset command recovers this rank."""
         assert self.control is not None and self.control.rank != 0
         while True:
             try:
                 self.step()
             except StopIteration:
                 return
+            except (CollectiveError, EngineStalled) as e:
+                log.error(f"TP worker rank {self.control.rank}: {e}; waiting for rank 0's reset")
 
     def kv_utilization(self) -> float:
         return 1.0 - self.allocator.num_free / self.allocator.num_blocks
@@ -892,19 +1100,38 @@ class LLMEngine:
                 if self._bg_stop:
                     return
             try:
+                if not self.ready:
+                    # requests queued while not ready fail fast (the decision service falls back); a recovery
+                    # attempt with a short drain bound runs before each wait
+                    if not self.recover(drain_timeout=0.05):
+                        self._fail_pending(EngineUnavailable(self.health["reason"] or "engine not ready"))
+                        with self._wake:
+                            self._wake.wait(0.05)
+                        continue
                 self.step()
                 time.sleep(0)   # let threads blocked on the GIL / engine lock in before the next step
-            except Exception as e:  # noqa: BLE001 -- every pending request fails, the loop keeps serving
+            except RequestRejected as e:   # only the offending request fails
+                r = e.request
+                r.error = e
+                self._finish(r, "error")
+            except (CollectiveError, EngineStalled, EngineUnavailable) as e:
+                # collective state unknown: every in-flight request fails; recovery runs on the next iteration
+                self._bg_error = e
+                self._fail_pending(e)
+            except Exception as e:  # noqa: BLE001 -- host-side bug: fail what was in flight, keep serving
                 log.error(f"Engine step failed: {e!r}")
                 self._bg_error = e
-                with self.lock:
-                    self._drain_inbox()
-                    for r in list(self.requests.values()):
-                        if not r.finished:
-                            r.error = e
-                            if r in self.waiting:
-                                self.waiting.remove(r)
-                            self._finish(r, "error")
+                self._fail_pending(e)
+
+    def _fail_pending(self, e: BaseException) -> None:
+        with self.lock:
+            self._drain_inbox()
+            for r in list(self.requests.values()):
+                if not r.finished:
+                    r.error = e
+                    if r in self.waiting:
+                        self.waiting.remove(r)
+                    self._finish(r, "error")
 
     # ------------------------------------------------------------------ blocking API
     def output(self, r: Request) -> Output:
@@ -922,25 +1149,35 @@ class LLMEngine:
             params = [params or SamplingParams()] * len(prompts)
         if self._bg_thread is not None:
             return self._generate_bg(prompts, params, deadline)
+        if not self.ready and not self.recover(drain_timeout=0.05):
+            raise EngineUnavailable(self.health["reason"] or "decision engine not ready")
         with self.lock:
-            reqs = [self.add_request(p, sp) for p, sp in zip(prompts, params)]
-            while not all(r.finished for r in reqs):
-                if deadline is not None and time.monotonic() > deadline:
-                    for r in reqs:
-                        if not r.finished:
-                            r.aborted = True
-                    if self.control is None:
-                        self._reap_aborted()
-                    for r in reqs:
-                        self.requests.pop(r.rid, None) if r.finished else None
-                    raise TimeoutError("decision engine deadline exceeded")
-                try:
-                    self.step()
-                except StopIteration:
-                    raise
-                except Exception:
-                    # an engine / collective failure ends these requests (their slots and KV blocks
-                    # are released) and propagates to the decision service's retry / breaker path
+            self._call_deadline = deadline
+            try:
+                return self._generate_sync(prompts, params, deadline)
+            finally:
+                self._call_deadline = None
+
+    def _generate_sync(self, prompts, params, deadline: Optional[float]) -> List[Output]:
+        reqs = [self.add_request(p, sp) for p, sp in zip(prompts, params)]
+        while not all(r.finished for r in reqs):
+            if deadline is not None and time.monotonic() > deadline:
+                for r in reqs:
+                    if not r.finished:
+                        r.aborted = True
+                if self.control is None:
+                    self._reap_aborted()
+                for r in reqs:
+                    self.requests.pop(r.rid, None) if r.finished else None
+                raise TimeoutError("decision engine deadline exceeded")
+            try:
+                self.step()
+            except StopIteration:
+                raise
+            except RequestRejected as e:
+                e.request.error = e
+                self._finish(e.request, "error")
+                if e.request in reqs:
                     for r in reqs:
                         if not r.finished:
                             if r in self.waiting:
@@ -948,10 +1185,20 @@ class LLMEngine:
                             self._finish(r, "error")
                         self.requests.pop(r.rid, None)
                     raise
-            outs = [self.output(r) for r in reqs]
-            for r in reqs:
-                self.requests.pop(r.rid, None)
-            return outs
+            except Exception:
+                # an engine / collective failure ends these requests (their slots and KV blocks
+                # are released) and propagates to the decision service's retry / breaker path
+                for r in reqs:
+                    if not r.finished:
+                        if r in self.waiting:
+                            self.waiting.remove(r)
+                        self._finish(r, "error")
+                    self.requests.pop(r.rid, None)
+                raise
+        outs = [self.output(r) for r in reqs]
+        for r in reqs:
+            self.requests.pop(r.rid, None)
+        return outs
 
     def _generate_bg(self, prompts, params, deadline: Optional[float]) -> List[Output]:
         reqs = [self.add_request(p, sp) for p, sp in zip(prompts, params)]

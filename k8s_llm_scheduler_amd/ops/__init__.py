@@ -501,6 +501,100 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
     return out
 
 
+# ----------------------------------------------------------------------------- big-tile MFMA GEMM (prefill rows)
+_PG_CFGS: Optional[list] = None
+
+
+def pgemm_configs() -> list:
+    """(BP weight rows, BQ tokens, LDS bytes) of every compiled pgemm.hip tile configuration."""
+    global _PG_CFGS
+    if _PG_CFGS is None:
+        _PG_CFGS = [tuple(c) for c in native().pgemm_configs()]
+    return _PG_CFGS
+
+
+def pgemm_ok(N: int, K: int, fp8: bool) -> bool:
+    """pgemm.hip can run this shape: 128-byte k-tiles, 4-column output groups."""
+    return N % 4 == 0 and (K * (1 if fp8 else 2)) % 128 == 0
+
+
+def pgemm_tiles(cfg: int, M: int, N: int, epi: int) -> int:
+    bp, bq, _ = pgemm_configs()[cfg]
+    feat = bp // 2 if epi == EPI_SWIGLU else bp
+    return math.ceil(N / feat) * math.ceil(M / bq)
+
+
+def pgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: int = 0, splits: int = 1, group_m: int = 4,
+          res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
+          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Big-tile MFMA GEMM (pgemm.hip): epi(x[M, K] @ w[N, K].T) for prefill-size M.  Same contract as :func:`mgemm`
+    (bf16 or Fp8Weight, SwiGLU with w = [Wg; Wu], residual epilogue, RMS prologue with the gamma folded into w);
+    ``splits`` k-slices per output tile, ``group_m`` m-tiles per tile-order group."""
+    M, K = x.shape
+    fp8 = _is_fp8(w)
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    if not pgemm_ok(N, K, fp8):
+        raise ValueError(f"pgemm: unsupported shape N={N} K={K}")
+    if fp8 and rms_eps is not None:
+        raise ValueError("pgemm: the RMS prologue needs bf16 activations")
+    if res is not None and (epi != EPI_BF16 or res.shape != (M, N)):
+        raise ValueError("pgemm: residual epilogue needs a bf16 [M, N] residual and the bf16 epilogue")
+    nwg, n_ws, n_tk = native().pgemm_plan(M, N, K, epi, int(fp8), cfg, splits)
+    if out is None:
+        out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
+    ws = torch.empty(n_ws, dtype=F32, device=x.device) if n_ws > 0 else None
+    tk = _zeroed_scratch(x.device, "pgemm", 4 * n_tk, 64 * 1024) if n_tk > 0 else 0
+    rp = _chk(res, BF16, "res") if res is not None else 0
+    rms, eps = (1, float(rms_eps)) if rms_eps is not None else (0, 0.0)
+    if fp8:
+        xq, sx = quantize_act_fp8(x.contiguous())
+        native().pgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, xq.data_ptr(), w.q.data_ptr(),
+                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, splits, group_m, rp, 0, 0.0, -1)
+    else:
+        native().pgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"),
+                       _chk(w, BF16, "w"), 0, 0, M, N, K, epi, 0, cfg, splits, group_m, rp, rms, eps, -1)
+    del ws
+    return out
+
+
+_P4_CFGS: Optional[list] = None
+
+
+def pgemm4_configs() -> list:
+    """(BP weight rows, BQ tokens, LDS bytes) of every compiled pgemm4.hip tile configuration (4 waves)."""
+    global _P4_CFGS
+    if _P4_CFGS is None:
+        _P4_CFGS = [tuple(c) for c in native().pgemm4_configs()]
+    return _P4_CFGS
+
+
+def pgemm4_tiles(cfg: int, M: int, N: int, epi: int) -> int:
+    bp, bq, _ = pgemm4_configs()[cfg]
+    feat = bp // 2 if epi == EPI_SWIGLU else bp
+    return math.ceil(N / feat) * math.ceil(M / bq)
+
+
+def pgemm4(x: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, cfg: int = 0, splits: int = 1, group_m: int = 4,
+           res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """4-wave big-tile bf16 MFMA GEMM (pgemm4.hip): epi(x[M, K] @ w[N, K].T), K % 64 == 0.  ``splits`` k-slices per
+    tile (fp32 slabs + a parallel combine kernel); residual epilogue and RMS prologue as :func:`mgemm`."""
+    M, K = x.shape
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    if res is not None and (epi != EPI_BF16 or res.shape != (M, N)):
+        raise ValueError("pgemm4: residual epilogue needs a bf16 [M, N] residual and the bf16 epilogue")
+    _nwg, n_slab = native().pgemm4_plan(M, N, K, epi, cfg, splits)
+    if out is None:
+        out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
+    slab = torch.empty(n_slab, dtype=F32, device=x.device) if n_slab > 0 else None
+    rp = _chk(res, BF16, "res") if res is not None else 0
+    rms, eps = (1, float(rms_eps)) if rms_eps is not None else (0, 0.0)
+    native().pgemm4(out.data_ptr(), slab.data_ptr() if slab is not None else 0, _chk(x, BF16, "x"), _chk(w, BF16, "w"),
+                    M, N, K, epi, cfg, splits, group_m, rp, rms, eps, -1)
+    del slab
+    return out
+
+
 def _mgemm_route(M: int, w, K: int, epi: int, fused: bool = False) -> bool:
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     return GEMM_BACKEND != "library" and _mgemm_ok(N, K, _is_fp8(w)) and \

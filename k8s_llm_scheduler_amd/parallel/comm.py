@@ -153,24 +153,68 @@ class TPGroup:
         self.ensure_healthy()
 
 
+    def reset_collectives(self, control: Optional["ControlChannel"] = None, timeout_s: float = 60.0) -> None:
+        """Recovery after a collective failure or stall (every rank of the replica calls this, with its device
+        drained): the xGMI protocol state goes back to its freshly-built state on every rank, an aborted or
+        failed RCCL communicator is replaced by a new one (unique id from the leader over the gloo control
+        group), and a bounded barrier makes sure no rank issues a collective before every rank has reset."""
+        if self.world <= 1 or self.simulate:
+            self.failed = None
+            return
+        torch.cuda.synchronize()
+        if self.xgmi is not None:
+            self.xgmi.reset()
+        if self.rccl is not None and (self.rccl.aborted or self.rccl.async_error()):
+            from .. import ops
+
+            if not self.rccl.aborted:
+                self.rccl.abort()
+            uid = ops.native().RcclComm.unique_id() if self.rank == 0 else None
+            if control is None:
+                raise CollectiveError("RCCL communicator rebuild needs the control channel")
+            uid = control.broadcast_object(uid)
+            self.rccl = ops.native().RcclComm(self.world, self.rank, uid)
+        if control is not None:
+            control.barrier(timeout_s)
+        self.failed = None
+
+    def abort_rccl(self) -> None:
+        """Abort the RCCL communicator so operations parked on a dead peer error out and the stream drains."""
+        if self.rccl is not None and not self.rccl.aborted:
+            self.rccl.abort()
+            self.failed = self.failed or f"RCCL communicator aborted on rank {self.rank}"
+
+
 class CollectiveError(RuntimeError):
     """A tensor-parallel collective failed; the decode results of this step are not trustworthy."""
 
 
 class ControlChannel:
-    """TP-rank-0 -> replica object broadcast on a CPU (gloo) group: the replica's leader (global
-    rank 0 runs the serving control plane) announces new requests, every other TP rank of the
-    replica follows its engine schedule (engine.LLMEngine._sync)."""
+    """TP-rank-0 -> replica schedule exchange on a CPU (gloo) group: the replica's leader (global rank 0
+    runs the serving control plane) announces new requests, aborts and reset commands, every other TP
+    rank follows its engine schedule (engine.LLMEngine._sync).  The exchange is an all-gather, so every
+    follower also reports its health each step: a collective failure seen by ONE rank (a peer that timed
+    out waiting for a stalled leader) reaches the leader before it launches more work."""
 
     def __init__(self, rank: int, group=None, src: int = 0):
         self.rank = rank      # TP rank within the replica
         self.group = group
         self.src = src        # global rank of the replica's leader
 
-    def exchange(self, payload):
-        obj = [payload]
-        dist.broadcast_object_list(obj, src=self.src, group=self.group)
-        return obj[0]
+    def exchange(self, payload, status=None):
+        """Leader: ``payload`` is the step message.  Returns (the leader's message, every rank's status)."""
+        objs = [None] * dist.get_world_size(self.group)
+        dist.all_gather_object(objs, (payload, status), group=self.group)
+        return objs[0][0], [o[1] for o in objs]
+
+    def barrier(self, timeout_s: float) -> None:
+        """Bounded barrier of the replica (gloo monitored barrier: raises if a rank does not arrive)."""
+        dist.monitored_barrier(group=self.group, timeout=datetime.timedelta(seconds=timeout_s))
+
+    def broadcast_object(self, obj):
+        box = [obj]
+        dist.broadcast_object_list(box, src=self.src, group=self.group)
+        return box[0]
 
 
 def replica_ranks(tp: TPGroup, replica: int) -> list:

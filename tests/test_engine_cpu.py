@@ -288,3 +288,24 @@ def test_nucleus_bins_cover_exact_nucleus():
         if extra:   # only boundary-bin ties: within 28/65536 in (M - l) / T of the last exact token
             lo = float(l[order[n - 1]])
             assert max((lo - float(l[i])) / T for i in extra) <= 28.0 / 65536 * 1.01
+
+
+@pytest.mark.parametrize("tp,slot_kib,expect_spec", [(2, 512, False), (4, 512, False), (8, 512, True),
+                                                       (4, 4096, True)])
+def test_spec_verify_graph_capture_gated_on_gather_size(tp, slot_kib, expect_spec):
+    """The speculative verify graph all-gathers SPEC_GRAPH_T rows of fp32 logits: at Llama-3.3-70B shapes
+    (vocab 128256) that is ~2 MB at TP=2 and ~1 MB at TP=4, above a 512 KiB xGMI slot, so that graph must not
+    be captured (eager verify) while one-row prefill buckets still are."""
+    from types import SimpleNamespace
+
+    from k8s_llm_scheduler_amd.engine.engine import SPEC_GRAPH_T, LLMEngine
+
+    vocab, hidden = 128256, 8192
+    xg = SimpleNamespace(slot_bytes=slot_kib << 10, max_allreduce_bytes=8 << 20)
+    fake = SimpleNamespace(model=SimpleNamespace(
+        tp=SimpleNamespace(world=tp, simulate=False, xgmi=xg, xgmi_max_ar=None),
+        cfg=SimpleNamespace(hidden=hidden),
+        lm_head=torch.empty(vocab // tp, 1)))
+    assert LLMEngine._prefill_bucket_capturable(fake, 16) is True        # one logits row: 257 KB at TP=2
+    got = LLMEngine._prefill_bucket_capturable(fake, SPEC_GRAPH_T, logits_rows=SPEC_GRAPH_T)
+    assert got is expect_spec

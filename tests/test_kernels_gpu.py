@@ -268,6 +268,33 @@ def test_nucleus_full_vocab_matches_reference(shards):
         assert out.tolist() == exp.tolist()
 
 
+def test_nucleus_scratch_shared_across_batch_sizes():
+    """One nucleus scratch buffer serves every batch size: top_p < 1 at B=1, then B=8, then B=3 on the same
+    buffer give the tokens of a run on a fresh buffer, and the row state is zero again afterwards (the
+    histograms of a small batch must never land in a larger batch's row state)."""
+    V = 128256
+    g = torch.Generator(DEV).manual_seed(11)
+    flat = torch.randn(8, V, device=DEV, generator=g) * 2.0
+    t = torch.full((8,), 0.7, device=DEV)
+    p = torch.tensor([0.9, 0.5, 0.8, 0.95, 0.6, 0.9, 0.7, 0.85], device=DEV)
+    seeds = torch.arange(1, 9, device=DEV, dtype=torch.int32)
+    ctr = torch.full((8,), 5, device=DEV, dtype=torch.int32)
+    fresh = {}
+    for B in (1, 8, 3):
+        ops._SCRATCH.pop(("sample_nucleus", torch.cuda.current_device()), None)   # a fresh zeroed buffer
+        fresh[B] = ops.sample(flat[:B].contiguous(), t[:B], p[:B], seeds[:B], ctr[:B], nucleus=True).cpu()
+    ops._SCRATCH.pop(("sample_nucleus", torch.cuda.current_device()), None)
+    ops.sample(flat[:8].contiguous(), t, p, seeds, ctr, nucleus=True)       # size the shared buffer for B=8
+    for B in (1, 8, 3, 8, 1):
+        got = ops.sample(flat[:B].contiguous(), t[:B], p[:B], seeds[:B], ctr[:B], nucleus=True).cpu()
+        assert got.tolist() == fresh[B].tolist(), f"B={B}"
+        torch.cuda.synchronize()
+        buf = ops._SCRATCH[("sample_nucleus", torch.cuda.current_device())]
+        rows = buf[: 4096 * 64].view(torch.int32).view(4096, 16)
+        # NucRow words 4 (maxkey), 7 (cnt0), 8 (cnt1) are re-armed to zero by every launch
+        assert int(rows[:, [4, 7, 8]].abs().sum()) == 0, f"row state not re-armed after B={B}"
+
+
 def test_hash_init_matches_reference():
     out = torch.empty(300, 257, dtype=torch.bfloat16, device=DEV)
     ops.hash_init_(out, gcols=1000, row0=7, col0=11, seed=3, tensor_id=9, scale=0.02)

@@ -12,8 +12,8 @@ for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursiv
         for r in csv.DictReader(fh):
             name = r.get("Kernel_Name", "?")
             short = name.split("(")[0].split("<")[0][-60:]
-            if "mgemm" in name:
-                short = "mgemm" + name[name.find("<"):name.find(">") + 1] if "<" in name else "mgemm"
+            if "mgemm" in name or "pgemm" in name:
+                short = name.split("(")[0].split("::")[-1][:90]
             acc[short][r.get("Counter_Name", "?")].append(float(r.get("Counter_Value", 0) or 0))
 for k, d in sorted(acc.items()):
     print(k)
