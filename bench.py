@@ -87,7 +87,8 @@ def main() -> int:
     from k8s_llm_scheduler_amd.control.prompt import PromptEngine
     from k8s_llm_scheduler_amd.engine import build_engine
     from k8s_llm_scheduler_amd.engine.synthetic import random_nodes, random_pod, reference_cluster
-    from k8s_llm_scheduler_amd.parallel import init_from_env
+    from k8s_llm_scheduler_amd.parallel import init_from_env, make_control_channel
+    from k8s_llm_scheduler_amd.parallel.replicas import ReplicaRouterBackend, make_replica_links, serve_replica
 
     logging.basicConfig(level=logging.WARNING, format="%(asctime)s %(levelname)s %(message)s")
     if args.verbose:
@@ -108,6 +109,12 @@ def main() -> int:
     dp = tp.replicas
     progress(f"process group ready (tp {tp.world}, comm {tp.comm_info.get('selected', '-')})")
 
+    # --arrival-rate on several ranks: rank 0 runs the scheduler, the other TP ranks of its replica follow its
+    # schedule (control channel), every other replica serves rank 0's requests over a link (least-loaded routing)
+    serving = args.arrival_rate > 0 and world > 1 and not tp.simulate
+    control = make_control_channel(tp) if serving else None
+    links = make_replica_links(tp) if serving else []
+
     t_init = time.perf_counter()
     bs = 16
     per_seq = max(2048, args.max_model_len) + args.gen_tokens + bs   # KV blocks reserved per decision
@@ -115,7 +122,7 @@ def main() -> int:
                        num_blocks=max(args.batch, 2) * (per_seq // bs + 2) + 64,
                        max_model_len=args.max_model_len, cuda_graphs=not args.no_graphs,
                        prefix_caching=not args.no_prefix_cache, capture=False, decode_chunk=8,
-                       weight_dtype=args.dtype, speculative_tokens=args.speculative)
+                       weight_dtype=args.dtype, speculative_tokens=args.speculative, control=control)
     progress("engine built")
     if eng.use_graphs:
         eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= max(1, args.batch)] or [1],
@@ -126,7 +133,16 @@ def main() -> int:
     progress(f"graphs captured, init {init_s:.1f}s")
 
     backend = LocalEngineBackend(eng, ignore_eos=True)
-    svc = DecisionService(backend, max_retries=3, max_tokens=args.gen_tokens, temperature=0.3, top_p=args.top_p,
+    if serving and tp.global_rank != 0:
+        if tp.rank == 0:
+            serve_replica(backend, links[0], eng)     # a remote replica's leader
+        else:
+            eng.serve_worker()                        # a TP follower of its replica's leader
+        dist.barrier()
+        dist.destroy_process_group()
+        return 0
+    router = ReplicaRouterBackend(backend, links) if links else None
+    svc = DecisionService(router or backend, max_retries=3, max_tokens=args.gen_tokens, temperature=0.3, top_p=args.top_p,
                           timeout=None, cache=None, breaker=CircuitBreaker())
     pe = PromptEngine(layout=args.prompt_layout)
     rng = random.Random(1234)
@@ -151,9 +167,14 @@ def main() -> int:
         raise SystemExit(f"prompt ({prompt_tokens} tokens) + --gen-tokens {args.gen_tokens} exceeds --max-model-len "
                          f"{args.max_model_len}: raise --max-model-len")
     if args.arrival_rate > 0:
-        if world > 1 and not tp.simulate:
-            raise SystemExit("--arrival-rate is a single-rank serving benchmark")
-        return run_arrivals(args, eng, svc, prompt_tokens, init_s, tp)
+        rc = run_arrivals(args, eng, svc, prompt_tokens, init_s, tp, router)
+        if serving:
+            if router is not None:
+                router.shutdown()
+            eng.shutdown_workers()
+            dist.barrier()
+            dist.destroy_process_group()
+        return rc
 
     distributed = world > 1 and not tp.simulate
 
@@ -241,7 +262,7 @@ def main() -> int:
     return 0
 
 
-def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
+def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp, router=None) -> int:
     """Continuous-mode serving under Poisson arrivals: the reference's watch -> decide -> bind loop
     (scheduler.py:662-729) with pods created at exponential inter-arrival times on an in-memory
     apiserver (3-node kind cluster); latency = pod creation -> successful binding."""
@@ -332,7 +353,7 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
         "metric": "scheduling_decisions_per_sec",
         "value": round(len(lat) / span, 4),
         "unit": "decisions/s",
-        "n_gpus": tp.world,
+        "n_gpus": tp.world * tp.replicas,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000 * span / max(1, len(lat)), 3),
@@ -343,7 +364,9 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp) -> int:
         "data": "synthetic Poisson pod arrivals on an in-memory apiserver, random-init weights",
         "config": {"model": args.preset, "arrival_rate_pods_per_s": args.arrival_rate, "prompt_tokens": prompt_tokens,
                    "gen_tokens": args.gen_tokens, "scheduler_mode": "continuous",
-                   "parallelism": f"tp{tp.world}" + ("-SIMULATED-no-comm" if tp.simulate else "")},
+                   "parallelism": (f"dp{tp.replicas}-" if tp.replicas > 1 else "") + f"tp{tp.world}"
+                   + ("-SIMULATED-no-comm" if tp.simulate else ""),
+                   "replica_dispatch": list(router.dispatched) if router is not None else None},
         "p50_detect_to_bind_ms": round(1000 * statistics.median(lat), 2),
         "p99_detect_to_bind_ms": round(1000 * lat[min(len(lat) - 1, int(0.99 * len(lat)))], 2),
         "max_detect_to_bind_ms": round(1000 * lat[-1], 2),

@@ -9,6 +9,8 @@
 #include <pybind11/stl.h>
 
 #include <cstdint>
+#include <cstring>
+#include <stdexcept>
 #include <string>
 
 #include "runtime/block_allocator.h"
@@ -56,8 +58,10 @@ int k8s_decode_attention_split(void* out, void* part, uint32_t* counters, const 
                                float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax,
                                hipStream_t s);
 int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
-               const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist,
-               int hist_stride, int* steps, void* scratch, void* nuc_scratch, hipStream_t s);
+               const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist, int hist_stride,
+               int* steps, void* scratch, void* nuc_scratch, const int* slots, const int* stop_cls, int* stop_json,
+               const int* stop_cfg, const int* stop_forced, const int* stop_forced_len, int stop_fstride,
+               int stop_eos_tok, int* stop_done, hipStream_t s);
 long long k8s_sample_scratch_bytes(int B);
 long long k8s_sample_nucleus_bytes(int B, int shards);
 int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab, hipStream_t s);
@@ -194,12 +198,27 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("sample", [](uintptr_t tokens, uintptr_t logits, int B, int Vs, int shards, uintptr_t temp, uintptr_t top_p,
                      uintptr_t seeds, uintptr_t counter, uintptr_t ctx_inc, uintptr_t hist, int hist_stride,
-                     uintptr_t steps, uintptr_t scratch, uintptr_t nuc_scratch, int64_t s) {
+                     uintptr_t steps, uintptr_t scratch, uintptr_t nuc_scratch, uintptr_t slots, uintptr_t cls,
+                     uintptr_t json, uintptr_t cfg, uintptr_t forced, uintptr_t forced_len, int fstride, int eos_tok,
+                     uintptr_t done, int64_t s) {
     check(k8s_sample(P<int>(tokens), P<float>(logits), B, Vs, shards, P<float>(temp), P<float>(top_p),
                      P<uint32_t>(seeds), P<int>(counter), P<int>(ctx_inc), P<int>(hist), hist_stride, P<int>(steps),
-                     P(scratch), P(nuc_scratch), S(s)),
+                     P(scratch), P(nuc_scratch), P<int>(slots), P<int>(cls), P<int>(json), P<int>(cfg), P<int>(forced),
+                     P<int>(forced_len), fstride, eos_tok, P<int>(done), S(s)),
           "sample");
   });
+  // Host memory the GPU can write (fine-grained, coherent): the decode graphs' done flags, polled by the host
+  // between replays without a device synchronisation.
+  m.def("host_mapped_alloc", [](size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      throw std::runtime_error("hipHostMalloc failed");
+    std::memset(p, 0, bytes);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) throw std::runtime_error("hipHostGetDevicePointer failed");
+    return py::make_tuple(reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(d));
+  });
+  m.def("host_mapped_free", [](uintptr_t p) { (void)hipHostFree(reinterpret_cast<void*>(p)); });
   m.def("sample_scratch_bytes", [](int B) { return k8s_sample_scratch_bytes(B); });
   m.def("sample_nucleus_bytes", [](int B, int shards) { return k8s_sample_nucleus_bytes(B, shards); });
   m.def("embedding", [](uintptr_t out, uintptr_t ids, uintptr_t table, int T, int H, int vocab, int64_t s) {

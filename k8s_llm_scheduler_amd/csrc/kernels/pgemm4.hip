@@ -140,13 +140,16 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
 #pragma unroll
   for (int f = 0; f < FQ; ++f) ss[f] = 0.f;
 
-  auto mma = [&](const bf16x8* A, const bf16x8* B, bool sq) {
-    __builtin_amdgcn_s_setprio(1);
+  // MFMAs of fragment rows [i0, i1) on one k-step's registers (+ the RMS squares of the x fragments)
+  auto mma = [&](const bf16x8* A, const bf16x8* B, int i0, int i1) {
 #pragma unroll
     for (int i = 0; i < FP; ++i)
+      if (i >= i0 && i < i1)
 #pragma unroll
-      for (int j = 0; j < FQ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+        for (int j = 0; j < FQ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
+  };
+  auto squares = [&](const bf16x8* B, bool sq) {
     if constexpr (RMS) {
       if (sq) {   // the two wave rows hold the same x fragments: each squares every other k-step
 #pragma unroll
@@ -159,14 +162,16 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
       }
     }
   };
-  // one k-step s: make s+1 visible, refill the slot of s-1 with s+3, read s+1, MFMA on s.  The steady-state
-  // loop runs the unconditional form (every k-step it touches exists); the last 2-4 k-steps are peeled
+  // One k-step s: make s+1 visible (counted vmcnt + barrier), refill the slot of s-1 with s+3 (LDS-DMA), read
+  // s+1 into the other register set, then the 64 MFMAs on s (registers read one k-step earlier).
   auto step_full = [&](int s, bf16x8* Ac, bf16x8* Bc, bf16x8* An, bf16x8* Bn) {
     p4_vmcnt<G>();
     p4_sync();
+    __builtin_amdgcn_sched_barrier(0);
     issue(s + 3);
     rd(s + 1, An, Bn);
-    mma(Ac, Bc, (s & 1) == wr);
+    mma(Ac, Bc, 0, FP);
+    squares(Bc, (s & 1) == wr);
   };
   auto step_tail = [&](int s, bf16x8* Ac, bf16x8* Bc, bf16x8* An, bf16x8* Bn) {
     if (s + 1 < n) {
@@ -175,7 +180,8 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
       if (s + 3 < n) issue(s + 3);
       rd(s + 1, An, Bn);
     }
-    mma(Ac, Bc, (s & 1) == wr);
+    mma(Ac, Bc, 0, FP);
+    squares(Bc, (s & 1) == wr);
   };
 
   // n is even (the host splits K in 64-deep units): the loop body is two k-steps with fixed register sets
@@ -361,7 +367,8 @@ constexpr int kP4NumCfgs = sizeof(kP4Cfgs) / sizeof(kP4Cfgs[0]);
 
 template <int C, int EPI, bool RMS>
 int p4_launch(const P4Args& a, hipStream_t s) {
-  hipLaunchKernelGGL((pgemm4_kernel<kP4Cfgs[C].fp, kP4Cfgs[C].fq, EPI, RMS>), dim3(a.nwg), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((pgemm4_kernel<kP4Cfgs[C].fp, kP4Cfgs[C].fq, EPI, RMS>), dim3(a.nwg), dim3(256), 0,
+                     s, a);
   return (int)hipGetLastError();
 }
 template <int C>

@@ -92,15 +92,95 @@ __device__ __forceinline__ unsigned long long pack_key(float score, int idx) {
   return ((unsigned long long)ord_key(score) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)idx);
 }
 
-__device__ __forceinline__ void write_token(int b, int tok, int* __restrict__ tokens, int* __restrict__ ctx_inc,
-                                            int* __restrict__ hist, int hist_stride, int* __restrict__ steps) {
-  tokens[b] = tok;
-  if (hist != nullptr) {
-    const int st = steps[b];
-    if (st < hist_stride) hist[(size_t)b * hist_stride + st] = tok;
-    steps[b] = st + 1;
+// Device-side stop detection of the decode graphs.  Per token, a class word built once from
+// the tokenizer vocabulary: x = eos (bit 0) | net brace delta (int8, bits 8-15) | min running depth relative to
+// the entry (int8, 16-23); y = holds a '{' (bit 0) | depth at the end when the first '{' of the answer is in it
+// (int8, 8-15) | min depth after that '{' (int8, 16-23).  Per slot: json state (-2: the prefill's first token is
+// not classified yet, -1: no '{' yet, d >= 1: depth) and cfg = eos stop (bit 0) | json stop (bit 1) |
+// max_tokens << 8.  The naive brace counter is the one of control/jsonextract.py json_object_closed, so the
+// device and the host agree on when an answer's first object closes.
+struct StopArgs {
+  const int2* cls;        // [vocab] token classes, or null (stop detection off)
+  int* json;              // [slots]
+  const int* cfg;         // [slots]
+  const int* forced;      // [slots][fstride] scripted answer tokens, or null
+  const int* forced_len;  // [slots]: -1 = sample; >= 0 = write forced[st] (EOS past the end)
+  int fstride;
+  int eos_tok;
+  int* done;              // [slots] host-mapped flags: set when the slot's answer finishes
+};
+
+__device__ __forceinline__ int json_step(int state, int2 c, bool& closed) {
+  closed = false;
+  if (state >= 1) {
+    const int amin = (int)(int8_t)((c.x >> 16) & 0xff), adelta = (int)(int8_t)((c.x >> 8) & 0xff);
+    if (state + amin <= 0) {
+      closed = true;
+      return 0;
+    }
+    return state + adelta;
   }
-  if (ctx_inc != nullptr) ctx_inc[b] += 1;
+  if (c.y & 1) {
+    const int bmin = (int)(int8_t)((c.y >> 16) & 0xff), bend = (int)(int8_t)((c.y >> 8) & 0xff);
+    if (bmin <= 0) {
+      closed = true;
+      return 0;
+    }
+    return bend;
+  }
+  return state;
+}
+
+// Decode-state update of state slot s (= the row, or slots[row]): tokens[s] = tok; hist[s][steps[s]] = tok;
+// steps[s]++; ctx[s]++ -- or, when the answer finished (EOS, closed JSON object, max_tokens), ctx[s] = 0 (later
+// replays skip the slot) and the host-mapped done flag.
+__device__ __forceinline__ void write_token(int s, int tok, int* __restrict__ tokens, int* __restrict__ ctx_inc,
+                                            int* __restrict__ hist, int hist_stride, int* __restrict__ steps,
+                                            const StopArgs& sa) {
+  const int st = steps != nullptr ? steps[s] : 0;
+  bool fin = false;
+  if (sa.cls != nullptr && hist != nullptr && ctx_inc != nullptr) {
+    const int cfg = sa.cfg[s], max_new = cfg >> 8;
+    int state = sa.json[s];
+    bool closed = false;
+    if (state == -2) {   // the first token, sampled by the prefill
+      const int t0 = hist[(size_t)s * hist_stride];
+      state = -1;
+      if ((cfg & 1) && (sa.cls[t0].x & 1)) {
+        fin = true;
+      } else if (cfg & 2) {
+        state = json_step(state, sa.cls[t0], closed);
+        fin = closed;
+      }
+      if (!fin && st >= max_new) fin = true;
+      if (fin) {   // the answer ended at its first token: emit nothing more
+        sa.json[s] = state;
+        ctx_inc[s] = 0;
+        if (sa.done != nullptr) __hip_atomic_store(&sa.done[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+    }
+    if (sa.forced != nullptr && sa.forced_len[s] >= 0)
+      tok = st < sa.forced_len[s] ? sa.forced[(size_t)s * sa.fstride + st] : sa.eos_tok;
+    const int2 c = sa.cls[tok];
+    if ((cfg & 1) && (c.x & 1)) {
+      fin = true;
+    } else {
+      if (cfg & 2) {
+        state = json_step(state, c, closed);
+        fin = closed;
+      }
+      if (st + 1 >= max_new) fin = true;
+    }
+    sa.json[s] = state;
+  }
+  tokens[s] = tok;
+  if (hist != nullptr) {
+    if (st < hist_stride) hist[(size_t)s * hist_stride + st] = tok;
+    steps[s] = st + 1;
+  }
+  if (ctx_inc != nullptr) ctx_inc[s] = fin ? 0 : ctx_inc[s] + 1;
+  if (fin && sa.done != nullptr) __hip_atomic_store(&sa.done[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // This workgroup's slice: inside ONE shard (gridDim.x = shards * per_shard), so a token is
@@ -121,18 +201,20 @@ __device__ __forceinline__ Slice slice_of(const float* logits, int b, int B, int
   return r;
 }
 
-__device__ __forceinline__ bool nuc_row(int b, const int* ctx_inc, const float* temperature, const float* top_p) {
-  return (ctx_inc == nullptr || ctx_inc[b] > 0) && temperature[b] > 0.f && top_p[b] < 1.f;
+__device__ __forceinline__ bool nuc_row(int b, const int* ctx_inc, const int* slots, const float* temperature,
+                                        const float* top_p) {
+  return (ctx_inc == nullptr || ctx_inc[slots != nullptr ? slots[b] : b] > 0) && temperature[b] > 0.f &&
+         top_p[b] < 1.f;
 }
 
 // pass 1: row max of the logits (ordered-key atomicMax)
 __global__ void __launch_bounds__(ST) nuc_max_kernel(const float* __restrict__ logits, int B, int Vs, int shards,
                                                      const float* __restrict__ temperature,
                                                      const float* __restrict__ top_p, const int* __restrict__ ctx_inc,
-                                                     NucRow* __restrict__ st) {
+                                                     const int* __restrict__ slots, NucRow* __restrict__ st) {
   __shared__ float red[ST / 64];
   const int b = blockIdx.y;
-  if (!nuc_row(b, ctx_inc, temperature, top_p)) return;
+  if (!nuc_row(b, ctx_inc, slots, temperature, top_p)) return;
   const Slice sl = slice_of(logits, b, B, Vs, shards);
   float m = -INFINITY;
   for (int j = sl.j0 + threadIdx.x; j < sl.j1; j += ST) m = fmaxf(m, sl.base[j]);
@@ -151,13 +233,14 @@ template <int LEVEL>
 __global__ void __launch_bounds__(ST) nuc_hist_kernel(const float* __restrict__ logits, int B, int Vs, int shards,
                                                       const float* __restrict__ temperature,
                                                       const float* __restrict__ top_p, const int* __restrict__ ctx_inc,
-                                                      NucRow* __restrict__ st, unsigned long long* __restrict__ ws) {
+                                                      const int* __restrict__ slots, NucRow* __restrict__ st,
+                                                      unsigned long long* __restrict__ ws) {
   __shared__ unsigned long long h[ST / 64][256];   // one histogram per wave: 4x fewer colliding atomics
   __shared__ unsigned long long scan[2][256];
   __shared__ uint32_t sh_prev;
   __shared__ int sh_sel;
   const int b = blockIdx.y;
-  if (!nuc_row(b, ctx_inc, temperature, top_p)) return;
+  if (!nuc_row(b, ctx_inc, slots, temperature, top_p)) return;
   const int tid = threadIdx.x, wid = tid >> 6;
   const float invT = 1.f / temperature[b];
   const float M = key_float(__hip_atomic_load(&st[b].maxkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -249,11 +332,13 @@ __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, co
                                                     const int* __restrict__ counter, int* __restrict__ ctx_inc,
                                                     int* __restrict__ hist, int hist_stride, int* __restrict__ steps,
                                                     unsigned long long* __restrict__ row_key,
-                                                    uint32_t* __restrict__ row_cnt, NucRow* __restrict__ nuc) {
+                                                    uint32_t* __restrict__ row_cnt, NucRow* __restrict__ nuc,
+                                                    const int* __restrict__ slots, StopArgs sa) {
   __shared__ float sv[ST / 64];
   __shared__ int si[ST / 64];
   const int b = blockIdx.y;
-  if (ctx_inc != nullptr && ctx_inc[b] <= 0) return;  // padded row
+  const int s = slots != nullptr ? slots[b] : b;       // decode-state slot of this row
+  if (ctx_inc != nullptr && ctx_inc[s] <= 0) return;  // padded (or finished) row
   const float T = temperature[b];
   const uint32_t seed = seeds[b];
   const uint32_t ctr = counter ? (uint32_t)counter[b] : 0u;
@@ -295,7 +380,7 @@ __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, co
         __hip_atomic_store(&w->cnt0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&w->cnt1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      write_token(b, tok, tokens, ctx_inc, hist, hist_stride, steps);
+      write_token(s, tok, tokens, ctx_inc, hist, hist_stride, steps, sa);
     }
   }
 }
@@ -314,9 +399,14 @@ using namespace k8sllm;
 //                the row states zero before the first call and left zero; the histograms are fully
 //                rewritten by every launch before they are read.
 constexpr int SAMPLE_ROW_CAP = 4096;
+// slots (or null): decode-state slot of every row (tokens / ctx_inc / hist / steps / stop state are indexed by
+// slot; temperature / top_p / seeds / counter by row).  stop_*: device-side stop detection (null cls = off).
 extern "C" int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
                           const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist,
-                          int hist_stride, int* steps, void* scratch, void* nuc_scratch, hipStream_t stream) {
+                          int hist_stride, int* steps, void* scratch, void* nuc_scratch, const int* slots,
+                          const int* stop_cls, int* stop_json, const int* stop_cfg, const int* stop_forced,
+                          const int* stop_forced_len, int stop_fstride, int stop_eos_tok, int* stop_done,
+                          hipStream_t stream) {
   if (B <= 0) return 0;
   if (B > SAMPLE_ROW_CAP) return -2;
   if (hist != nullptr && steps == nullptr) return -1;
@@ -329,12 +419,24 @@ extern "C" int k8s_sample(int* tokens, const float* logits, int B, int Vs, int s
   if (nuc_scratch != nullptr) {
     st = static_cast<NucRow*>(nuc_scratch);
     auto* ws = reinterpret_cast<unsigned long long*>(st + SAMPLE_ROW_CAP);
-    nuc_max_kernel<<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, st);
-    nuc_hist_kernel<0><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, st, ws);
-    nuc_hist_kernel<1><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, st, ws);
+    nuc_max_kernel<<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, slots, st);
+    nuc_hist_kernel<0><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, slots, st, ws);
+    nuc_hist_kernel<1><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, slots, st, ws);
   }
+  StopArgs sa;
+  sa.cls = reinterpret_cast<const int2*>(stop_cls);
+  sa.json = stop_json;
+  sa.cfg = stop_cfg;
+  sa.forced = stop_forced;
+  sa.forced_len = stop_forced_len;
+  sa.fstride = stop_fstride;
+  sa.eos_tok = stop_eos_tok;
+  sa.done = stop_done;
+  if (sa.cls != nullptr && (sa.json == nullptr || sa.cfg == nullptr || hist == nullptr || ctx_inc == nullptr ||
+                            (sa.forced != nullptr && sa.forced_len == nullptr)))
+    return -1;
   sample_kernel<<<grid, ST, 0, stream>>>(tokens, logits, B, Vs, shards, temperature, top_p, seeds, counter, ctx_inc,
-                                         hist, hist_stride, steps, key, cnt, st);
+                                         hist, hist_stride, steps, key, cnt, st, slots, sa);
   return (int)hipGetLastError();
 }
 

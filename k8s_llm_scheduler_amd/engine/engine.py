@@ -160,8 +160,15 @@ class LLMEngine:
                  max_model_len: Optional[int] = None, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
                  prefix_caching: bool = True, decode_chunk: int = 4, seed: int = 0, metrics=None,
                  control=None, capture_nucleus: bool = False, speculative_tokens: int = 0,
-                 watchdog_s: float = 60.0, on_unrecoverable: str = "stay"):
+                 watchdog_s: float = 60.0, on_unrecoverable: str = "stay", device_stop: bool = True,
+                 mixed_steps: bool = True):
         self.model = model
+        # Device-side stop detection: the decode graphs' sampler finishes rows itself (EOS,
+        # closed JSON object, max_tokens) and raises a host-mapped flag; the host checks it after every replay
+        # instead of after a whole decode_chunk.  Mixed steps (item 5): a prefill step also advances every
+        # running decode by one token in the same varlen forward, and new arrivals end a decode chunk early.
+        self.device_stop = bool(device_stop)
+        self.mixed_steps = bool(mixed_steps)
         # Bounded device waits: every host wait for device results polls an event against
         # min(call deadline, step start + watchdog_s) instead of blocking in a synchronize, so a hung collective
         # surfaces as EngineStalled inside llm.timeout.  ``on_unrecoverable``: "exit" ends the process (exit code
@@ -176,6 +183,13 @@ class LLMEngine:
         self._last_event = None
         self._pinned: Dict[tuple, torch.Tensor] = {}
         self.health = {"ready": True, "reason": "", "failures": 0, "recoveries": 0, "since": time.time()}
+        # test fault injection on a follower rank: ("stall", step, seconds) sleeps before that step's device work,
+        # ("raise", step, 0) fails that step with a CollectiveError after its collectives ran (step = 1-based
+        # count of schedule messages)
+        self.fault: Optional[tuple] = None
+        self._steps = 0
+        if control is not None and control.rank == 0:
+            control.start_monitor()
         # prompt-lookup speculative decoding (_spec_decode): drafted tokens per step, 0 = off
         self.speculative_tokens = max(0, int(speculative_tokens))
         # also capture decode graphs with the top-p passes (config llm.top_p < 1); otherwise chunks
@@ -236,6 +250,7 @@ class LLMEngine:
         # background serving loop (start_background): callers of generate() only touch the inbox and
         # wait on their requests' events, so a submitter never waits for a whole engine step
         self._inbox: List[Request] = []
+        self._pf_events: List[tuple] = []   # (start, end) CUDA events of prefills not accounted yet
         self._inbox_lock = threading.Lock()
         self._wake = threading.Condition(self._inbox_lock)
         self._bg_thread: Optional[threading.Thread] = None
@@ -245,7 +260,8 @@ class LLMEngine:
         self.stats = {"prefill_tokens": 0, "cached_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "graph_replays": 0, "prefill_graph_replays": 0, "prefill_overlap_chunks": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "spec_steps": 0, "spec_graph_replays": 0, "spec_drafted": 0,
-                      "spec_accepted": 0, "stalls": 0}
+                      "spec_accepted": 0, "stalls": 0, "mixed_steps": 0, "mixed_decode_rows": 0,
+                      "early_chunk_stops": 0}
 
     # ------------------------------------------------------------------ bounded device waits / health
     def _wait_limit(self) -> Optional[float]:
@@ -288,11 +304,18 @@ class LLMEngine:
             buf.copy_(t, non_blocking=True)
             outs.append(buf)
         self._wait_device(what)
+        if self._pf_events:
+            self._account_prefill()
         return outs
 
     def _fail(self, reason: str) -> None:
         if self.health["ready"]:
             log.error(f"Decision engine not ready: {reason}")
+            if self.control is not None and self.control.rank != 0:
+                try:
+                    self.control.report_failure(reason)
+                except Exception as e:  # noqa: BLE001
+                    log.error(f"failure report to rank 0 failed: {e!r}")
         self.health.update(ready=False, reason=reason, failures=self.health["failures"] + 1, since=time.time())
         if self.metrics is not None and hasattr(self.metrics, "engine_health"):
             self.metrics.engine_health(False)
@@ -305,7 +328,8 @@ class LLMEngine:
         """(live, ready, detail) for /healthz and /readyz: live while the serving loop (if started) runs."""
         t = self._bg_thread
         live = t is None or t.is_alive()
-        return live, self.ready, {"reason": self.health["reason"], "failures": self.health["failures"],
+        peer = self.control.peer_failure() if self.control is not None and self.control.rank == 0 else None
+        return live, self.ready and not peer, {"peer_failure": peer, "reason": self.health["reason"], "failures": self.health["failures"],
                                   "recoveries": self.health["recoveries"], "stalls": self.stats["stalls"]}
 
     def _drained(self, timeout_s: float) -> bool:
@@ -347,6 +371,7 @@ class LLMEngine:
         try:
             if announce and self.control is not None and self.control.rank == 0:
                 self.control.exchange({"new": [], "abort": [], "stop": False, "reset": True})
+                self.control.clear_failures()
             err = EngineUnavailable(self.health["reason"] or "engine reset")
             for r in list(self.requests.values()) + list(self.waiting) + list(self.prefilling) + \
                     list(self.running.values()):
@@ -410,6 +435,31 @@ class LLMEngine:
         self.p_packed = torch.zeros(3 * Tm + 4 + _P_SPLIT, **i32)
         self.p_bt = torch.zeros(1, self.max_blocks_per_seq, **i32)
         self.v_last = torch.arange(SPEC_GRAPH_T, **i32)       # the verify graph's logits rows: all of them
+        # device-side stop detection state (sampler.hip StopArgs)
+        self.s_json = torch.full((B,), -2, **i32)
+        self.s_cfg = torch.zeros(B, **i32)
+        self.s_forced = torch.zeros(B, self.max_new_cap, **i32)
+        self.s_forced_len = torch.full((B,), -1, **i32)
+        self.stop_cls = ops.token_stop_classes(self.tok, self.model.cfg.vocab).to(dev)
+        if self.gpu:
+            host, devp = ops.native().host_mapped_alloc(4 * B)
+            import ctypes
+
+            import numpy as np
+
+            self._done_ptr = devp
+            self._done_host = np.ctypeslib.as_array((ctypes.c_int32 * B).from_address(host))
+            self._done_mem = host
+        else:
+            self._done_cpu = torch.zeros(B, dtype=torch.int32)
+            self._done_host = self._done_cpu.numpy()
+
+    def _stop_args(self) -> Optional[dict]:
+        if not self.device_stop:
+            return None
+        return {"cls": self.stop_cls, "json": self.s_json, "cfg": self.s_cfg, "forced": self.s_forced,
+                "forced_len": self.s_forced_len, "eos_tok": self.tok.eot_id,
+                "done": self._done_ptr if self.gpu else self._done_cpu}
 
     def _ctx_classes(self) -> List[int]:
         """Context-length classes with their own decode graph: contexts <= 1024 tokens (one
@@ -421,7 +471,7 @@ class LLMEngine:
                                            max_context or self.max_model_len)
         ops.sample(logits, self.s_temp[:B], self.s_top_p[:B], self.s_seeds[:B], self.s_ctx[:B],
                    shards=logits.shape[0], tokens_out=self.s_tokens[:B], ctx_inc=self.s_ctx[:B],
-                   hist=self.s_hist[:B], steps=self.s_steps[:B], nucleus=nucleus)
+                   hist=self.s_hist[:B], steps=self.s_steps[:B], nucleus=nucleus, stop=self._stop_args())
 
     @staticmethod
     def _wants_nucleus(reqs) -> bool:
@@ -615,23 +665,22 @@ class LLMEngine:
             self._enqueue(r)
 
     def _sync(self):
-        """Replicate rank 0's new requests and aborts to every rank, and collect every rank's health.  Returns
-        False on a stop command (worker shutdown), "reset" after a recovery reset (workers), else True.  A worker
-        that reports a failure makes rank 0 fail this step before it launches anything."""
+        """Replicate rank 0's new requests and aborts to every rank.  Returns False on a stop command (worker
+        shutdown), "reset" after a recovery reset (workers), else True.  Rank 0 first checks the followers'
+        failure reports: a collective failure seen by any rank fails this step before it launches anything."""
         if self.control is None:
             return True
-        status = None if self.ready and not self.model.tp.failed else (self.health["reason"] or self.model.tp.failed)
         if self.control.rank == 0:
+            peer = self.control.peer_failure()
+            if peer:
+                raise CollectiveError(peer)
             msg = {"new": [(r.rid, r.prompt_ids, r.params.__dict__, r.seed) for r in self._outbox],
                    "abort": sorted(r.rid for r in self.requests.values() if r.aborted and not r.finished),
                    "stop": False}
             self._outbox = []
-            _, statuses = self.control.exchange(msg, status)
-            bad = [(i, st) for i, st in enumerate(statuses) if st and i != 0]
-            if bad:
-                raise CollectiveError(f"TP rank(s) {[i for i, _ in bad]} failed: {bad[0][1]}")
+            self.control.exchange(msg)
             return True
-        msg, _ = self.control.exchange(None, status)
+        msg = self.control.exchange(None)
         if msg.get("stop"):
             return False
         if msg.get("reset"):
@@ -647,10 +696,16 @@ class LLMEngine:
         for rid in msg["abort"]:
             if rid in self.requests:
                 self.requests[rid].aborted = True
+        self._steps += 1
+        f = self.fault
+        if f is not None and f[0] == "stall" and self._steps == f[1]:
+            self.fault = None
+            time.sleep(f[2])   # fault injection (tests): this follower stalls before its device work
         return True
 
     def shutdown_workers(self) -> None:
         if self.control is not None and self.control.rank == 0:
+            self.control.stop_monitor()
             self.control.exchange({"new": [], "abort": [], "stop": True})
 
     def _reap_aborted(self) -> None:
@@ -746,7 +801,13 @@ class LLMEngine:
         dev = self.device
         t = lambda x: torch.tensor(x, dtype=torch.int32).to(dev, non_blocking=True)
         t0 = time.perf_counter()
-        Tb = next((b for b in PREFILL_GRAPH_BUCKETS if b >= len(ids)), None) if len(chunk) == 1 else None
+        if self.gpu:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        # mixed step: every running decode rides along as a 1-token sequence (its next token), so an arrival's
+        # prefill does not stall the decodes in flight
+        dec = sorted(self.running) if self.mixed_steps and self.running else []
+        Tb = next((b for b in PREFILL_GRAPH_BUCKETS if b >= len(ids)), None) if len(chunk) == 1 and not dec else None
         if self.use_graphs and Tb is not None and Tb in self.prefill_graphs:
             r0 = chunk[0][0]
             self._fill_prefill_state(ids, pos, slots, ctx[0], r0.blocks, Tb)
@@ -754,6 +815,32 @@ class LLMEngine:
             graph.replay()
             self.stats["prefill_graph_replays"] += 1
             self.stats["prefill_overlap_chunks"] += bool(self._overlap_split_at(Tb))
+        elif dec:
+            d = torch.tensor(dec, dtype=torch.long, device=dev)
+            ctx_d = self.s_ctx.index_select(0, d)
+            pos_d = ctx_d - 1
+            blk = self.s_bt.index_select(0, d).gather(1, (pos_d // bs).long().unsqueeze(1)).squeeze(1)
+            n_p = len(ids)
+            ids_t = torch.cat([t(ids), self.s_tokens.index_select(0, d)])
+            pos_t = torch.cat([t(pos), pos_d])
+            slot_t = torch.cat([t(slots), blk * bs + pos_d % bs])
+            cu_all = cu + [cu[-1] + k + 1 for k in range(len(dec))]
+            ctx_t = torch.cat([t(ctx), ctx_d])
+            bt_t = torch.cat([bt.to(dev, non_blocking=True), self.s_bt.index_select(0, d)])
+            last_t = t(last + [n_p + k for k in range(len(dec))])
+            logits = self.model.forward_prefill(ids_t, pos_t, slot_t, t(cu_all), ctx_t, bt_t,
+                                                max(e - s for _, s, e in chunk), last_t)
+            # the decode rows' tokens: the decode graphs' sampler (same counters, same stop detection), with the
+            # state of each row's slot updated in place
+            ld = logits[:, len(chunk):].contiguous()
+            ops.sample(ld, self.s_temp.index_select(0, d), self.s_top_p.index_select(0, d),
+                       self.s_seeds.index_select(0, d), ctx_d.clone(), shards=ld.shape[0], tokens_out=self.s_tokens,
+                       ctx_inc=self.s_ctx, hist=self.s_hist, steps=self.s_steps,
+                       nucleus=self._wants_nucleus(self.running[x] for x in dec), slots=d.to(torch.int32),
+                       stop=self._stop_args())
+            logits = logits[:, :len(chunk)]
+            self.stats["mixed_steps"] += 1
+            self.stats["mixed_decode_rows"] += len(dec)
         else:
             bt_d = bt.to(dev, non_blocking=True)
             split = None
@@ -783,6 +870,10 @@ class LLMEngine:
             ctr = torch.tensor([len(r.prompt_ids) for r in rs], dtype=torch.int32, device=dev)
             toks = ops.sample(sub, temp, top_p, seeds, ctr, shards=sub.shape[0], nucleus=self._wants_nucleus(rs))
             slots_t = torch.tensor([r.slot for r in rs], dtype=torch.long, device=dev)
+            forced0 = [(k, r.params.forced_output_ids[0]) for k, r in enumerate(rs) if r.params.forced_output_ids]
+            if forced0:   # scripted answers replace the sampled first token too
+                fk = torch.tensor([k for k, _ in forced0], dtype=torch.long, device=dev)
+                toks = toks.index_copy(0, fk, torch.tensor([v for _, v in forced0], dtype=torch.int32, device=dev))
             self.s_tokens[slots_t] = toks
             self.s_ctx[slots_t] = ctr + 1
             self.s_hist[slots_t, 0] = toks
@@ -790,6 +881,7 @@ class LLMEngine:
             self.s_temp[slots_t] = temp
             self.s_top_p[slots_t] = top_p
             self.s_seeds[slots_t] = seeds
+            self._init_stop_state(rs, slots_t)
             for r in rs:
                 row = torch.zeros(self.max_blocks_per_seq, dtype=torch.int32)
                 row[:len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
@@ -800,10 +892,49 @@ class LLMEngine:
                 self.prefilling.remove(r)
                 self.running[r.slot] = r
         if self.gpu:
-            self.model.tp.snapshot_health()
-            self._wait_device("prefill")
-            self.model.tp.check_health()
-        self.stats["prefill_time"] += time.perf_counter() - t0
+            # no per-prefill wait: the decode that follows in this step waits (bounded) for both and checks the
+            # collectives' health; only a step that prefills and decodes nothing bounds its device work here.
+            # prefill_time is GPU time, from events read once they completed.
+            self._pf_events.append((ev0, torch.cuda.Event(enable_timing=True)))
+            self._pf_events[-1][1].record()
+            if not self.running:
+                self.model.tp.snapshot_health()
+                self._wait_device("prefill")
+                self.model.tp.check_health()
+                self._account_prefill()
+        else:
+            self.stats["prefill_time"] += time.perf_counter() - t0
+
+    def _account_prefill(self) -> None:
+        """Add the GPU time of completed prefills to stats["prefill_time"] (after a device wait)."""
+        keep = []
+        for a, b in self._pf_events:
+            if b.query():
+                self.stats["prefill_time"] += a.elapsed_time(b) / 1e3
+            else:
+                keep.append((a, b))
+        self._pf_events = keep
+
+    def _init_stop_state(self, rs: Sequence[Request], slots_t: torch.Tensor) -> None:
+        """Device stop state of freshly prefilled slots: first token unclassified (-2), stop config (EOS / JSON
+        close / max_tokens), the scripted answer of forced requests, done flag clear."""
+        if not self.device_stop:
+            return
+        dev = self.device
+        cfg, flen = [], []
+        for r in rs:
+            p = r.params
+            c = (0 if p.ignore_eos else 1) | (2 if p.stop_on_json_close and not p.ignore_eos else 0)
+            cfg.append(c | (min(p.max_tokens, self.max_new_cap) << 8))
+            f = p.forced_output_ids
+            flen.append(-1 if f is None else min(len(f), self.max_new_cap))
+            if f is not None and f:
+                n = min(len(f), self.max_new_cap)
+                self.s_forced[r.slot, :n] = torch.tensor(f[:n], dtype=torch.int32).to(dev, non_blocking=True)
+            self._done_host[r.slot] = 0
+        self.s_json[slots_t] = -2
+        self.s_cfg[slots_t] = torch.tensor(cfg, dtype=torch.int32, device=dev)
+        self.s_forced_len[slots_t] = torch.tensor(flen, dtype=torch.int32, device=dev)
 
     def _decode(self, max_steps: Optional[int] = None) -> List[Request]:
         if not self.running:
@@ -818,13 +949,27 @@ class LLMEngine:
         nuc = self._wants_nucleus(self.running.values())
         t0 = time.perf_counter()
         graph = self.graphs.get((B, mc, nuc)) if self.use_graphs else None
-        for _ in range(steps):
+        # device-side stop detection: the sampler sets a host-mapped done flag when an answer ends (EOS, closed
+        # JSON object, max_tokens, end of a scripted answer), so the chunk ends after the replay that finished a
+        # request instead of running its remaining replays.  The flags are read after a wait for the replay that
+        # wrote them, so every TP rank takes the same decision; a new arrival ends the chunk too on a single-rank
+        # engine (a TP engine's followers cannot see rank 0's arrivals mid-chunk).
+        early = self.device_stop and max_steps is None and steps > 1
+        live = list(self.running)
+        ran = 0
+        for i in range(steps):
             if graph is not None:
                 graph.replay()
                 self.stats["graph_replays"] += 1
             else:
                 self._decode_step(B, mc, nuc)
-        self.stats["decode_steps"] += steps
+            ran += 1
+            if early and i + 1 < steps:
+                self._wait_device("decode")
+                if self._done_host[live].any() or (self.control is None and self._inbox):
+                    self.stats["early_chunk_stops"] += 1
+                    break
+        self.stats["decode_steps"] += ran
         tp = self.model.tp
         tp.snapshot_health()             # rides on the bounded wait below
         hist, nsteps = self._fetch(self.s_hist[:B], self.s_steps[:B], what="decode")
@@ -839,10 +984,14 @@ class LLMEngine:
             for tkn in new:
                 if forced is not None:  # scripted answer; past its end: EOS
                     i = len(r.output_ids)
-                    tkn = forced[i] if i < len(forced) else next(iter(self.tok.eos_ids))
+                    tkn = forced[i] if i < len(forced) else self.tok.eot_id
                 r.output_ids.append(tkn)
                 if self._stopped(r, tkn):
                     break
+            if not r.finished and self.device_stop and self._done_host[slot]:
+                # the device ended the answer (its stop rules are the host's; this only guards a disagreement,
+                # which would otherwise leave a request whose slot no replay advances)
+                self._finish(r, "length" if len(r.output_ids) >= r.params.max_tokens else "stop")
             if r.finished:
                 finished.append(r)
             elif len(r.output_ids) >= r.params.max_tokens:
@@ -1020,7 +1169,13 @@ class LLMEngine:
             if not worker and not self.ready:
                 raise EngineUnavailable(self.health["reason"] or "decision engine not ready")
             try:
-                return self._step(worker)
+                out = self._step(worker)
+                f = self.fault
+                if worker and f is not None and f[0] == "raise" and self._steps == f[1]:
+                    # fault injection (tests): this follower's collectives of the step ran, then "failed"
+                    self.fault = None
+                    raise CollectiveError(f"injected collective failure on rank {self.control.rank}")
+                return out
             except (CollectiveError, EngineStalled) as e:
                 self._fail(str(e))
                 raise

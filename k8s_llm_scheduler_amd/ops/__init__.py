@@ -849,14 +849,20 @@ def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor,
            counter: torch.Tensor, *, shards: int = 1, tokens_out: Optional[torch.Tensor] = None,
            ctx_inc: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None,
-           steps: Optional[torch.Tensor] = None, nucleus: Optional[bool] = None) -> torch.Tensor:
+           steps: Optional[torch.Tensor] = None, nucleus: Optional[bool] = None,
+           slots: Optional[torch.Tensor] = None, stop: Optional[dict] = None) -> torch.Tensor:
     """Sample one token per row.  logits: [B, V] or sharded [shards, B, Vs] fp32.  Optionally
-    updates decode state in place: tokens_out[b] = tok, ctx_inc[b] += 1, hist[b, steps[b]] = tok,
-    steps[b] += 1 (rows with ctx_inc[b] <= 0 are padding and untouched).
+    updates decode state in place: tokens_out[s] = tok, ctx_inc[s] += 1, hist[s, steps[s]] = tok,
+    steps[s] += 1 (slots with ctx_inc[s] <= 0 are padding and untouched), where s = slots[b] (or b).
 
     ``nucleus``: run the top-p passes (rows with 0 < temperature and top_p < 1).  None = decide
     from the tensors (a device sync: not inside graph capture); False = top_p is ignored, which is
-    what a graph captured for top_p = 1 requests does (three fewer launches per token)."""
+    what a graph captured for top_p = 1 requests does (three fewer launches per token).
+
+    ``stop``: device-side stop detection of the decode graphs (sampler.hip StopArgs): dict with ``cls``
+    [vocab, 2] int32 token classes, ``json`` / ``cfg`` [slots] int32, optional ``forced`` [slots, n] /
+    ``forced_len`` [slots] scripted tokens, ``eos_tok`` and ``done`` (GPU: a host-mapped device pointer int;
+    CPU: an int32 tensor).  A finished answer sets ctx_inc[s] = 0 and done[s] = 1."""
     if logits.dim() == 3:
         S, B, Vs = logits.shape
     else:
@@ -864,30 +870,61 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
     if not _gpu(logits):
         full = logits.permute(1, 0, 2).reshape(B, S * Vs) if logits.dim() == 3 else logits
         toks = ref.sample(full, temperature, top_p, seeds, counter)
-        active = ctx_inc > 0 if ctx_inc is not None else torch.ones(B, dtype=torch.bool)
-        if tokens_out is not None:
-            tokens_out[:B] = torch.where(active, toks, tokens_out[:B])
-        if hist is not None:
-            for b in range(B):
-                if active[b] and int(steps[b]) < hist.shape[1]:
-                    hist[b, int(steps[b])] = toks[b]
-            steps[:B] += active.to(steps.dtype)
-        if ctx_inc is not None:
-            ctx_inc[:B] += active.to(ctx_inc.dtype)
+        idx = [int(slots[b]) if slots is not None else b for b in range(B)]
+        if stop is not None and hist is not None and ctx_inc is not None:
+            for b, s in enumerate(idx):
+                if int(ctx_inc[s]) > 0:
+                    ref.write_token_stop(s, int(toks[b]), tokens_out, ctx_inc, hist, steps, stop)
+            return toks
+        active = [ctx_inc is None or int(ctx_inc[s]) > 0 for s in idx]
+        for b, s in enumerate(idx):
+            if not active[b]:
+                continue
+            if tokens_out is not None:
+                tokens_out[s] = toks[b]
+            if hist is not None:
+                if int(steps[s]) < hist.shape[1]:
+                    hist[s, int(steps[s])] = toks[b]
+                steps[s] += 1
+            if ctx_inc is not None:
+                ctx_inc[s] += 1
         return toks
     if nucleus is None:
         nucleus = bool(((top_p < 1) & (temperature > 0)).any())
     out = tokens_out if tokens_out is not None else torch.empty(B, dtype=I32, device=logits.device)
     nuc = _zeroed_scratch(logits.device, "sample_nucleus", native().sample_nucleus_bytes(B, S),
                           native().sample_nucleus_bytes(64, S)) if nucleus else 0
+    if stop is not None:
+        fz = stop.get("forced")
+        st_args = (_chk(stop["cls"], I32, "stop.cls"), _chk(stop["json"], I32, "stop.json"),
+                   _chk(stop["cfg"], I32, "stop.cfg"), _chk(fz, I32, "stop.forced") if fz is not None else 0,
+                   _chk(stop["forced_len"], I32, "stop.forced_len") if fz is not None else 0,
+                   fz.shape[1] if fz is not None else 0, int(stop["eos_tok"]), int(stop["done"]))
+    else:
+        st_args = (0, 0, 0, 0, 0, 0, 0, 0)
     native().sample(_chk(out, I32, "tokens"), _chk(logits, F32, "logits"), B, Vs, S,
                     _chk(temperature, F32, "temperature"), _chk(top_p, F32, "top_p"),
                     _chk(seeds, I32, "seeds"), _chk(counter, I32, "counter"),
                     _chk(ctx_inc, I32, "ctx_inc") if ctx_inc is not None else 0,
                     _chk(hist, I32, "hist") if hist is not None else 0,
                     hist.shape[1] if hist is not None else 0,
-                    _chk(steps, I32, "steps") if steps is not None else 0, _sample_scratch(logits.device, B), nuc, -1)
+                    _chk(steps, I32, "steps") if steps is not None else 0, _sample_scratch(logits.device, B), nuc,
+                    _chk(slots, I32, "slots") if slots is not None else 0, *st_args, -1)
     return out
+
+
+_STOP_CLS: dict = {}
+
+
+def token_stop_classes(tok, vocab: int) -> torch.Tensor:
+    """[vocab, 2] int32 token classes for the sampler's device-side stop detection (EOS ids and brace counts of
+    every token's decoded text; reference.token_stop_classes), built once per tokenizer."""
+    key = (id(tok._tok), vocab)
+    if key not in _STOP_CLS:
+        n = min(vocab, tok._tok.get_vocab_size())
+        texts = tok._tok.decode_batch([[i] for i in range(n)], skip_special_tokens=True)
+        _STOP_CLS[key] = ref.token_stop_classes(texts, sorted(tok.eos_ids), vocab)
+    return _STOP_CLS[key]
 
 
 _SCRATCH: dict = {}

@@ -270,3 +270,105 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
         score = torch.where(keep, l / T + g, torch.full_like(l, float("-inf")))
         out[b] = int(torch.argmax(score))
     return out
+
+
+# ----------------------------------------------------------------------------- device-side stop detection (oracle)
+def token_stop_classes(texts, eos_ids, vocab: int) -> torch.Tensor:
+    """Per-token class words of sampler.hip's stop detection, [vocab, 2] int32, from each token's decoded text
+    (``texts[i]`` for token i; missing / special tokens: no braces).  x = eos | net brace delta << 8 | min running
+    depth relative to the entry << 16; y = has '{' | depth at the end counted from the token's first '{' << 8 |
+    min depth after that '{' << 16 (int8 fields)."""
+    def i8(v: int) -> int:
+        return max(-128, min(127, v)) & 0xFF
+
+    out = torch.zeros(vocab, 2, dtype=torch.int32)
+    xs, ys = [0] * vocab, [0] * vocab
+    for i, t in enumerate(texts[:vocab]):
+        if not t or ("{" not in t and "}" not in t):
+            continue
+        d = m = 0
+        for ch in t:
+            if ch == "{":
+                d += 1
+            elif ch == "}":
+                d -= 1
+                m = min(m, d)
+        xs[i] = (i8(d) << 8) | (i8(m) << 16)
+        k = t.find("{")
+        if k >= 0:
+            d2, m2 = 1, 1
+            for ch in t[k + 1:]:
+                if ch == "{":
+                    d2 += 1
+                elif ch == "}":
+                    d2 -= 1
+                    m2 = min(m2, d2)
+            ys[i] = 1 | (i8(d2) << 8) | (i8(m2) << 16)
+    for e in eos_ids:
+        if 0 <= e < vocab:
+            xs[e] |= 1
+    out[:, 0] = torch.tensor(xs, dtype=torch.int64).to(torch.int32)
+    out[:, 1] = torch.tensor(ys, dtype=torch.int64).to(torch.int32)
+    return out
+
+
+def _i8(v: int) -> int:
+    v &= 0xFF
+    return v - 256 if v >= 128 else v
+
+
+def json_step(state: int, cx: int, cy: int):
+    """(new state, closed) -- sampler.hip json_step."""
+    if state >= 1:
+        amin, adelta = _i8(cx >> 16), _i8(cx >> 8)
+        if state + amin <= 0:
+            return 0, True
+        return state + adelta, False
+    if cy & 1:
+        bmin, bend = _i8(cy >> 16), _i8(cy >> 8)
+        if bmin <= 0:
+            return 0, True
+        return bend, False
+    return state, False
+
+
+def write_token_stop(s: int, tok: int, tokens, ctx_inc, hist, steps, stop) -> None:
+    """sampler.hip write_token with stop detection, for state slot s (CPU reference of the decode graphs)."""
+    st = int(steps[s])
+    fin = False
+    cls, cfg = stop["cls"], int(stop["cfg"][s])
+    max_new = cfg >> 8
+    state = int(stop["json"][s])
+    if state == -2:
+        t0 = int(hist[s, 0])
+        state = -1
+        if (cfg & 1) and (int(cls[t0, 0]) & 1):
+            fin = True
+        elif cfg & 2:
+            state, fin = json_step(state, int(cls[t0, 0]), int(cls[t0, 1]))
+        if not fin and st >= max_new:
+            fin = True
+        if fin:
+            stop["json"][s] = state
+            ctx_inc[s] = 0
+            stop["done"][s] = 1
+            return
+    forced, flen = stop.get("forced"), stop.get("forced_len")
+    if forced is not None and int(flen[s]) >= 0:
+        tok = int(forced[s, st]) if st < int(flen[s]) else int(stop["eos_tok"])
+    cx, cy = int(cls[tok, 0]), int(cls[tok, 1])
+    if (cfg & 1) and (cx & 1):
+        fin = True
+    else:
+        if cfg & 2:
+            state, fin = json_step(state, cx, cy)
+        if st + 1 >= max_new:
+            fin = True
+    stop["json"][s] = state
+    tokens[s] = tok
+    if st < hist.shape[1]:
+        hist[s, st] = tok
+    steps[s] = st + 1
+    ctx_inc[s] = 0 if fin else int(ctx_inc[s]) + 1
+    if fin:
+        stop["done"][s] = 1

@@ -22,6 +22,7 @@ import datetime
 import logging
 import os
 import socket
+import threading
 import time
 from dataclasses import dataclass, field
 from typing import Optional
@@ -161,7 +162,8 @@ class TPGroup:
         if self.world <= 1 or self.simulate:
             self.failed = None
             return
-        torch.cuda.synchronize()
+        if self.xgmi is not None or self.rccl is not None:
+            torch.cuda.synchronize()
         if self.xgmi is not None:
             self.xgmi.reset()
         if self.rccl is not None and (self.rccl.aborted or self.rccl.async_error()):
@@ -190,22 +192,87 @@ class CollectiveError(RuntimeError):
 
 
 class ControlChannel:
-    """TP-rank-0 -> replica schedule exchange on a CPU (gloo) group: the replica's leader (global rank 0
-    runs the serving control plane) announces new requests, aborts and reset commands, every other TP
-    rank follows its engine schedule (engine.LLMEngine._sync).  The exchange is an all-gather, so every
-    follower also reports its health each step: a collective failure seen by ONE rank (a peer that timed
-    out waiting for a stalled leader) reaches the leader before it launches more work."""
+    """TP-rank-0 -> replica schedule broadcast on a CPU (gloo) group: the replica's leader (global rank 0
+    runs the serving control plane) announces new requests, aborts and reset commands, every other TP rank
+    follows its engine schedule (engine.LLMEngine._sync).  The broadcast is one-way, so a follower that
+    stalls never blocks the leader's host loop (the leader's bounded device waits catch the stall).
 
-    def __init__(self, rank: int, group=None, src: int = 0):
+    Followers report failures the other way through the process group's TCP store (``report_failure``);
+    the leader polls it from a background thread (``peer_failure``), so a collective failure seen by ONE
+    rank -- a peer that timed out waiting for a stalled leader -- reaches the leader without a per-step
+    round trip."""
+
+    def __init__(self, rank: int, group=None, src: int = 0, replica: int = 0, world: int = 1):
         self.rank = rank      # TP rank within the replica
         self.group = group
         self.src = src        # global rank of the replica's leader
+        self.replica = replica
+        self.world = world
+        self._store = None
+        self._failure: Optional[str] = None
+        self._monitor: Optional[threading.Thread] = None
+        self._monitor_stop = threading.Event()
 
-    def exchange(self, payload, status=None):
-        """Leader: ``payload`` is the step message.  Returns (the leader's message, every rank's status)."""
-        objs = [None] * dist.get_world_size(self.group)
-        dist.all_gather_object(objs, (payload, status), group=self.group)
-        return objs[0][0], [o[1] for o in objs]
+    def exchange(self, payload):
+        obj = [payload]
+        dist.broadcast_object_list(obj, src=self.src, group=self.group)
+        return obj[0]
+
+    # ---- failure reports (followers -> leader)
+    def _key(self, rank: int) -> str:
+        return f"k8s_engine_failure/{self.replica}/{rank}"
+
+    def store(self):
+        if self._store is None:
+            try:
+                self._store = dist.distributed_c10d._get_default_store()
+            except Exception:  # noqa: BLE001 -- no store (single process): reports are dropped
+                self._store = False
+        return self._store or None
+
+    def report_failure(self, reason: str) -> None:
+        st = self.store()
+        if st is not None:
+            st.set(self._key(self.rank), reason[:500])
+
+    def clear_failures(self) -> None:
+        st = self.store()
+        if st is not None:
+            for r in range(self.world):
+                st.set(self._key(r), "")
+        self._failure = None
+
+    def start_monitor(self, period_s: float = 0.05) -> None:
+        """Leader: poll the followers' failure keys in the background."""
+        if self.rank != 0 or self.world <= 1 or self._monitor is not None or self.store() is None:
+            return
+        keys = [self._key(r) for r in range(1, self.world)]
+
+        def run():
+            st = self.store()
+            while not self._monitor_stop.is_set() and dist.is_initialized():
+                try:
+                    for k in keys:
+                        if st.check([k]):
+                            v = st.get(k).decode()
+                            if v and self._failure is None:
+                                self._failure = f"TP rank {k.rsplit('/', 1)[1]} failed: {v}"
+                except Exception:  # noqa: BLE001 -- store gone (shutdown)
+                    return
+                self._monitor_stop.wait(period_s)
+
+        self._monitor = threading.Thread(target=run, name="tp-health-monitor", daemon=True)
+        self._monitor.start()
+
+    def peer_failure(self) -> Optional[str]:
+        return self._failure
+
+    def stop_monitor(self) -> None:
+        """Before the process group goes away (the monitor thread uses its store)."""
+        self._monitor_stop.set()
+        if self._monitor is not None:
+            self._monitor.join(timeout=5)
+            self._monitor = None
 
     def barrier(self, timeout_s: float) -> None:
         """Bounded barrier of the replica (gloo monitored barrier: raises if a rank does not arrive)."""
@@ -231,7 +298,7 @@ def make_control_channel(tp: TPGroup) -> Optional[ControlChannel]:
         g = dist.new_group(ranks=ranks, backend="gloo", timeout=datetime.timedelta(days=7))
         if r == tp.replica:
             mine = g
-    return ControlChannel(tp.rank, mine, src=tp.leader)
+    return ControlChannel(tp.rank, mine, src=tp.leader, replica=tp.replica, world=tp.world)
 
 
 def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backend: Optional[str] = None,

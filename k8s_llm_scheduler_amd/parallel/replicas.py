@@ -3,25 +3,29 @@
 With ``WORLD_SIZE = replicas x tp`` (``engine.tp`` / ``K8S_TP``), ranks ``[r*tp, (r+1)*tp)`` form
 replica ``r``: a complete tensor-parallel engine with its own weights, KV cache, RCCL communicator and
 xGMI peer regions (``comm.init_from_env``).  Global rank 0 runs the control plane (the reference's
-whole ``scheduler.py``) and the leader of replica 0.  The leader of every other replica receives
-batches of chat requests from rank 0 over a two-rank gloo link, runs them on its engine (its TP
-followers track its schedule through the replica's ``ControlChannel``) and sends the completion
-texts back.
+whole ``scheduler.py``) and the leader of replica 0.  The leader of every other replica serves chat
+requests from rank 0 over a :class:`ReplicaLink`; its TP followers track its schedule through the
+replica's ``ControlChannel``.
 
-:class:`ReplicaRouterBackend` is the decision backend on rank 0: a batch (``scheduler.mode:
-batched``) is dealt round-robin over the replicas, remote shares go out on one thread per link
-while the local share runs on rank 0's own engine, and the texts come back in request order.  A
-failure of any share raises, so retries / circuit breaker / fallback of the decision service see
-one failed engine call, as for a single engine.  The reference has no counterpart (one remote
-HTTPS call per pod, ``scheduler.py:425-433``).
+:class:`ReplicaRouterBackend` is the decision backend on rank 0.  Every request of a call goes to the
+replica with the fewest requests in flight (ties rotate), so single-pod calls -- every call of the
+``sequential`` and ``continuous`` scheduler modes -- spread over the replicas instead of staying on
+replica 0.  Links are multiplexed: requests carry ids, a receiver thread on each side completes them as
+they finish, and a remote leader hands every request to its engine's background serving loop, so the
+remote replica batches continuously and any number of requests can be outstanding per link.  A failure
+of any share raises, so retries / circuit breaker / fallback of the decision service see one failed
+engine call, as for a single engine.  The reference has no counterpart (one remote HTTPS call per pod,
+``scheduler.py:425-433``; pods detected one at a time, ``:662-681``).
 """
 
 from __future__ import annotations
 
 import datetime
+import itertools
 import logging
 import threading
-from typing import List, Optional, Sequence
+from concurrent.futures import Future, ThreadPoolExecutor
+from typing import Dict, List, Optional, Sequence
 
 import torch.distributed as dist
 
@@ -33,35 +37,93 @@ _STOP = "__stop__"
 
 
 class ReplicaLink:
-    """Two-rank gloo group between global rank 0 and the leader of one remote replica."""
+    """Rank 0 <-> the leader of one remote replica: two two-rank gloo groups, one per direction, each used by
+    exactly one thread per side (so the collectives stay in the same order on both ranks).  Requests and replies
+    carry ids: any number can be outstanding, replies arrive in completion order."""
 
-    def __init__(self, replica: int, leader: int, group):
+    def __init__(self, replica: int, leader: int, down, up):
         self.replica = replica
         self.leader = leader        # global rank of the remote replica's TP rank 0
-        self.group = group
-        self._lock = threading.Lock()
+        self.down = down            # rank 0 -> leader (requests, stop)
+        self.up = up                # leader -> rank 0 (replies, stop acknowledgement)
+        self._send_lock = threading.Lock()
+        self._ids = itertools.count()
+        self._pending: Dict[int, Future] = {}
+        self._plock = threading.Lock()
+        self._rx: Optional[threading.Thread] = None
+        self.inflight = 0           # requests sent and not answered yet (router load)
 
-    def _bcast(self, obj, src: int):
+    @staticmethod
+    def _bcast(obj, src: int, group):
         box = [obj]
-        dist.broadcast_object_list(box, src=src, group=self.group)
+        dist.broadcast_object_list(box, src=src, group=group)
         return box[0]
 
-    # rank-0 side
+    # ---- rank-0 side
+    def _start_rx(self) -> None:
+        if self._rx is not None:
+            return
+
+        def run():
+            while True:
+                msg = self._bcast(None, self.leader, self.up)
+                if msg == _STOP:
+                    break
+                with self._plock:
+                    fut = self._pending.pop(msg["id"], None)
+                if fut is None:
+                    continue
+                if "error" in msg:
+                    fut.set_exception(RuntimeError(f"replica {self.replica}: {msg['error']}"))
+                else:
+                    fut.set_result(list(msg["texts"]))
+            with self._plock:   # the link is closed: nothing more will be answered
+                left, self._pending = self._pending, {}
+            for fut in left.values():
+                fut.set_exception(RuntimeError(f"replica {self.replica} link closed"))
+
+        self._rx = threading.Thread(target=run, name=f"replica{self.replica}-rx", daemon=True)
+        self._rx.start()
+
+    def submit(self, requests) -> Future:
+        """Send a share of chat requests; the future resolves to their texts (request order)."""
+        self._start_rx()
+        fut: Future = Future()
+        rid = next(self._ids)
+        n = len(requests)
+        with self._plock:
+            self._pending[rid] = fut
+            self.inflight += n
+
+        def done(_f, n=n):
+            with self._plock:
+                self.inflight -= n
+
+        fut.add_done_callback(done)
+        with self._send_lock:
+            self._bcast({"id": rid, "requests": list(requests)}, 0, self.down)
+        return fut
+
     def request(self, payload):
-        with self._lock:   # one outstanding batch per link: request/reply stay paired
-            self._bcast(payload, 0)
-            return self._bcast(None, self.leader)
+        """Blocking form (one share, returns the leader's reply dict)."""
+        try:
+            return {"texts": self.submit(payload["requests"]).result()}
+        except RuntimeError as e:
+            return {"error": str(e)}
 
     def stop(self) -> None:
-        with self._lock:
-            self._bcast(_STOP, 0)
+        self._start_rx()
+        with self._send_lock:
+            self._bcast(_STOP, 0, self.down)
+        self._rx.join(timeout=120)
 
-    # leader side
+    # ---- leader side
     def receive(self):
-        return self._bcast(None, 0)
+        return self._bcast(None, 0, self.down)
 
     def reply(self, payload) -> None:
-        self._bcast(payload, self.leader)
+        with self._send_lock:
+            self._bcast(payload, self.leader, self.up)
 
 
 def make_replica_links(tp: TPGroup) -> List[ReplicaLink]:
@@ -73,57 +135,80 @@ def make_replica_links(tp: TPGroup) -> List[ReplicaLink]:
     me = tp.global_rank
     for r in range(1, tp.replicas):
         leader = r * tp.world
-        g = dist.new_group(ranks=[0, leader], backend="gloo", timeout=datetime.timedelta(days=7))
+        down = dist.new_group(ranks=[0, leader], backend="gloo", timeout=datetime.timedelta(days=7))
+        up = dist.new_group(ranks=[0, leader], backend="gloo", timeout=datetime.timedelta(days=7))
         if me in (0, leader):
-            links.append(ReplicaLink(r, leader, g))
+            links.append(ReplicaLink(r, leader, down, up))
     return links
 
 
 class ReplicaRouterBackend:
-    """Decision backend of rank 0 that spreads every batch over all engine replicas."""
+    """Decision backend of rank 0 that sends every request to the least-loaded engine replica."""
 
     def __init__(self, local, links: Sequence[ReplicaLink]):
         self.local = local
         self.links = list(links)
         self.name = f"{getattr(local, 'name', 'local')}x{len(self.links) + 1}"
         self.dispatched = [0] * (len(self.links) + 1)
+        self._local_inflight = 0
+        self._lock = threading.Lock()
+        self._cursor = 0
 
     @property
     def replicas(self) -> int:
         return len(self.links) + 1
 
+    @property
+    def engine(self):
+        """The local engine (start_backend_loop puts it in background mode for concurrent callers)."""
+        return getattr(self.local, "engine", None)
+
+    def _loads(self) -> List[int]:
+        return [self._local_inflight] + [link.inflight for link in self.links]
+
+    def assign(self, n: int) -> List[int]:
+        """Replica of each of ``n`` requests: least in flight first, ties rotate (so serial single-request calls
+        alternate over the replicas)."""
+        with self._lock:
+            loads = self._loads()
+            out = []
+            for _ in range(n):
+                k = self.replicas
+                best = min(range(k), key=lambda i: (loads[i], (i - self._cursor) % k))
+                out.append(best)
+                loads[best] += 1
+                self._cursor = (best + 1) % k
+            for i in out:
+                self.dispatched[i] += 1
+            self._local_inflight += out.count(0)
+            return out
+
     def complete(self, requests) -> List[str]:
-        n = self.replicas
-        shares = [list(requests[i::n]) for i in range(n)]
-        results: List[Optional[List[str]]] = [None] * n
-        errors: List[Optional[BaseException]] = [None] * n
-
-        def remote(i: int) -> None:
-            try:
-                resp = self.links[i - 1].request({"requests": shares[i]})
-                if "error" in resp:
-                    raise RuntimeError(f"replica {i}: {resp['error']}")
-                results[i] = list(resp["texts"])
-            except BaseException as e:  # noqa: BLE001 -- re-raised on the calling thread
-                errors[i] = e
-
-        threads = [threading.Thread(target=remote, args=(i,), daemon=True) for i in range(1, n) if shares[i]]
-        for t in threads:
-            t.start()
-        try:
-            results[0] = self.local.complete(shares[0]) if shares[0] else []
-        except BaseException as e:  # noqa: BLE001
-            errors[0] = e
-        for t in threads:
-            t.join()
-        for i in range(n):
-            self.dispatched[i] += len(shares[i])
-            if shares[i] and errors[i] is not None:
-                raise errors[i]
+        where = self.assign(len(requests))
+        shares: List[List[int]] = [[] for _ in range(self.replicas)]
+        for j, i in enumerate(where):
+            shares[i].append(j)
+        futs = {i: self.links[i - 1].submit([requests[j] for j in shares[i]])
+                for i in range(1, self.replicas) if shares[i]}
         out: List[str] = [""] * len(requests)
-        for i in range(n):
-            for j, text in enumerate(results[i] or []):
-                out[i + j * n] = text
+        err: Optional[BaseException] = None
+        try:
+            if shares[0]:
+                for j, text in zip(shares[0], self.local.complete([requests[j] for j in shares[0]])):
+                    out[j] = text
+        except BaseException as e:  # noqa: BLE001 -- the remote shares are still collected, then re-raised
+            err = e
+        finally:
+            with self._lock:
+                self._local_inflight -= len(shares[0])
+        for i, fut in futs.items():
+            try:
+                for j, text in zip(shares[i], fut.result()):
+                    out[j] = text
+            except BaseException as e:  # noqa: BLE001
+                err = err or e
+        if err is not None:
+            raise err
         return out
 
     def shutdown(self) -> None:
@@ -134,19 +219,30 @@ class ReplicaRouterBackend:
                 log.warning(f" replica {link.replica} did not acknowledge shutdown: {e}")
 
 
-def serve_replica(backend, link: ReplicaLink, engine=None) -> None:
-    """Leader of a remote replica: answer rank 0's batches until it sends stop, then release the
-    replica's TP followers (``engine.shutdown_workers``)."""
+def serve_replica(backend, link: ReplicaLink, engine=None, workers: int = 64) -> None:
+    """Leader of a remote replica: hand every request share from rank 0 to the engine's background serving loop
+    (so shares from concurrent rank-0 callers batch together), reply as each completes, until rank 0 sends stop;
+    then release the replica's TP followers (``engine.shutdown_workers``)."""
+    if engine is not None and hasattr(engine, "start_background"):
+        engine.start_background()
+    pool = ThreadPoolExecutor(max_workers=workers, thread_name_prefix=f"replica{link.replica}")
+
+    def handle(msg):
+        try:
+            link.reply({"id": msg["id"], "texts": backend.complete(msg["requests"])})
+        except Exception as e:  # noqa: BLE001 -- reported to rank 0, which decides (retry/fallback)
+            link.reply({"id": msg["id"], "error": f"{type(e).__name__}: {e}"})
+
     try:
         while True:
             msg = link.receive()
             if msg == _STOP:
-                return
-            try:
-                texts = backend.complete(msg["requests"])
-                link.reply({"texts": texts})
-            except Exception as e:  # noqa: BLE001 -- reported to rank 0, which decides (retry/fallback)
-                link.reply({"error": f"{type(e).__name__}: {e}"})
+                break
+            pool.submit(handle, msg)
+        pool.shutdown(wait=True)
+        link.reply(_STOP)
     finally:
         if engine is not None:
+            if hasattr(engine, "stop_background"):
+                engine.stop_background()
             engine.shutdown_workers()

@@ -45,3 +45,21 @@ def test_bench_arrival_mode():
 def test_bench_refuses_prompt_longer_than_max_model_len():
     p = _run("--preset", "tiny", "--nodes", "64", "--max-model-len", "2048", "--steps", "1", "--warmup", "0")
     assert p.returncode != 0 and "max-model-len" in (p.stderr + p.stdout)
+
+
+def test_bench_arrival_mode_with_replicas():
+    """--arrival-rate with --tp < world: 4 ranks as 2 replicas x TP=2 on gloo; rank 0 routes every
+    single-pod decision to the least-loaded replica, so both replicas serve pods."""
+    from mp_harness import free_port
+
+    env = dict(os.environ, PYTHONPATH=ROOT, K8S_TP_BACKEND="gloo", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "4", "--tp", "2",
+           "--preset", "tiny", "--arrival-rate", "20", "--steps", "12", "--warmup", "1", "--batch", "4",
+           "--gen-tokens", "8"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["bound"] == 12 and d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp2-tp2"
+    disp = d["config"]["replica_dispatch"]
+    assert sum(disp) == 13 and min(disp) >= 3, disp

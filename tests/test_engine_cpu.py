@@ -309,3 +309,56 @@ def test_spec_verify_graph_capture_gated_on_gather_size(tp, slot_kib, expect_spe
     assert LLMEngine._prefill_bucket_capturable(fake, 16) is True        # one logits row: 257 KB at TP=2
     got = LLMEngine._prefill_bucket_capturable(fake, SPEC_GRAPH_T, logits_rows=SPEC_GRAPH_T)
     assert got is expect_spec
+
+
+@pytest.mark.parametrize("k", [1, 5, 9])
+def test_forced_json_close_runs_exactly_k_decode_steps(k):
+    """Device-side stop detection (sampler StopArgs): an answer whose JSON object closes at token k (token 0
+    comes from the prefill) costs exactly k decode steps, whatever decode_chunk is; without it the chunk
+    runs to its end."""
+    eng = build_engine("tiny", device="cpu", max_batch=2, max_model_len=256, num_blocks=64, seed=1, decode_chunk=4)
+    (lb,), (fill,), (rb,) = eng.tok.encode("{"), eng.tok.encode("a"), eng.tok.encode("}")
+    ids = [lb] + [fill] * (k - 1) + [rb]      # the closing brace is answer token k
+    p = SamplingParams(max_tokens=64, temperature=0.0, forced_output_ids=ids)
+    o = eng.generate(["pick a node"], p)[0]
+    assert o.finish_reason == "json" and o.token_ids == ids
+    assert eng.stats["decode_steps"] == k
+    eng.device_stop = False
+    eng.stats["decode_steps"] = 0
+    o = eng.generate(["pick a node"], p)[0]
+    assert o.token_ids == ids and eng.stats["decode_steps"] == 4 * math.ceil(k / 4)
+
+
+def test_device_stop_on_eos_and_max_tokens():
+    eng = build_engine("tiny", device="cpu", max_batch=2, max_model_len=256, num_blocks=64, seed=1, decode_chunk=4)
+    o = eng.generate(["a"], SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))[0]
+    assert len(o.token_ids) == 6 and o.finish_reason == "length" and eng.stats["decode_steps"] == 5
+    eos = eng.tok.eot_id
+    eng.stats["decode_steps"] = 0
+    o = eng.generate(["a"], SamplingParams(max_tokens=30, temperature=0.0, forced_output_ids=[11, 12, eos, 13]))[0]
+    assert o.token_ids == [11, 12] and o.finish_reason == "stop" and eng.stats["decode_steps"] == 2
+
+
+def test_mixed_prefill_decode_steps_match_split_path():
+    """A request arriving while others decode is prefilled in one varlen forward together with the decode rows
+    (mixed step); tokens equal the split path (prefill, then decode)."""
+    prompts = [[5, 6, 7, 8 + i] * (3 + 2 * i) for i in range(3)]
+    params = [SamplingParams(max_tokens=20, temperature=0.6, seed=3 + i, ignore_eos=True) for i in range(3)]
+
+    def run(mixed):
+        eng = build_engine("tiny", device="cpu", max_batch=4, max_model_len=256, num_blocks=128, seed=1)
+        eng.mixed_steps = mixed
+        reqs = [eng.add_request(prompts[0], params[0])]
+        eng.step()                      # request 0: prefill + decode
+        eng.step()
+        reqs.append(eng.add_request(prompts[1], params[1]))
+        eng.step()                      # request 1 prefills while 0 decodes
+        reqs.append(eng.add_request(prompts[2], params[2]))
+        while eng.has_work():
+            eng.step()
+        return [r.output_ids for r in reqs], eng.stats["mixed_steps"]
+
+    mixed, n_mixed = run(True)
+    split, n_split = run(False)
+    assert n_mixed >= 2 and n_split == 0
+    assert mixed == split and all(len(t) == 20 for t in mixed)

@@ -1,0 +1,100 @@
+"""Bounded engine waits and recovery with a stalled tensor-parallel peer, on the GPU.
+
+Two ranks share the test GPU (gloo process group + xGMI peer-memory collectives with a 600 s poll timeout, so the
+kernels themselves never give up).  Rank 1 follows rank 0's schedule and stalls for 6 s before the device work of
+its second step.  Rank 0, in sequential mode with ``llm.timeout`` = 2 s:
+
+* the stalled decision falls back within ~2-3 s (the engine's bounded device wait raises EngineStalled; the
+  retries fail fast while the device has not drained) and ``/readyz`` turns 503;
+* once rank 1 resumes, its collectives complete rank 0's parked ones; the next decision drains, resets every
+  rank's collectives (control-channel reset command, xGMI protocol state zeroed, bounded barrier) and goes
+  through the engine again; ``/readyz`` is 200.
+"""
+
+import json
+import time
+import urllib.error
+import urllib.request
+
+import pytest
+import torch
+
+from mp_harness import free_port, run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+def _probe(port: int):
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/readyz", timeout=5) as r:
+            return r.status, json.loads(r.read())
+    except urllib.error.HTTPError as e:
+        return e.code, json.loads(e.read())
+
+
+def _rank(rank, world):
+    import os
+
+    import torch.distributed as dist
+
+    from k8s_llm_scheduler_amd.control import DecisionService, LocalEngineBackend
+    from k8s_llm_scheduler_amd.control.breaker import CircuitBreaker
+    from k8s_llm_scheduler_amd.control.metrics import SchedulerMetrics
+    from k8s_llm_scheduler_amd.control.prompt import PromptEngine
+    from k8s_llm_scheduler_amd.engine import build_engine
+    from k8s_llm_scheduler_amd.engine.synthetic import reference_cluster
+    from k8s_llm_scheduler_amd.parallel import init_from_env, make_control_channel
+
+    tp = init_from_env("cuda", backend="gloo", comm="xgmi")
+    assert tp.xgmi is not None
+    control = make_control_channel(tp)
+    eng = build_engine("tiny", tp=tp, device="cuda", max_batch=2, max_model_len=512, num_blocks=128, seed=1,
+                       control=control, watchdog_s=2.0)
+    out = {}
+    if rank == 1:
+        eng.fault = ("stall", 2, 6.0)   # the second schedule message: sleep 6 s before the device work
+        eng.serve_worker()
+        out = dict(health=dict(eng.health))
+    else:
+        port = int(os.environ["K8S_TEST_PROBE_PORT"])
+        metrics = SchedulerMetrics(True, port)
+        metrics.add_health_source("engine", eng.health_probe)
+        metrics.start()
+        svc = DecisionService(LocalEngineBackend(eng, ignore_eos=True), max_retries=3, max_tokens=8, timeout=2.0,
+                              breaker=CircuitBreaker(50, 60), sleep=lambda s: None)
+        nodes, pods = reference_cluster()
+        build = lambda i: PromptEngine().build(pods[i], nodes)   # noqa: E731
+        d1 = svc.decide(build(0), pods[0], nodes)
+        r1 = _probe(port)
+        t0 = time.monotonic()
+        d2 = svc.decide(build(1), pods[1], nodes)                # rank 1 stalls under this one
+        t_d2 = time.monotonic() - t0
+        r2 = _probe(port)
+        end = time.monotonic() + 30
+        while not eng._drained(0.0) and time.monotonic() < end:  # rank 1 resumes after ~6 s
+            time.sleep(0.1)
+        d3 = svc.decide(build(2), pods[2], nodes)
+        r3 = _probe(port)
+        out = dict(d1=(d1.fallback_needed, d1.reasoning), ready1=r1[0], d2=(d2.fallback_needed, d2.reasoning),
+                   t_d2=t_d2, ready2=r2[0], body2=r2[1], d3=(d3.fallback_needed, d3.reasoning), ready3=r3[0],
+                   health=dict(eng.health), stalls=eng.stats["stalls"])
+        eng.shutdown_workers()
+        metrics.stop()
+    dist.barrier()
+    dist.destroy_process_group()
+    return out
+
+
+def test_stalled_peer_falls_back_fast_then_recovers():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    port = free_port()
+    res = run_ranks(_rank, 2, env={"K8S_XGMI_TIMEOUT_S": "600", "K8S_TP_COMM": "xgmi",
+                                   "K8S_TEST_PROBE_PORT": str(port)}, timeout_s=300)
+    r0 = res[0]
+    engine_answer = lambda d: (not d[0]) or "JSON" in d[1]   # noqa: E731 -- random weights: the JSON parse fails
+    assert engine_answer(r0["d1"]) and r0["ready1"] == 200, r0
+    assert r0["d2"][0] and r0["t_d2"] < 3.5 and r0["stalls"] >= 1, r0     # fell back within ~llm.timeout
+    assert r0["ready2"] == 503, r0
+    assert engine_answer(r0["d3"]) and r0["ready3"] == 200, r0             # through the engine again
+    assert r0["health"]["recoveries"] == 1 and res[1]["health"]["recoveries"] == 1, res

@@ -50,10 +50,24 @@ def _worker(rank, world, tp_size, port, q):
         if tp.global_rank == 0:
             router = ReplicaRouterBackend(local, links)
             texts = router.complete(_requests())
-            again = router.complete(_requests()[:1])      # a lone request stays on replica 0
+            again = router.complete(_requests()[:1])      # a lone request: the next replica in rotation
+            batch_dispatch = list(router.dispatched)
+            # continuous serving: the local engine runs its background loop, 20 single-pod calls from 8
+            # threads -- every call goes to the least-loaded replica
+            from concurrent.futures import ThreadPoolExecutor
+
+            from k8s_llm_scheduler_amd.control.scheduler import start_backend_loop
+
+            assert start_backend_loop(router)
+            reqs = _requests()
+            with ThreadPoolExecutor(8) as ex:
+                conc = list(ex.map(lambda i: router.complete([reqs[i % len(reqs)]])[0], range(20)))
+            conc_dispatch = [b - a for a, b in zip(batch_dispatch, router.dispatched)]
+            eng.stop_background()
             router.shutdown()
             eng.shutdown_workers()
-            q.put(("router", texts, again, list(router.dispatched), (tp.replica, tp.replicas, tp.world)))
+            q.put(("router", texts, again, batch_dispatch, (tp.replica, tp.replicas, tp.world), conc,
+                   conc_dispatch))
         elif tp.rank == 0:
             serve_replica(local, links[0], eng)
             q.put(("leader", tp.replica, tp.global_rank))
@@ -88,11 +102,13 @@ def test_two_replicas_of_tp2_match_single_engine():
     assert not errors, errors[0][2]
     assert all(p.exitcode == 0 for p in procs)
     router = next(g for g in got if g[0] == "router")
-    _, texts, again, dispatched, layout = router
+    _, texts, again, dispatched, layout, conc, conc_dispatch = router
     assert layout == (0, 2, 2)
     assert texts == want
     assert again == want[:1]
-    assert dispatched == [3 + 1, 2]          # round-robin deal: requests 0,2,4 local, 1,3 remote
+    assert dispatched == [3, 2 + 1]          # least loaded, ties rotate: 0,1,0,1,0 then the lone one on 1
+    assert conc == [want[i % len(want)] for i in range(20)]
+    assert min(conc_dispatch) >= 8 and sum(conc_dispatch) == 20, conc_dispatch
     assert sorted(g[0] for g in got) == ["follower", "follower", "leader", "router"]
 
 

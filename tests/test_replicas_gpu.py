@@ -42,6 +42,18 @@ def _rank(rank, world):
     if tp.global_rank == 0:
         router = ReplicaRouterBackend(local, links)
         out.update(role="router", texts=router.complete(_requests(dup=2)), dispatched=list(router.dispatched))
+        # continuous serving: local engine in its background loop, 10 single-pod calls from 5 threads
+        from concurrent.futures import ThreadPoolExecutor
+
+        from k8s_llm_scheduler_amd.control.scheduler import start_backend_loop
+
+        assert start_backend_loop(router)
+        reqs = _requests()
+        before = list(router.dispatched)
+        with ThreadPoolExecutor(5) as ex:
+            conc = list(ex.map(lambda i: router.complete([reqs[i % 5]])[0], range(10)))
+        out.update(conc=conc, conc_dispatch=[b - a for a, b in zip(before, router.dispatched)])
+        eng.stop_background()
         router.shutdown()
         eng.shutdown_workers()
     elif tp.rank == 0:
@@ -70,10 +82,13 @@ def test_two_replicas_of_tp2_share_one_gpu():
     assert all(r["xgmi_err"] == 0 for r in res.values())
     assert all(r["graph_replays"] > 0 for r in res.values()), res   # every rank decoded through its graphs
     router = res[0]
-    assert router["dispatched"] == [5, 5]            # round-robin deal: even positions local, odd remote
+    assert router["dispatched"] == [5, 5]            # least loaded, ties rotate: even positions local, odd remote
+    assert min(router["conc_dispatch"]) >= 3, router["conc_dispatch"]   # continuous mode: both replicas serve
     texts = router["texts"]
     rep0, rep1 = texts[0::2], texts[1::2]            # the same five prompts on each replica, as the same batch
     assert rep0 == rep1
     assert sum(a == b for a, b in zip(rep0, want)) >= 4, (rep0, want)
+    conc = router["conc"]
+    assert sum(conc[i] in (rep0[i % 5], rep1[i % 5]) for i in range(10)) >= 8, (conc, rep0)
     print(f"2 replicas x TP=2 on one GPU: replica texts identical, {sum(a == b for a, b in zip(rep0, want))}/5 "
           f"equal to TP=1")
