@@ -289,6 +289,23 @@ class LLMEngine:
             spins += 1
             time.sleep(0 if spins < 200 else 2e-5)
 
+    def _poll_event(self, ev=None) -> bool:
+        """Wait (bounded by the call deadline / watchdog) for ``ev`` or, without one, for the work enqueued so far;
+        False at the deadline (nothing raised: the caller keeps the TP ranks' schedules matched)."""
+        if not self.gpu:
+            return True
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        limit = self._wait_limit()
+        spins = 0
+        while not ev.query():
+            if limit is not None and time.monotonic() > limit:
+                return False
+            spins += 1
+            time.sleep(0 if spins < 200 else 2e-5)
+        return True
+
     def _fetch(self, *ts: torch.Tensor, what: str = "step") -> List[torch.Tensor]:
         """Small device tensors -> host, through reused pinned buffers and one bounded wait.  The returned
         tensors are overwritten by the next fetch: read them right away."""
@@ -701,6 +718,12 @@ class LLMEngine:
         if f is not None and f[0] == "stall" and self._steps == f[1]:
             self.fault = None
             time.sleep(f[2])   # fault injection (tests): this follower stalls before its device work
+        elif f is not None and f[0] == "stall_on_key":
+            st = self.control.store()
+            if st is not None and st.check([f[1]]):   # (tests) stall at the first step after the leader sets the key
+                self.fault = None
+                st.delete_key(f[1])
+                time.sleep(f[2])
         return True
 
     def shutdown_workers(self) -> None:
@@ -954,8 +977,18 @@ class LLMEngine:
         # request instead of running its remaining replays.  The flags are read after a wait for the replay that
         # wrote them, so every TP rank takes the same decision; a new arrival ends the chunk too on a single-rank
         # engine (a TP engine's followers cannot see rank 0's arrivals mid-chunk).
+        #
+        # Every rank of a TP replica must run the same replays.  Single rank: wait for replay i, then decide
+        # (exact: the chunk ends right after the replay that finished an answer).  TP: the leader decides and
+        # broadcasts the decision (ControlChannel.decide, one int on the gloo group); it decides on replay i - 1
+        # while replay i runs, so no rank's GPU idles (at most one extra replay, which finished slots skip).
+        # A leader wait that hits its deadline decides "run the chunk out" -- the ranks stay matched and the
+        # fetch below raises EngineStalled.
         early = self.device_stop and max_steps is None and steps > 1
+        tp_ctl = self.control if self.control is not None and self.control.world > 1 else None
+        lag = 1 if tp_ctl is not None else 0
         live = list(self.running)
+        events: List = []
         ran = 0
         for i in range(steps):
             if graph is not None:
@@ -964,11 +997,25 @@ class LLMEngine:
             else:
                 self._decode_step(B, mc, nuc)
             ran += 1
-            if early and i + 1 < steps:
-                self._wait_device("decode")
-                if self._done_host[live].any() or (self.control is None and self._inbox):
-                    self.stats["early_chunk_stops"] += 1
-                    break
+            if early and self.gpu and lag:
+                ev = torch.cuda.Event()
+                ev.record()
+                events.append(ev)
+            if not early or i + 1 >= steps or i < lag:
+                continue
+            stop = 0
+            if tp_ctl is None or tp_ctl.rank == 0:
+                if self._poll_event(events[i - lag] if lag and self.gpu else None):
+                    stop = int(bool(self._done_host[live].any()) or (tp_ctl is None and bool(self._inbox)))
+                else:
+                    stop = 2          # deadline: run the chunk out, the fetch raises
+            if tp_ctl is not None:
+                stop = tp_ctl.decide(stop)
+            if stop == 1:
+                self.stats["early_chunk_stops"] += 1
+                break
+            if stop == 2:
+                early = False
         self.stats["decode_steps"] += ran
         tp = self.model.tp
         tp.snapshot_health()             # rides on the bounded wait below
@@ -1150,8 +1197,9 @@ class LLMEngine:
             self.requests.pop(r.rid, None)
             r.done.set()
         if r.slot >= 0:
-            self.s_ctx[r.slot] = 0
-            self.s_steps[r.slot] = 0
+            # fill kernels, never a host->device copy: this also runs on error paths while the stream is stalled
+            self.s_ctx[r.slot:r.slot + 1].fill_(0)
+            self.s_steps[r.slot:r.slot + 1].fill_(0)
             self.running.pop(r.slot, None)
             if r in self.prefilling:
                 self.prefilling.remove(r)
@@ -1247,7 +1295,7 @@ class LLMEngine:
 
     def _bg_loop(self) -> None:
         if self.gpu:
-            torch.cuda.set_device(self.device)
+            torch.cuda.set_device(self.s_tokens.device)   # (the tensors carry the index; "cuda" alone does not)
         while True:
             with self._wake:
                 while not self._bg_stop and not self._inbox and not self.has_work():

@@ -440,28 +440,6 @@ def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
     return mgemm_heuristic(M, N, K, epi, fp8)
 
 
-# routing credit for a fused mgemm (RMS prologue / residual epilogue) against library GEMM + the separate
-# kernel it absorbs.  0 by default: with 5 us the TP=1 B=64 decode moved QKV off the library and got slower
-# (30.6 -> 31.7 ms/step, profiles/bench_r2c_tp1_b64_credit5.json) -- the table's plain-GEMM times already
-# rank these shapes well
-FUSION_CREDIT_US = float(os.environ.get("K8S_FUSION_CREDIT_US", "0"))
-
-
-def mgemm_preferred(M: int, N: int, K: int, epi: int, fp8: bool, fused: bool = False) -> bool:
-    """K8S_GEMM=auto: the hand-written GEMM unless the tuned table measured the library GEMM more than 3 %
-    faster at this shape (prefill-size row counts, where mgemm's tiles are not yet at the library's
-    MFMA efficiency: profiles/mgemm_vs_hipblaslt_bf16.txt).  ``fused``: the call carries the RMS prologue or
-    the residual epilogue, which the library route pays as one more kernel (FUSION_CREDIT_US)."""
-    if GEMM_BACKEND == "mgemm":
-        return True
-    if GEMM_BACKEND == "library":
-        return False
-    pick = _mg_table_row(M, N, K, epi, fp8)
-    if pick is None or not pick[4]:
-        return M <= 128          # untuned shape: mgemm's streaming tiles are safe, its prefill tiles are not
-    return pick[3] <= 1.03 * pick[4] + (FUSION_CREDIT_US if fused else 0.0)
-
-
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
           grid: Optional[int] = None, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
           out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -595,10 +573,98 @@ def pgemm4(x: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, cfg: int = 0, 
     return out
 
 
-def _mgemm_route(M: int, w, K: int, epi: int, fused: bool = False) -> bool:
+# ----------------------------------------------------------------------------- GEMM routing (M > GEMV_MAX_M)
+# Tuned big-tile plans: engine/assets/pgemm_gfx950.json, written by tools/pgemm_tune.py, keyed "M,N,K,epi,fp8" ->
+# [kernel, cfg, splits, group_m, us, library us].  A row count between tuned buckets takes the plan of the nearest
+# bucket at or above it; past the largest tuned bucket, the largest one's (big tiles, no split-K: it only gets
+# better with more rows).
+_PG_TABLE: Optional[dict] = None
+PG_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "assets",
+                             "pgemm_gfx950.json")
+PG_MIN_M = 129      # below: mgemm's streaming tiles (batched decode, short prefill chunks)
+
+
+def _pg_load_table() -> dict:
+    global _PG_TABLE
+    if _PG_TABLE is None:
+        _PG_TABLE = {}
+        if os.environ.get("K8S_PGEMM_TABLE", "1") != "0" and os.path.isfile(PG_TABLE_PATH):
+            import json
+
+            with open(PG_TABLE_PATH) as f:
+                plans = json.load(f).get("plans", {})
+            for k, v in plans.items():
+                m, n, kk, epi, fp8 = (int(t) for t in k.split(","))
+                _PG_TABLE.setdefault((n, kk, epi, fp8), []).append((m, str(v[0]), int(v[1]), int(v[2]), int(v[3]),
+                                                                    float(v[4])))
+            for lst in _PG_TABLE.values():
+                lst.sort()
+    return _PG_TABLE
+
+
+def pgemm_heuristic(M: int, N: int, K: int, epi: int, fp8: bool, num_cus: int = 256) -> Tuple[str, int, int, int]:
+    """Big-tile plan of a shape the table has never seen: 256 x 256 tiles (pgemm.hip), split-K until the grid
+    covers the CUs."""
+    cfg = 0
+    tiles = pgemm_tiles(cfg, M, N, epi)
+    kt = K * (1 if fp8 else 2) // 128
+    s = 1
+    while tiles * s * 2 <= num_cus and kt // (s * 2) >= 8:
+        s *= 2
+    return "pgemm", cfg, s, (1 if M <= 256 else 8)
+
+
+def pgemm_plan_for(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[Tuple[str, int, int, int], Optional[float]]:
+    """((kernel, cfg, splits, group_m), tuned us or None) of the GEMM at M rows: kernel "pgemm" / "pgemm4", or "mgemm"
+    where the tuner measured mgemm's own tuned plan faster."""
+    rows = _pg_load_table().get((N, K, epi, int(fp8)))
+    if rows:
+        pick = next((r for r in rows if r[0] >= M), rows[-1])
+        kern, cfg, sp, gm = pick[1:5]
+        ok = kern == "mgemm" or (kern == "pgemm" and cfg < len(pgemm_configs())) or \
+             (kern == "pgemm4" and not fp8 and cfg < len(pgemm4_configs()) and K % 64 == 0)
+        if ok:
+            return (kern, cfg, sp, gm), (pick[5] if pick[0] >= M else None)
+    return pgemm_heuristic(M, N, K, epi, fp8), None
+
+
+def gemm_route(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[str, Optional[tuple]]:
+    """Kernel of a GEMM with M > GEMV_MAX_M rows: ("mgemm", None), ("pgemm" | "pgemm4", (cfg, splits, group_m)) or
+    ("library", None).  K8S_GEMM=auto (default): hand-written always -- mgemm for streaming row counts, the tuned
+    fastest of mgemm and the big-tile kernels from PG_MIN_M rows on; =library: hipBLASLt / _scaled_mm (the A/B oracle);
+    =mgemm / =pgemm force one hand-written kernel family."""
+    if GEMM_BACKEND == "library":
+        return "library", None
+    mg_ok, pg_ok = _mgemm_ok(N, K, fp8), pgemm_ok(N, K, fp8)
+    if GEMM_BACKEND == "mgemm" or (mg_ok and not pg_ok):
+        return ("mgemm", None) if mg_ok else ("library", None)
+    if not pg_ok:
+        return "library", None
+    plan, pg_us = pgemm_plan_for(M, N, K, epi, fp8)
+    if GEMM_BACKEND == "pgemm":
+        if plan[0] == "mgemm":
+            plan = pgemm_heuristic(M, N, K, epi, fp8)
+        return plan[0], plan[1:]
+    if M < PG_MIN_M or plan[0] == "mgemm":   # (the tuner records "mgemm" where its tuned plan was faster)
+        return "mgemm", None
+    return plan[0], plan[1:]
+
+
+def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
+          out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Routed hand-written GEMM of M > GEMV_MAX_M rows (None: the library route)."""
+    M, K = x2.shape
+    fp8 = _is_fp8(w)
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
-    return GEMM_BACKEND != "library" and _mgemm_ok(N, K, _is_fp8(w)) and \
-        mgemm_preferred(M, N, K, epi, _is_fp8(w), fused)
+    kern, plan = gemm_route(M, N, K, epi, fp8)
+    if kern == "library" or (fp8 and rms_eps is not None):
+        return None   # (fp8: the activations are quantized after the norm, so the caller normalises first)
+    if kern == "mgemm":
+        return mgemm(x2, w, epi, res=res, rms_eps=rms_eps, out=out)
+    cfg, sp, gm = plan
+    if kern == "pgemm4":
+        return pgemm4(x2, w, epi, cfg=cfg, splits=sp, group_m=gm, res=res, rms_eps=rms_eps, out=out)
+    return pgemm(x2, w, epi, cfg=cfg, splits=sp, group_m=gm, res=res, rms_eps=rms_eps, out=out)
 
 
 def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Tensor:
@@ -606,8 +672,10 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
     load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
     copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM."""
     M, K = r.shape
-    if _gpu(r) and M > GEMV_MAX_M and not _is_fp8(w) and _mgemm_route(M, w, K, epi, fused=True):
-        return mgemm(r.contiguous(), w, epi, rms_eps=eps)
+    if _gpu(r) and M > GEMV_MAX_M and not _is_fp8(w):
+        y = _gemm(r.contiguous(), w, epi, rms_eps=eps)
+        if y is not None:
+            return y
     ones = _ones(K, r.device)
     x = rmsnorm(r, ones, eps)
     if epi == EPI_SWIGLU:
@@ -619,8 +687,10 @@ def linear_residual(x: torch.Tensor, w, res: torch.Tensor) -> torch.Tensor:
     """res + x @ w.T (bf16), written into ``res`` (the residual stream).  mgemm route: the add is the GEMM's
     epilogue; otherwise GEMM + add."""
     M, K = x.shape
-    if _gpu(x) and M > GEMV_MAX_M and _mgemm_route(M, w, K, EPI_BF16, fused=True):
-        return mgemm(x.contiguous(), w, EPI_BF16, res=res, out=res)
+    if _gpu(x) and M > GEMV_MAX_M:
+        y = _gemm(x.contiguous(), w, EPI_BF16, res=res, out=res)
+        if y is not None:
+            return y
     y = linear(x, w)
     if y.is_cuda:
         res.add_(y)
@@ -639,12 +709,10 @@ def _ones(K: int, dev) -> torch.Tensor:
     return _ONES[key]
 
 
-# GEMMs with more than GEMV_MAX_M rows: K8S_GEMM=mgemm runs the hand-written MFMA GEMM (mgemm.hip) for every
-# shape, =library hipBLASLt / rocBLAS through torch, =auto (default) mgemm unless the tuned table measured the
-# library more than 3 % faster at that shape (today: prefill-size row counts; batched decode is mgemm).
+# GEMMs with more than GEMV_MAX_M rows: see gemm_route.
 GEMM_BACKEND = os.environ.get("K8S_GEMM", "auto")
-if GEMM_BACKEND not in ("mgemm", "library", "auto"):
-    raise ValueError(f"K8S_GEMM must be mgemm, library or auto (got {GEMM_BACKEND!r})")
+if GEMM_BACKEND not in ("mgemm", "pgemm", "library", "auto"):
+    raise ValueError(f"K8S_GEMM must be auto, mgemm, pgemm or library (got {GEMM_BACKEND!r})")
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
@@ -654,11 +722,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
         return ref.linear(_ref_act_quant(x, w), w, out_dtype)
     x2 = x.reshape(-1, x.shape[-1])
     epi = EPI_F32 if out_dtype == F32 else EPI_BF16
+    y = None
     if x2.shape[0] <= GEMV_MAX_M:
         y = _gemv(x2.contiguous(), w, epi, out_dtype or BF16)
-    elif GEMM_BACKEND != "library" and _mgemm_ok(w.shape[0], x2.shape[1], _is_fp8(w)) and out_dtype in (None, BF16, F32) \
-            and mgemm_preferred(x2.shape[0], w.shape[0], x2.shape[1], epi, _is_fp8(w)):
-        y = mgemm(x2.contiguous(), w, epi)
+    elif out_dtype in (None, BF16, F32):
+        y = _gemm(x2.contiguous(), w, epi)
+    if y is not None:
+        pass
     elif _is_fp8(w):
         y = _fp8_gemm(x2, w, out_dtype)
     else:
@@ -813,11 +883,13 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     if not _gpu(x, w_gate_up):
         return ref.linear_swiglu(_ref_act_quant(x, w_gate_up), w_gate_up)
     x2 = x.reshape(-1, x.shape[-1])
+    y = None
     if x2.shape[0] <= GEMV_MAX_M:
         y = _gemv(x2.contiguous(), w_gate_up, EPI_SWIGLU, BF16)
-    elif GEMM_BACKEND != "library" and _mgemm_ok(w_gate_up.shape[0] // 2, x2.shape[1], _is_fp8(w_gate_up)) \
-            and mgemm_preferred(x2.shape[0], w_gate_up.shape[0] // 2, x2.shape[1], EPI_SWIGLU, _is_fp8(w_gate_up)):
-        y = mgemm(x2.contiguous(), w_gate_up, EPI_SWIGLU)
+    else:
+        y = _gemm(x2.contiguous(), w_gate_up, EPI_SWIGLU)
+    if y is not None:
+        pass
     elif _is_fp8(w_gate_up):
         y = silu_mul(_fp8_gemm(x2, w_gate_up))
     else:

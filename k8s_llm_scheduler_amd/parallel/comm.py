@@ -278,6 +278,17 @@ class ControlChannel:
         """Bounded barrier of the replica (gloo monitored barrier: raises if a rank does not arrive)."""
         dist.monitored_barrier(group=self.group, timeout=datetime.timedelta(seconds=timeout_s))
 
+    def decide(self, value: int) -> int:
+        """The leader's small integer decision (e.g. end a decode chunk early) to every rank of the replica: one
+        int64 broadcast on the gloo group; followers pass anything and get the leader's value."""
+        if self.world <= 1:
+            return value
+        if getattr(self, "_dbuf", None) is None:
+            self._dbuf = torch.zeros(1, dtype=torch.int64)
+        self._dbuf[0] = value
+        dist.broadcast(self._dbuf, src=self.src, group=self.group)
+        return int(self._dbuf[0])
+
     def broadcast_object(self, obj):
         box = [obj]
         dist.broadcast_object_list(box, src=self.src, group=self.group)

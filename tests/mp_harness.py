@@ -6,6 +6,7 @@ result or traceback.  Ranks may share one GPU (LOCAL_RANK % device_count) -- the
 import os
 import queue
 import socket
+import sys
 import traceback
 
 import torch.multiprocessing as mp
@@ -19,7 +20,11 @@ def free_port() -> int:
     return p
 
 
-def _entry(fn, rank, world, port, env, q):
+def _entry(fn, rank, world, port, env, q, dump_after=None):
+    if dump_after:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(dump_after, exit=False)   # a hung rank shows where it waits
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                           LOCAL_RANK=str(rank), HSA_ENABLE_IPC_MODE_LEGACY="0", **env)
@@ -33,15 +38,20 @@ def run_ranks(fn, world: int, env=None, timeout_s: float = 600.0) -> dict:
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, dict(env or {}), q)) for r in range(world)]
+    dump = max(10.0, timeout_s - 30)
+    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, dict(env or {}), q, dump)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
     import time
 
-    t0 = time.monotonic()
+    t0 = tick = time.monotonic()
     try:
         while len(got) < world and time.monotonic() - t0 < timeout_s:
+            if time.monotonic() - tick > 30:   # progress on the real stderr (not captured): long GPU runs stay visible
+                tick = time.monotonic()
+                print(f"[mp_harness] {fn.__name__}: {len(got)}/{world} ranks done after {tick - t0:.0f}s",
+                      file=sys.__stderr__, flush=True)
             try:
                 r, status, payload = q.get(timeout=5)
                 got[r] = (status, payload)

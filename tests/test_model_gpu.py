@@ -101,6 +101,32 @@ def test_batched_decode_matches_cpu_reference(models, gemm, monkeypatch):
     torch.testing.assert_close(outs["cuda"].cpu(), outs["cpu"], atol=6e-2, rtol=5e-2)
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+def test_long_prefill_on_big_tile_gemms_matches_cpu_reference(fp8):
+    """A 600-token prefill: every projection has M = 600 >= PG_MIN_M rows, so gemm_route puts them on the big-tile
+    kernels (pgemm / pgemm4, RMS prologue + residual epilogue fused) -- never the library -- vs the CPU model."""
+    calls = []
+    real = ops._gemm
+
+    def spy(x2, w, epi, **kw):
+        calls.append(ops.gemm_route(x2.shape[0], w.shape[0] // (2 if epi == ops.EPI_SWIGLU else 1), x2.shape[1],
+                                    epi, ops._is_fp8(w))[0])
+        return real(x2, w, epi, **kw)
+
+    g = LlamaModel(CFG, device="cuda", seed=4, max_model_len=2048, weight_dtype="fp8" if fp8 else "bf16")
+    c = LlamaModel(CFG, device="cpu", seed=4, max_model_len=2048, weight_dtype="fp8" if fp8 else "bf16")
+    ids = [(13 * p + 5) % 16000 for p in range(600)]
+    orig, ops._gemm = ops._gemm, spy
+    try:
+        lg_g, _ = _prefill(g, ids)
+    finally:
+        ops._gemm = orig
+    lg_c, _ = _prefill(c, ids)
+    assert calls and all(k in ("pgemm", "pgemm4", "mgemm") for k in calls) and \
+        sum(k.startswith("pgemm") for k in calls) >= 3 * CFG.num_layers, calls
+    torch.testing.assert_close(lg_g.cpu(), lg_c, atol=1.5e-1 if fp8 else 6e-2, rtol=5e-2)
+
+
 def test_fp8_model_gpu_matches_cpu_reference():
     """fp8 projections: GPU (fp8 GEMVs, dequantized prefill GEMMs) vs the CPU model with the
     same fp8 weights; both quantize the same bf16 init, so only rounding ties may differ."""
@@ -143,3 +169,40 @@ def test_tp8_shard_decode_with_fused_attention_oproj(monkeypatch):
     torch.cuda.synchronize()
     torch.testing.assert_close(outs[True], outs[False], atol=3e-2, rtol=3e-2)
     assert ops.attn_oproj_timeouts(torch.device("cuda")) == 0
+
+
+@pytest.mark.parametrize("k", [1, 6])
+def test_engine_gpu_forced_json_close_exact_decode_steps(k):
+    """Device-side stop detection in the decode graphs: the closing brace at answer token k costs exactly k decode
+    steps (graph replays), with decode_chunk = 4."""
+    eng = build_engine("tiny", device="cuda:0", max_batch=4, num_blocks=256, max_model_len=1024, seed=3, decode_chunk=4)
+    (lb,), (fill,), (rb,) = eng.tok.encode("{"), eng.tok.encode("a"), eng.tok.encode("}")
+    ids = [lb] + [fill] * (k - 1) + [rb]
+    o = eng.generate(["pick a node"], SamplingParams(max_tokens=64, temperature=0.0, forced_output_ids=ids))[0]
+    assert o.token_ids == ids and o.finish_reason == "json"
+    assert eng.stats["decode_steps"] == k and eng.stats["graph_replays"] == k
+
+
+def test_engine_gpu_mixed_steps_match_split_path():
+    prompts = [[5, 6, 7, 8 + i] * (3 + 2 * i) for i in range(3)]
+    params = [SamplingParams(max_tokens=20, temperature=0.6, seed=3 + i, ignore_eos=True) for i in range(3)]
+
+    def run(mixed):
+        eng = build_engine("tiny", device="cuda:0", max_batch=4, num_blocks=256, max_model_len=1024, seed=3)
+        eng.mixed_steps = mixed
+        reqs = [eng.add_request(prompts[0], params[0])]
+        eng.step()
+        eng.step()
+        reqs.append(eng.add_request(prompts[1], params[1]))
+        eng.step()
+        reqs.append(eng.add_request(prompts[2], params[2]))
+        while eng.has_work():
+            eng.step()
+        return [r.output_ids for r in reqs], eng.stats["mixed_steps"]
+
+    mixed, n_mixed = run(True)
+    split, _ = run(False)
+    assert n_mixed >= 2 and all(len(t) == 20 for t in mixed)
+    # bf16 GPU numerics: the decode rows of a mixed step run the prefill kernels; sampled tokens agree
+    same = sum(a == b for x, y in zip(mixed, split) for a, b in zip(x, y))
+    assert same >= 0.9 * 60, (mixed, split)

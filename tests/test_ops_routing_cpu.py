@@ -1,5 +1,5 @@
-"""GEMM routing without a GPU: the mgemm plan table's row buckets, the nearest-bucket lookup and its limit,
-the auto policy (library only where the table measured it faster), and the GEMV row threshold."""
+"""GEMM routing without a GPU: the mgemm / pgemm plan tables' row buckets and nearest-bucket lookups, the auto policy
+(hand-written kernels always; the library only as the K8S_GEMM=library oracle), and the GEMV row threshold."""
 
 import json
 
@@ -13,50 +13,77 @@ def test_row_buckets():
         [2, 2, 4, 4, 8, 8, 16, 16, 32, 1024, 2048, 2048, 8192, 8192]
 
 
-def test_table_lookup_stays_inside_the_tuned_range():
+def test_mgemm_table_lookup_stays_inside_the_tuned_range():
     table = ops._mg_load_table()
     assert table, "engine/assets/mgemm_gfx950.json is missing or empty"
-    # fp8 shapes are tuned up to 256 rows: an 8192-row prefill chunk is untuned, not a 256-row plan
     fp8_keys = [k for k in table if k[3] == 1]
     assert fp8_keys
     n, k, epi, _ = fp8_keys[0]
     top = max(r[0] for r in table[fp8_keys[0]])
     assert ops._mg_table_row(top, n, k, epi, True) is not None
     assert ops._mg_table_row(4 * top + 1, n, k, epi, True) is None
-    assert not ops.mgemm_preferred(4 * top + 1, n, k, epi, True)   # untuned prefill rows: the library
 
 
-def test_auto_policy_follows_the_table(monkeypatch):
+LLAMA_TP1 = [(10240, 8192, ops.EPI_BF16), (8192, 8192, ops.EPI_BF16), (28672, 8192, ops.EPI_SWIGLU),
+             (8192, 28672, ops.EPI_BF16)]
+
+
+@pytest.mark.parametrize("backend", ["auto", "pgemm"])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_auto_never_routes_to_the_library(monkeypatch, backend, fp8):
+    monkeypatch.setattr(ops, "GEMM_BACKEND", backend)
+    for M in (3, 8, 64, 128, 129, 245, 256, 1000, 2048, 8192, 20000):
+        for N, K, epi in LLAMA_TP1:
+            kern, plan = ops.gemm_route(M, N, K, epi, fp8)
+            assert kern in ("mgemm", "pgemm", "pgemm4"), (M, N, K, kern)
+            if fp8:
+                assert kern != "pgemm4"           # the 4-wave kernel is bf16 only
+            if backend == "auto" and M < ops.PG_MIN_M:
+                assert kern == "mgemm"
+            if kern.startswith("pgemm"):
+                cfg, sp, gm = plan
+                cfgs = ops.pgemm_configs() if kern == "pgemm" else ops.pgemm4_configs()
+                assert 0 <= cfg < len(cfgs) and sp >= 1 and gm >= 1
+
+
+def test_pgemm_table_picks_nearest_bucket_at_or_above(monkeypatch):
+    monkeypatch.setattr(ops, "_PG_TABLE", {(100, 256, 0, 0): [(256, "pgemm4", 3, 2, 4, 10.0),
+                                                               (2048, "pgemm", 0, 1, 8, 50.0)]})
+    assert ops.pgemm_plan_for(200, 100, 256, 0, False) == (("pgemm4", 3, 2, 4), 10.0)
+    assert ops.pgemm_plan_for(257, 100, 256, 0, False) == (("pgemm", 0, 1, 8), 50.0)
+    assert ops.pgemm_plan_for(9000, 100, 256, 0, False) == (("pgemm", 0, 1, 8), None)   # past the top: its plan
+    # fp8 has no 4-wave kernel: a bf16-only plan is not used for it
+    monkeypatch.setattr(ops, "_PG_TABLE", {(100, 256, 0, 1): [(256, "pgemm4", 3, 2, 4, 10.0)]})
+    assert ops.pgemm_plan_for(200, 100, 256, 0, True)[0][0] == "pgemm"
+
+
+def test_auto_follows_the_tuned_winner(monkeypatch):
     monkeypatch.setattr(ops, "GEMM_BACKEND", "auto")
-    with open(ops.MG_TABLE_PATH) as f:
-        plans = json.load(f)["plans"]
-    checked = 0
-    for key, (cfg, grid, mg_us, lib_us) in list(plans.items())[:200]:
-        mb, n, k, epi, fp8 = (int(t) for t in key.split(","))
-        row = ops._mg_table_row(mb, n, k, epi, bool(fp8))
-        if row is None or row[0] != mb:
-            continue
-        assert ops.mgemm_preferred(mb, n, k, epi, bool(fp8)) == (row[3] <= 1.03 * row[4])
-        checked += 1
-    assert checked > 50
+    monkeypatch.setattr(ops, "_PG_TABLE", {(1024, 1024, 0, 0): [(256, "mgemm", 0, 0, 0, 25.0),
+                                                                 (512, "pgemm", 0, 2, 4, 30.0)]})
+    assert ops.gemm_route(256, 1024, 1024, 0, False)[0] == "mgemm"
+    assert ops.gemm_route(300, 1024, 1024, 0, False) == ("pgemm", (0, 2, 4))
+    monkeypatch.setattr(ops, "GEMM_BACKEND", "pgemm")
+    assert ops.gemm_route(256, 1024, 1024, 0, False)[0] == "pgemm"
     monkeypatch.setattr(ops, "GEMM_BACKEND", "library")
-    assert not ops.mgemm_preferred(64, 8192, 8192, ops.EPI_BF16, False)
-    monkeypatch.setattr(ops, "GEMM_BACKEND", "mgemm")
-    assert ops.mgemm_preferred(8192, 8192, 8192, ops.EPI_BF16, False)
+    assert ops.gemm_route(256, 1024, 1024, 0, False) == ("library", None)
+
+
+def test_shipped_pgemm_table_is_consistent():
+    if not __import__("os").path.isfile(ops.PG_TABLE_PATH):
+        pytest.skip("no tuned pgemm table")
+    with open(ops.PG_TABLE_PATH) as f:
+        plans = json.load(f)["plans"]
+    assert plans
+    for key, v in plans.items():
+        m, n, k, epi, fp8 = (int(t) for t in key.split(","))
+        kern, cfg, sp, gm = v[:4]
+        assert kern in ("mgemm", "pgemm", "pgemm4") and not (fp8 and kern == "pgemm4")
+        assert ops.pgemm_plan_for(m, n, k, epi, bool(fp8))[0] == (kern, cfg, sp, gm)
 
 
 def test_gemv_threshold_and_kernel_limit():
     assert 1 <= ops.GEMV_MAX_M <= ops.GEMV_KERNEL_MAX_M == 8
-
-
-def test_fused_routing_credit_only_when_asked(monkeypatch):
-    monkeypatch.setattr(ops, "GEMM_BACKEND", "auto")
-    monkeypatch.setattr(ops, "_mg_table_row", lambda *a: (64, 0, 1, 50.0, 46.0))   # library 8 % faster
-    monkeypatch.setattr(ops, "FUSION_CREDIT_US", 0.0)
-    assert not ops.mgemm_preferred(64, 1, 1, 0, False, fused=True)
-    monkeypatch.setattr(ops, "FUSION_CREDIT_US", 5.0)
-    assert ops.mgemm_preferred(64, 1, 1, 0, False, fused=True)
-    assert not ops.mgemm_preferred(64, 1, 1, 0, False)
 
 
 if __name__ == "__main__":

@@ -2,7 +2,7 @@
 
 Two ranks share the test GPU (gloo process group + xGMI peer-memory collectives with a 600 s poll timeout, so the
 kernels themselves never give up).  Rank 1 follows rank 0's schedule and stalls for 6 s before the device work of
-its second step.  Rank 0, in sequential mode with ``llm.timeout`` = 2 s:
+the first step after rank 0 arms the fault (a key in the process group's store), i.e. under the second decision.  Rank 0, in sequential mode with ``llm.timeout`` = 2 s:
 
 * the stalled decision falls back within ~2-3 s (the engine's bounded device wait raises EngineStalled; the
   retries fail fast while the device has not drained) and ``/readyz`` turns 503;
@@ -52,7 +52,7 @@ def _rank(rank, world):
                        control=control, watchdog_s=2.0)
     out = {}
     if rank == 1:
-        eng.fault = ("stall", 2, 6.0)   # the second schedule message: sleep 6 s before the device work
+        eng.fault = ("stall_on_key", "k8s_fault_stall", 6.0)   # once rank 0 sets the key: sleep 6 s before the device work
         eng.serve_worker()
         out = dict(health=dict(eng.health))
     else:
@@ -66,6 +66,7 @@ def _rank(rank, world):
         build = lambda i: PromptEngine().build(pods[i], nodes)   # noqa: E731
         d1 = svc.decide(build(0), pods[0], nodes)
         r1 = _probe(port)
+        control.store().set("k8s_fault_stall", "1")
         t0 = time.monotonic()
         d2 = svc.decide(build(1), pods[1], nodes)                # rank 1 stalls under this one
         t_d2 = time.monotonic() - t0
@@ -90,7 +91,7 @@ def test_stalled_peer_falls_back_fast_then_recovers():
         pytest.skip("no GPU")
     port = free_port()
     res = run_ranks(_rank, 2, env={"K8S_XGMI_TIMEOUT_S": "600", "K8S_TP_COMM": "xgmi",
-                                   "K8S_TEST_PROBE_PORT": str(port)}, timeout_s=300)
+                                   "K8S_TEST_PROBE_PORT": str(port)}, timeout_s=150)
     r0 = res[0]
     engine_answer = lambda d: (not d[0]) or "JSON" in d[1]   # noqa: E731 -- random weights: the JSON parse fails
     assert engine_answer(r0["d1"]) and r0["ready1"] == 200, r0

@@ -77,7 +77,7 @@ def test_two_replicas_of_tp2_share_one_gpu():
     eng = build_engine("tiny", device="cuda", max_batch=8, max_model_len=512, num_blocks=128, seed=1)
     want = LocalEngineBackend(eng, ignore_eos=True).complete(_requests())
     del eng
-    res = run_ranks(_rank, 4, env={"K8S_TP_BACKEND": "gloo", "K8S_TP_COMM": "xgmi"}, timeout_s=400)
+    res = run_ranks(_rank, 4, env={"K8S_TP_BACKEND": "gloo", "K8S_TP_COMM": "xgmi"}, timeout_s=150)
     assert sorted(r["role"] for r in res.values()) == ["follower", "follower", "leader", "router"]
     assert all(r["xgmi_err"] == 0 for r in res.values())
     assert all(r["graph_replays"] > 0 for r in res.values()), res   # every rank decoded through its graphs

@@ -8,7 +8,8 @@ enough weight copies to exceed the 256 MiB Infinity Cache (prefill weights are c
 
     python tools/pgemm_tune.py --tp 1 8 --m 256 512 2048 8192 [--fp8] [--write] [--json-out f.json]
 
---write merges the winners into engine/assets/pgemm_gfx950.json (the table ops.gemm_plan reads).
+--write merges the winners into engine/assets/pgemm_gfx950.json (the table ops.gemm_route reads; a shape where
+mgemm's own tuned plan was faster is recorded as "mgemm").
 """
 
 from __future__ import annotations
@@ -106,8 +107,13 @@ def main() -> int:
                         best = (us, (kern, c, s, gm))
                 us, (kern, c, s, gm) = best
                 flop = 2.0 * M * wrows * K
-                plans[f"{M},{N},{K},{epi},{int(a.fp8)}"] = [kern, c, s, gm, round(us, 2), round(lib_us, 2)]
-                row = dict(tp=tp, proj=name, M=M, N=N, K=K, epi=epi, fp8=a.fp8, lib_us=round(lib_us, 2),
+                if mg_us < us:   # mgemm's own tuned plan wins: the router keeps this shape on mgemm
+                    plans[f"{M},{N},{K},{epi},{int(a.fp8)}"] = ["mgemm", 0, 0, 0, round(mg_us, 2), round(lib_us, 2)]
+                else:
+                    plans[f"{M},{N},{K},{epi},{int(a.fp8)}"] = [kern, c, s, gm, round(us, 2), round(lib_us, 2)]
+                hand = min(us, mg_us)
+                row = dict(tp=tp, proj=name, M=M, N=N, K=K, epi=epi, fp8=a.fp8, lib_us=round(lib_us, 2), hand_us=round(hand, 2),
+                           hand_vs_lib=round(lib_us / hand, 3),
                            mgemm_us=round(mg_us, 2), pgemm_us=round(us, 2), kernel=kern, cfg=c, splits=s, group_m=gm,
                            vs_lib=round(lib_us / us, 3), tflops=round(flop / us / 1e6, 1),
                            tbps=round(wbytes / us / 1e6, 2))
@@ -118,7 +124,9 @@ def main() -> int:
             del Ws
             torch.cuda.empty_cache()
     n_win = sum(r["vs_lib"] >= 1.0 for r in rows)
-    print(f"# pgemm >= library on {n_win}/{len(rows)} shapes; {time.time() - t0:.0f}s", flush=True)
+    n_hand = sum(r["hand_vs_lib"] >= 1.0 for r in rows)
+    print(f"# pgemm >= library on {n_win}/{len(rows)} shapes, best hand-written (pgemm/pgemm4/mgemm) on {n_hand}; "
+          f"{time.time() - t0:.0f}s", flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:
             json.dump(rows, f, indent=1)
