@@ -188,6 +188,7 @@ class LLMEngine:
         # count of schedule messages)
         self.fault: Optional[tuple] = None
         self._steps = 0
+        self._reset_seen = 0        # follower: the leader's last reset generation handled
         if control is not None and control.rank == 0:
             control.start_monitor()
         # prompt-lookup speculative decoding (_spec_decode): drafted tokens per step, 0 = off
@@ -278,16 +279,48 @@ class LLMEngine:
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self._last_event = ev
+        if not self._await(ev, what):
+            self.stats["stalls"] += 1
+            msg = f"engine stalled: {what} did not complete within the deadline (rank {self.model.tp.rank})"
+            self._fail(msg)
+            raise EngineStalled(msg)
+
+    def _await(self, ev, what: Optional[str]) -> bool:
+        """Poll ``ev``.  Leader (or single rank): False once the call deadline / watchdog passes.  TP follower: a
+        follower's host bookkeeping must track the leader's schedule step for step, so it never gives up on its
+        own -- past the watchdog it reports the stall to the leader (failure key in the store) and keeps waiting,
+        until the work completes or the leader requests a reset (then EngineStalled)."""
+        worker = self.control is not None and self.control.rank != 0
         limit = self._wait_limit()
-        spins = 0
+        spins, reported = 0, False
+        next_check = time.monotonic() + 0.2
         while not ev.query():
-            if limit is not None and time.monotonic() > limit:
-                self.stats["stalls"] += 1
-                msg = f"engine stalled: {what} did not complete within the deadline (rank {self.model.tp.rank})"
-                self._fail(msg)
-                raise EngineStalled(msg)
+            now = time.monotonic()
+            if worker:
+                if limit is not None and now > limit and not reported:
+                    reported = True
+                    self.stats["stalls"] += 1
+                    self._fail(f"engine stalled: {what or 'a step'} did not complete within the watchdog "
+                               f"(rank {self.model.tp.rank})")
+                if now > next_check:
+                    next_check = now + 0.05
+                    if self.control.reset_generation() > self._reset_seen:
+                        raise EngineStalled(f"rank 0 requested a reset while {what or 'a step'} was in flight "
+                                            f"(rank {self.model.tp.rank})")
+            elif limit is not None and now > limit:
+                return False
             spins += 1
             time.sleep(0 if spins < 200 else 2e-5)
+        return True
+
+    def _dev(self, x, dtype=torch.int32) -> torch.Tensor:
+        """Host data -> the engine's device without ever blocking the host: staged through pinned memory (the caching
+        host allocator keeps the block until its copy has run), because a copy from pageable memory waits for the
+        stream -- behind a stalled collective that is an unbounded wait."""
+        t = x if isinstance(x, torch.Tensor) else torch.tensor(x, dtype=dtype)
+        if not self.gpu:
+            return t
+        return t.pin_memory().to(self.device, non_blocking=True)
 
     def _poll_event(self, ev=None) -> bool:
         """Wait (bounded by the call deadline / watchdog) for ``ev`` or, without one, for the work enqueued so far;
@@ -297,14 +330,7 @@ class LLMEngine:
         if ev is None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
-        limit = self._wait_limit()
-        spins = 0
-        while not ev.query():
-            if limit is not None and time.monotonic() > limit:
-                return False
-            spins += 1
-            time.sleep(0 if spins < 200 else 2e-5)
-        return True
+        return self._await(ev, None)
 
     def _fetch(self, *ts: torch.Tensor, what: str = "step") -> List[torch.Tensor]:
         """Small device tensors -> host, through reused pinned buffers and one bounded wait.  The returned
@@ -387,6 +413,7 @@ class LLMEngine:
         tp = self.model.tp
         try:
             if announce and self.control is not None and self.control.rank == 0:
+                self.control.request_reset()   # releases followers parked in a device wait (_await)
                 self.control.exchange({"new": [], "abort": [], "stop": False, "reset": True})
                 self.control.clear_failures()
             err = EngineUnavailable(self.health["reason"] or "engine reset")
@@ -640,8 +667,8 @@ class LLMEngine:
             host[o + 4], host[o + 5] = n1, ctx_len
         bt = torch.zeros(1, self.max_blocks_per_seq, dtype=torch.int32)
         bt[0, :len(blocks)] = torch.tensor(blocks, dtype=torch.int32)
-        self.p_packed.copy_(host.to(self.device, non_blocking=True))
-        self.p_bt.copy_(bt.to(self.device, non_blocking=True))
+        self.p_packed.copy_(self._dev(host))
+        self.p_bt.copy_(self._dev(bt))
 
     # ------------------------------------------------------------------ requests
     def render_chat(self, system: str, user: str) -> List[int]:
@@ -701,6 +728,7 @@ class LLMEngine:
         if msg.get("stop"):
             return False
         if msg.get("reset"):
+            self._reset_seen = self.control.reset_generation()
             if not self._drained(max(5.0, self.watchdog_s)):
                 self._fail("reset: device did not drain")
                 self._unrecoverable("device did not drain for the reset")
@@ -730,6 +758,7 @@ class LLMEngine:
         if self.control is not None and self.control.rank == 0:
             self.control.stop_monitor()
             self.control.exchange({"new": [], "abort": [], "stop": True})
+            self.control.flush()
 
     def _reap_aborted(self) -> None:
         for r in sorted((r for r in self.requests.values() if r.aborted and not r.finished), key=lambda r: r.rid):
@@ -822,7 +851,7 @@ class LLMEngine:
             last.append(cu[-1] - 1)
             bt[i, :len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
         dev = self.device
-        t = lambda x: torch.tensor(x, dtype=torch.int32).to(dev, non_blocking=True)
+        t = self._dev
         t0 = time.perf_counter()
         if self.gpu:
             ev0 = torch.cuda.Event(enable_timing=True)
@@ -839,7 +868,7 @@ class LLMEngine:
             self.stats["prefill_graph_replays"] += 1
             self.stats["prefill_overlap_chunks"] += bool(self._overlap_split_at(Tb))
         elif dec:
-            d = torch.tensor(dec, dtype=torch.long, device=dev)
+            d = self._dev(dec, torch.long)
             ctx_d = self.s_ctx.index_select(0, d)
             pos_d = ctx_d - 1
             blk = self.s_bt.index_select(0, d).gather(1, (pos_d // bs).long().unsqueeze(1)).squeeze(1)
@@ -849,7 +878,7 @@ class LLMEngine:
             slot_t = torch.cat([t(slots), blk * bs + pos_d % bs])
             cu_all = cu + [cu[-1] + k + 1 for k in range(len(dec))]
             ctx_t = torch.cat([t(ctx), ctx_d])
-            bt_t = torch.cat([bt.to(dev, non_blocking=True), self.s_bt.index_select(0, d)])
+            bt_t = torch.cat([self._dev(bt), self.s_bt.index_select(0, d)])
             last_t = t(last + [n_p + k for k in range(len(dec))])
             logits = self.model.forward_prefill(ids_t, pos_t, slot_t, t(cu_all), ctx_t, bt_t,
                                                 max(e - s for _, s, e in chunk), last_t)
@@ -865,13 +894,13 @@ class LLMEngine:
             self.stats["mixed_steps"] += 1
             self.stats["mixed_decode_rows"] += len(dec)
         else:
-            bt_d = bt.to(dev, non_blocking=True)
+            bt_d = self._dev(bt)
             split = None
             T0 = self._overlap_split_at(len(ids))
             if T0:
                 halves = []
                 for c_h, x_h, seqs in split_prefill_meta(cu, ctx, T0):
-                    idx = torch.tensor(seqs, dtype=torch.long, device=dev)
+                    idx = self._dev(seqs, torch.long)
                     halves.append((t(c_h), t(x_h), bt_d.index_select(0, idx),
                                    max(b - a for a, b in zip(c_h, c_h[1:]))))
                 split = (T0, halves[0], halves[1])
@@ -884,19 +913,19 @@ class LLMEngine:
             r.computed = e
             self.allocator.commit_prefix(r.blocks, r.prompt_ids, e)
         if done:
-            idx = torch.tensor([i for i, _ in done], device=dev)
+            idx = self._dev([i for i, _ in done], torch.long)
             sub = logits.index_select(1, idx).contiguous()   # [tp, n, Vs]
             rs = [r for _, r in done]
-            temp = torch.tensor([r.params.temperature for r in rs], dtype=torch.float32, device=dev)
-            top_p = torch.tensor([r.params.top_p for r in rs], dtype=torch.float32, device=dev)
-            seeds = torch.tensor([r.seed for r in rs], dtype=torch.int32, device=dev)
-            ctr = torch.tensor([len(r.prompt_ids) for r in rs], dtype=torch.int32, device=dev)
+            temp = self._dev([r.params.temperature for r in rs], torch.float32)
+            top_p = self._dev([r.params.top_p for r in rs], torch.float32)
+            seeds = self._dev([r.seed for r in rs])
+            ctr = self._dev([len(r.prompt_ids) for r in rs])
             toks = ops.sample(sub, temp, top_p, seeds, ctr, shards=sub.shape[0], nucleus=self._wants_nucleus(rs))
-            slots_t = torch.tensor([r.slot for r in rs], dtype=torch.long, device=dev)
+            slots_t = self._dev([r.slot for r in rs], torch.long)
             forced0 = [(k, r.params.forced_output_ids[0]) for k, r in enumerate(rs) if r.params.forced_output_ids]
             if forced0:   # scripted answers replace the sampled first token too
-                fk = torch.tensor([k for k, _ in forced0], dtype=torch.long, device=dev)
-                toks = toks.index_copy(0, fk, torch.tensor([v for _, v in forced0], dtype=torch.int32, device=dev))
+                fk = self._dev([k for k, _ in forced0], torch.long)
+                toks = toks.index_copy(0, fk, self._dev([v for _, v in forced0]))
             self.s_tokens[slots_t] = toks
             self.s_ctx[slots_t] = ctr + 1
             self.s_hist[slots_t, 0] = toks
@@ -908,7 +937,7 @@ class LLMEngine:
             for r in rs:
                 row = torch.zeros(self.max_blocks_per_seq, dtype=torch.int32)
                 row[:len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
-                self.s_bt[r.slot] = row.to(dev, non_blocking=True)
+                self.s_bt[r.slot] = self._dev(row)
             now = time.perf_counter()
             for r in rs:
                 r.first_token_time = now
@@ -953,11 +982,11 @@ class LLMEngine:
             flen.append(-1 if f is None else min(len(f), self.max_new_cap))
             if f is not None and f:
                 n = min(len(f), self.max_new_cap)
-                self.s_forced[r.slot, :n] = torch.tensor(f[:n], dtype=torch.int32).to(dev, non_blocking=True)
+                self.s_forced[r.slot, :n] = self._dev(f[:n])
             self._done_host[r.slot] = 0
         self.s_json[slots_t] = -2
-        self.s_cfg[slots_t] = torch.tensor(cfg, dtype=torch.int32, device=dev)
-        self.s_forced_len[slots_t] = torch.tensor(flen, dtype=torch.int32, device=dev)
+        self.s_cfg[slots_t] = self._dev(cfg)
+        self.s_forced_len[slots_t] = self._dev(flen)
 
     def _decode(self, max_steps: Optional[int] = None) -> List[Request]:
         if not self.running:
@@ -1109,7 +1138,7 @@ class LLMEngine:
                 top_p += [r.params.top_p] * n
                 seeds += [r.seed] * n
                 ctr += range(p + 1, p + n + 1)     # the decode step's sampler counter: the context length
-            t = lambda x, dt=torch.int32: torch.tensor(x, dtype=dt).to(dev, non_blocking=True)   # noqa: E731
+            t = self._dev
             if len(rows) == 1 and self.spec_graph is not None and len(ids) <= SPEC_GRAPH_T:
                 # one sequence: replay the captured verify forward (padding rows write K/V to the scratch slot
                 # and their draws are ignored)
@@ -1123,7 +1152,7 @@ class LLMEngine:
                     ctr + [1] * pad
             else:
                 logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx),
-                                                    bt.to(dev, non_blocking=True), max(len(x[1]) for x in rows),
+                                                    self._dev(bt), max(len(x[1]) for x in rows),
                                                     t(list(range(len(ids)))))
             toks = ops.sample(logits, t(temp, torch.float32), t(top_p, torch.float32), t(seeds), t(ctr),
                               shards=logits.shape[0], nucleus=self._wants_nucleus(r for r, _, _ in rows))
@@ -1233,6 +1262,8 @@ class LLMEngine:
             self.model.tp.ensure_healthy()
         self._drain_inbox()
         sync = self._sync()
+        if worker:
+            self._step_t0 = time.monotonic()   # a follower's step starts when the leader's schedule arrives
         if sync is False:
             raise StopIteration("engine stopped by rank 0")
         if sync == "reset":

@@ -21,6 +21,7 @@ from __future__ import annotations
 import datetime
 import logging
 import os
+import pickle
 import socket
 import threading
 import time
@@ -192,10 +193,11 @@ class CollectiveError(RuntimeError):
 
 
 class ControlChannel:
-    """TP-rank-0 -> replica schedule broadcast on a CPU (gloo) group: the replica's leader (global rank 0
-    runs the serving control plane) announces new requests, aborts and reset commands, every other TP rank
-    follows its engine schedule (engine.LLMEngine._sync).  The broadcast is one-way, so a follower that
-    stalls never blocks the leader's host loop (the leader's bounded device waits catch the stall).
+    """TP-rank-0 -> replica schedule messages on a CPU (gloo) group: the replica's leader (global rank 0
+    runs the serving control plane) announces new requests, aborts, reset commands and mid-chunk decisions,
+    every other TP rank follows its engine schedule (engine.LLMEngine._sync).  The messages are one-way and
+    posted asynchronously (isend), so a follower that stalls never blocks the leader's host loop (the leader's
+    bounded device waits catch the stall).
 
     Followers report failures the other way through the process group's TCP store (``report_failure``);
     the leader polls it from a background thread (``peer_failure``), so a collective failure seen by ONE
@@ -213,10 +215,39 @@ class ControlChannel:
         self._monitor: Optional[threading.Thread] = None
         self._monitor_stop = threading.Event()
 
+    # Leader -> follower traffic is point-to-point and ASYNCHRONOUS on the leader (gloo isend; a broadcast would
+    # wait for every follower to post its receive, so one stalled follower would stall the leader's host loop).
+    # Followers receive in order (blocking: they only follow).  Tags: 1 schedule length, 2 schedule bytes,
+    # 3 decisions.
+    def _post(self, t: torch.Tensor, tag: int) -> None:
+        pend = [(w, b) for w, b in getattr(self, "_pending", []) if not w.is_completed()]
+        for dst in range(self.src + 1, self.src + self.world):
+            pend.append((dist.isend(t, dst=dst, group=self.group, tag=tag), t))
+        self._pending = pend   # keeps each sent tensor alive until its send completed
+
     def exchange(self, payload):
-        obj = [payload]
-        dist.broadcast_object_list(obj, src=self.src, group=self.group)
-        return obj[0]
+        """Leader: post ``payload`` (any picklable schedule message) to every follower and return it.  Follower:
+        the leader's next message."""
+        if self.world <= 1:
+            return payload
+        if self.rank == 0:
+            data = pickle.dumps(payload)
+            self._post(torch.tensor([len(data)], dtype=torch.int64), 1)
+            self._post(torch.frombuffer(bytearray(data), dtype=torch.uint8), 2)
+            return payload
+        hdr = torch.zeros(1, dtype=torch.int64)
+        dist.recv(hdr, src=self.src, group=self.group, tag=1)
+        buf = torch.empty(int(hdr[0]), dtype=torch.uint8)
+        dist.recv(buf, src=self.src, group=self.group, tag=2)
+        return pickle.loads(buf.numpy().tobytes())
+
+    def flush(self, timeout_s: float = 30.0) -> None:
+        """Leader: wait (bounded) for the posted messages to be delivered (before the process group goes away)."""
+        end = time.monotonic() + timeout_s
+        for w, _ in getattr(self, "_pending", []):
+            while not w.is_completed() and time.monotonic() < end:
+                time.sleep(1e-3)
+        self._pending = []
 
     # ---- failure reports (followers -> leader)
     def _key(self, rank: int) -> str:
@@ -278,16 +309,32 @@ class ControlChannel:
         """Bounded barrier of the replica (gloo monitored barrier: raises if a rank does not arrive)."""
         dist.monitored_barrier(group=self.group, timeout=datetime.timedelta(seconds=timeout_s))
 
+    def _reset_key(self) -> str:
+        return f"k8s_engine_reset/{self.replica}"
+
+    def request_reset(self) -> None:
+        """Leader: bump the replica's reset generation (followers parked in a device wait poll it)."""
+        st = self.store()
+        if st is not None:
+            st.add(self._reset_key(), 1)
+
+    def reset_generation(self) -> int:
+        st = self.store()
+        if st is None:
+            return 0
+        return int(st.add(self._reset_key(), 0))
+
     def decide(self, value: int) -> int:
         """The leader's small integer decision (e.g. end a decode chunk early) to every rank of the replica: one
-        int64 broadcast on the gloo group; followers pass anything and get the leader's value."""
+        int64 posted to each follower; followers pass anything and get the leader's value."""
         if self.world <= 1:
             return value
-        if getattr(self, "_dbuf", None) is None:
-            self._dbuf = torch.zeros(1, dtype=torch.int64)
-        self._dbuf[0] = value
-        dist.broadcast(self._dbuf, src=self.src, group=self.group)
-        return int(self._dbuf[0])
+        if self.rank == 0:
+            self._post(torch.tensor([value], dtype=torch.int64), 3)
+            return value
+        buf = torch.zeros(1, dtype=torch.int64)
+        dist.recv(buf, src=self.src, group=self.group, tag=3)
+        return int(buf[0])
 
     def broadcast_object(self, obj):
         box = [obj]
@@ -495,6 +542,21 @@ def _graph_time_us(fn, iters: int = 32, reps: int = 5) -> float:
     return best
 
 
+def comm_thresholds(table: dict, cap: int):
+    """Transport thresholds from graph-timed all-reduces, ``table`` = {bytes: {"ll"?, "oneshot"?, "twoshot", "rccl"?:
+    us}} (max over ranks): (LL up to the largest size where it is no slower than both one-shot kernels, two-shot from
+    the smallest size where it beats the flagged one-shot, xGMI up to the largest size where its best kernel beats
+    RCCL -- the whole xGMI capacity ``cap`` if it wins at the largest size measured)."""
+    ll_max = max([n for n, r in table.items() if "ll" in r and r["ll"] <= min(r.get("oneshot", 1e9), r["twoshot"])],
+                 default=0)
+    two_min = min([n for n, r in table.items() if r["twoshot"] < r.get("oneshot", 1e9)], default=0)
+    best = {n: min(v for k, v in r.items() if k != "rccl") for n, r in table.items()}
+    xgmi_max = max([n for n in table if "rccl" not in table[n] or best[n] < table[n]["rccl"]], default=0)
+    if table and xgmi_max == max(table):
+        xgmi_max = cap
+    return ll_max, two_min, xgmi_max
+
+
 def autotune_comm(tp: TPGroup, sizes=(16384, 65536, 262144, 1 << 20, 4 << 20)) -> None:
     """Graph-time every all-reduce transport at every message size class the engine issues (decode B=1:
     16 KiB; batched decode: up to 1 MiB at B=64; prefill chunks: MiBs), max over ranks, and set the
@@ -533,14 +595,8 @@ def autotune_comm(tp: TPGroup, sizes=(16384, 65536, 262144, 1 << 20, 4 << 20)) -
         log.info(f" all-reduce autotune {n} B: {row}")
     xg.ll_max_bytes, xg.twoshot_min_bytes = keep
     ok = xg.error() == 0
-    # thresholds from the measurements
-    ll_max = max([n for n, r in table.items() if "ll" in r and r["ll"] <= min(r.get("oneshot", 1e9), r["twoshot"])],
-                 default=0)
-    two_min = min([n for n, r in table.items() if r["twoshot"] < r.get("oneshot", 1e9)], default=0)
+    ll_max, two_min, xgmi_max = comm_thresholds(table, cap)
     best = {n: min(v for k, v in r.items() if k != "rccl") for n, r in table.items()}
-    xgmi_max = max([n for n in table if "rccl" not in table[n] or best[n] < table[n]["rccl"]], default=0)
-    if xgmi_max == max(sizes):
-        xgmi_max = cap
     xg.ll_max_bytes = ll_max
     xg.twoshot_min_bytes = two_min if two_min else cap + 16   # never, unless above the one-shot capacity
     tp.xgmi_max_ar = xgmi_max

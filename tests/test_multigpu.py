@@ -49,6 +49,7 @@ def _check_collectives(tp, res):
                 assert torch.equal(x.cpu(), (want32 + r.cpu().float()).to(torch.bfloat16)), \
                     f"xgmi {path} all_reduce+residual n={n}"
             xg.ll_max_bytes = keep
+        _check_twoshot(tp, res)
         for n in (4, 4096, 2048 * 4):
             src = torch.arange(n, dtype=torch.float32, device="cuda") + 1e6 * tp.rank
             out = tp.all_gather_shards(src)
@@ -86,6 +87,56 @@ def _check_collectives(tp, res):
                 torch.cuda.synchronize()
                 tol = 0 if dt == torch.float32 else 0.02 * float(want.abs().max())
                 assert float((x.float().cpu() - want).abs().max()) <= tol + 1e-3, f"rccl all_reduce {dt} n={n}"
+
+
+def _check_twoshot(tp, res):
+    """Two-shot all-reduce (reduce-scatter + all-gather through the peer slots), bit-exact against the fixed-order
+    fp32 sum at the MiB sizes the autotune routes to it (a 256-token TP = 8 prefill all-reduces 4 MiB), with and
+    without the fused residual, eager and replayed from a graph."""
+    xg, world = tp.xgmi, tp.world
+    keep = (xg.ll_max_bytes, xg.twoshot_min_bytes)
+    xg.ll_max_bytes, xg.twoshot_min_bytes = 0, 16
+    cap = xg.max_allreduce_bytes
+    sizes = sorted({n for n in (1 << 20, 2 << 20, 4 << 20, cap) if n <= cap})
+    try:
+        for seed, nbytes in enumerate(sizes):
+            n = nbytes // 2
+            want32 = sum(_data(r, n, 50 + seed).float() for r in range(world))
+            x = _data(tp.rank, n, 50 + seed).cuda()
+            tp.all_reduce_(x)
+            torch.cuda.synchronize()
+            assert torch.equal(x.cpu(), want32.to(torch.bfloat16)), f"two-shot all_reduce {nbytes} B"
+            r = _data(99, n, 50 + seed).cuda()
+            x = _data(tp.rank, n, 50 + seed).cuda()
+            tp.all_reduce_(x, residual=r)
+            torch.cuda.synchronize()
+            assert torch.equal(x.cpu(), (want32 + r.cpu().float()).to(torch.bfloat16)), f"two-shot + residual {nbytes} B"
+        # graph replays of the largest size: the slot / epoch state advances on the device
+        n = sizes[-1] // 2
+        src = _data(tp.rank, n, 77).cuda()
+        want = sum(_data(r, n, 77).float() for r in range(world)).to(torch.bfloat16)
+        buf = torch.empty_like(src)
+
+        def step():
+            buf.copy_(src)
+            tp.all_reduce_(buf)
+
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(3):
+                step()
+        for _ in range(4):
+            g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(buf.cpu(), want), "two-shot graph replay"
+    finally:
+        xg.ll_max_bytes, xg.twoshot_min_bytes = keep
+    res["twoshot_sizes"] = sizes
 
 
 def _model_and_engine(tp, res, preset="tiny-tp8"):
@@ -181,6 +232,7 @@ def _rehearsal_rank(rank, world):
 def _assert_model(res, world):
     r0 = res[0]
     assert all(res[r].get("xgmi_err", 0) == 0 for r in range(world))
+    assert r0.get("twoshot_sizes"), "two-shot sizes were not checked"
     if "tokens" not in r0:
         return
     assert r0["prefill_err"] < 0.03 * r0["logit_scale"] + 0.03, r0

@@ -81,6 +81,9 @@ def _worker(rank, world, port, q):
         res["graph_us_16k_flagged"] = _graph_time_us(
             lambda: xg.all_reduce_bf16(x.data_ptr(), x.data_ptr(), 16384, -1)) if x.numel() * 2 >= 16384 else 0.0
         xg.ll_max_bytes = ll
+        from test_multigpu import _check_twoshot
+
+        _check_twoshot(tp, res)                   # world 2: 1 MiB, the two-shot capacity
         # all-gather (fp32 logits layout, shard-major)
         for n in (4, 4096, 16032 * 4):
             src = torch.arange(n, dtype=torch.float32, device="cuda") + 1e6 * rank
@@ -178,6 +181,7 @@ def test_xgmi_two_ranks_one_gpu():
           f"TP2 vs TP1 max |d logit| prefill {r0['prefill_err']:.3g} decode {r0['decode_err']:.3g} "
           f"(scale {r0['logit_scale']:.3g})")
     assert r0["err"] == 0 and r1["err"] == 0
+    assert r0["twoshot_sizes"] == [1 << 20]
     assert r0["prefill_err"] < 0.05 * r0["logit_scale"] + 0.05
     assert r0["decode_err"] < 0.05 * r0["logit_scale"] + 0.05
     assert r0["tokens"] == r1["tokens"]          # replicated sampling from identical gathered logits
