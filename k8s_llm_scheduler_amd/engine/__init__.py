@@ -18,11 +18,12 @@ _GEMM_TABLE_LOADED = False
 
 
 def _load_gemm_table() -> bool:
-    """Pin the library GEMMs of batched decode (8 < rows: hipBLASLt / rocBLAS through F.linear) to the
-    solutions ``tools/tune_gemms.py`` measured fastest on MI355X (PyTorch TunableOp table, read with
-    tuning OFF, so captured graphs replay fixed kernels; shapes missing from the table keep the
-    library default).  TP=1, 64 rows: down 157 -> 117 us, gate/up 183 -> 164 us.  K8S_GEMM_TABLE=0
-    disables; a table written by another torch / hipBLASLt / arch fails its validators and is ignored."""
+    """Pin the library GEMMs (hipBLASLt / rocBLAS through F.linear) to the solutions ``tools/tune_gemms.py``
+    measured fastest on MI355X (PyTorch TunableOp table, read with tuning OFF, so captured graphs replay fixed
+    kernels; shapes missing from the table keep the library default).  The engine only issues library GEMMs
+    with K8S_GEMM=library (the A/B oracle of the hand-written kernels) -- the GEMM tuners load it for their
+    library columns.  K8S_GEMM_TABLE=0 disables; a table written by another torch / hipBLASLt / arch fails its
+    validators and is ignored."""
     global _GEMM_TABLE_LOADED
     if _GEMM_TABLE_LOADED:
         return True
@@ -63,10 +64,10 @@ def resolve_tokenizer(weights: Optional[str], tokenizer: Optional[str]) -> Optio
                             "random-init weights)")
 
 
-def warm_library_gemms(model) -> None:
-    """Run every library GEMM shape the engine can issue (layer 0's projections at each row bucket of
-    ops.GEMM_M_BUCKETS) once, so hipBLASLt / rocBLAS load their kernels now instead of inside the first
-    timed prefill (a first-use code-object load cost ~0.3 s in a TP=8-shape run)."""
+def warm_gemms(model) -> None:
+    """Run every routed GEMM shape the engine can issue below 1k rows (layer 0's projections at each row bucket of
+    ops.GEMM_M_BUCKETS) once, so every kernel / tile variant is loaded now instead of inside the first timed
+    prefill (a first-use code-object load cost ~0.3 s in a TP=8-shape run)."""
     import torch
 
     from .. import ops
@@ -101,7 +102,9 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
     if device is None:
         device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
     cfg = get_config(weights or preset) if weights else get_config(preset)
-    if device.startswith("cuda"):
+    from .. import ops
+
+    if device.startswith("cuda") and ops.GEMM_BACKEND == "library":
         _load_gemm_table()
     t0 = time.perf_counter()
     model = LlamaModel(cfg, tp, device=device, seed=seed, weights=weights, max_model_len=max_model_len,
@@ -118,7 +121,7 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
                     capture_nucleus=capture_nucleus, speculative_tokens=speculative_tokens, watchdog_s=watchdog_s,
                     on_unrecoverable=on_unrecoverable)
     if device.startswith("cuda"):
-        warm_library_gemms(model)
+        warm_gemms(model)
     if capture and eng.use_graphs:
         t1 = time.perf_counter()
         eng.capture_graphs()

@@ -1,5 +1,5 @@
 """One GEMM shape, mgemm (given config) and the library path back to back -- a target for
-`rocprofv3 --pmc ...` counter passes (tools/gpu_gemm_pmc.sh)."""
+`rocprofv3 --pmc ...` counter passes (tools/gpu_pgemm_pmc.sh)."""
 import argparse
 import sys
 
