@@ -344,6 +344,15 @@ PYBIND11_MODULE(_C, m) {
       .def("all_gather", [](XgmiComm& c, uintptr_t in, uintptr_t out, long long bytes, int64_t s) {
         c.all_gather(P(in), P(out), bytes, S(s));
       })
+      .def(
+          "gemv_allreduce",
+          [](XgmiComm& c, uintptr_t out, uintptr_t x, uintptr_t w, uintptr_t wscale, int M, int N, int K,
+             uintptr_t residual, int64_t s) {
+            return c.gemv_allreduce(P(out), P(x), P(w), reinterpret_cast<const float*>(wscale), M, N, K, P(residual),
+                                    S(s));
+          },
+          py::arg("out"), py::arg("x"), py::arg("w"), py::arg("wscale"), py::arg("M"), py::arg("N"), py::arg("K"),
+          py::arg("residual") = 0, py::arg("stream") = -1)
       .def("error", &XgmiComm::error)
       .def("snapshot_error", [](XgmiComm& c, int64_t s) { c.snapshot_error(S(s)); }, py::arg("stream") = -1)
       .def("last_error", &XgmiComm::last_error)

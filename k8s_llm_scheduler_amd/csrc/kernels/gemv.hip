@@ -63,6 +63,32 @@ __device__ __forceinline__ float dot16_fp8(u32x4 w, u32x4 x0, u32x4 x1, float ac
 
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
+// Tensor-parallel all-reduce fused into a row-parallel projection (o_proj / down at TP > 1 decode; SURVEY
+// K8 / K11 + K14 + K2): out = residual + sum over ranks of x_r . W_r^T, without a collective kernel.
+// Each wave owns two adjacent output rows, so its bf16-rounded partials for one input row are one 32-bit
+// word; lanes t < world push that word as an LL granule {word, epoch} (one 8-byte system-coherent store,
+// arrives untorn) into source row `rank` of rank t's fused-LL region (own rank included).  Workgroups are
+// grouped; the last workgroup of a group to finish (an arrival ticket) polls the group's granules from
+// all world sources in its own region until every tag equals the epoch, sums them in rank order 0..W-1
+// (fp32) plus the residual and rounds once: the same bits as the separate LL all-reduce, on every rank.
+// Only one workgroup per group ever waits for peers, after its own share of the weight stream is done.
+// Epochs are per group (identical on every rank: same grid, same call sequence); two parities per
+// (source, word) are enough for the reason the separate LL kernel gives (xgmi.hip).  Polls are bounded:
+// a timeout sets a bit of *err and the kernel drains.
+constexpr int GAR_MAX_WORLD = 8;
+constexpr int GAR_MAX_GROUPS = 64;
+constexpr int GAR_SYS = 1 | 16;  // buffer-op aux: sc0 | sc1 (system coherence)
+struct GemvAr {
+  char* base[GAR_MAX_WORLD];  // fused-LL region of every rank, mapped in this process
+  long long row_bytes;        // capacity of one (parity, source) row
+  uint32_t* epochs;           // [GAR_MAX_GROUPS] per-group epochs (uncached)
+  uint32_t* tickets;          // [GAR_MAX_GROUPS] arrival tickets, zero between calls (uncached)
+  uint32_t* err;              // poll-timeout bitmask
+  const bf16_t* res;          // [M, N_out] residual (may alias out)
+  long long timeout_ticks;    // s_memrealtime ticks (100 MHz)
+  int rank, world, group;     // group: workgroups per arrival group
+};
+
 // Fused pre-norm prologue (NORM): the GEMV input is rmsnorm(x + res_in) * nw, computed by every
 // workgroup from the full rows (L2-resident, M x K x 4 bytes), and workgroup (0, 0) writes the
 // updated residual r = x + res_in to res_out.  res_in and res_out must be different buffers
@@ -81,20 +107,24 @@ __device__ __forceinline__ void norm_row_chunk(const bf16_t* __restrict__ x, con
 // folded into W (W' = W * nw, done once at model load): the prologue only stages r = x + res_in and
 // its sum of squares, and the per-row 1/rms scales the accumulator in the epilogue -- no
 // normalisation pass and no barrier between the row statistics and the weight stream.
-template <int M, int RPW, int EPI, int NORM, bool FP8, int KW, int NT = 256>
+template <int M, int RPW, int EPI, int NORM, bool FP8, int KW, int NT = 256, bool AR = false>
 __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float* __restrict__ partial,
                                                    const bf16_t* __restrict__ x, const void* __restrict__ W,
                                                    int N_out, int K, int KS, int half_rows,
                                                    const bf16_t* __restrict__ res_in, bf16_t* __restrict__ res_out,
                                                    const bf16_t* __restrict__ nw, float eps,
-                                                   const float* __restrict__ wscale) {
+                                                   const float* __restrict__ wscale, GemvAr ar) {
   constexpr int EPC = FP8 ? 16 : 8;  // weights per 16-byte chunk
   constexpr int WB = FP8 ? 1 : 2;    // bytes per weight
+  static_assert(!AR || (EPI == EPI_BF16 && RPW == 2 && KW == 1 && NORM == 0), "fused all-reduce: plain 2-row waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u32x4* xs = reinterpret_cast<u32x4*>(smem);  // [M][KS/8]
   constexpr int NWV = NT / 64;  // waves per workgroup; NWV / KW row sets
   __shared__ float nred[NWV][M];
+  __shared__ uint32_t ar_state[2];  // AR: [epoch, last-arriver flag]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (AR && threadIdx.x == 0)
+    ar_state[0] = __hip_atomic_load(ar.epochs + blockIdx.x / ar.group, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   const int kb = blockIdx.y * KS;
   const int klen = min(KS, K - kb);
   const int nch = klen / EPC;  // 16-byte weight chunks in this slice
@@ -337,6 +367,79 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
 
+  if constexpr (AR) {
+    typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+    const uint32_t e = ar_state[0];
+    const int W = ar.world, nwd = N_out >> 1;  // LL words per input row
+    const long long par = (long long)(e & 1) * W;
+    // 1. push: lane t < W sends this wave's M words to rank t (row `rank` of its parity-(e & 1) slot)
+    if (active && lane < W) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(ar.base[lane] + (par + ar.rank) * ar.row_bytes, 0,
+                                                        (int)ar.row_bytes, 0x00020000);
+      const float s0 = FP8 ? wscale[r0] : 1.f, s1 = FP8 ? wscale[r0 + 1] : 1.f;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const u32x2 g = u32x2{pack_bf2(acc[0][m] * s0, acc[1][m] * s1), e};
+        __builtin_amdgcn_raw_buffer_store_b64(g, rs, (m * nwd + (r0 >> 1)) * 8, 0, GAR_SYS);
+      }
+    }
+    // 2. arrival ticket of this workgroup's group; the last arriver reduces the group's rows
+    const int grp = blockIdx.x / ar.group;
+    const int g0 = grp * ar.group, gn = min((int)gridDim.x, g0 + ar.group);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(ar.tickets + grp, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      ar_state[1] = old == (uint32_t)(gn - g0 - 1);
+    }
+    __syncthreads();
+    if (!ar_state[1]) return;
+    if (threadIdx.x == 0) {  // every workgroup of the group has read its epoch and arrived: reset for the next call
+      __hip_atomic_store(ar.tickets + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ar.epochs + grp, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // 3. words [w0, w1) of every input row, summed over the W sources in rank order, + residual, one rounding
+    constexpr int ROWS_WG = (NT / 64) * RPW;
+    const int w0 = g0 * ROWS_WG / 2, w1 = min(nwd, gn * ROWS_WG / 2), nw = w1 - w0;
+    const char* mine = ar.base[ar.rank] + par * ar.row_bytes;
+    const uint32_t* res = reinterpret_cast<const uint32_t*>(ar.res);
+    uint32_t* o = reinterpret_cast<uint32_t*>(out);
+    for (int i = threadIdx.x; i < M * nw; i += NT) {
+      const int m = i / nw, wi = m * nwd + w0 + (i - m * nw);
+      u32x2 g[GAR_MAX_WORLD];
+#pragma unroll
+      for (int t = 0; t < GAR_MAX_WORLD; ++t)
+        if (t < W)
+          g[t] = __builtin_amdgcn_raw_buffer_load_b64(
+              __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(mine) + t * ar.row_bytes, 0, (int)ar.row_bytes,
+                                                0x00020000), wi * 8, 0, GAR_SYS);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      float lo = 0.f, hi = 0.f;
+#pragma unroll
+      for (int t = 0; t < GAR_MAX_WORLD; ++t) {
+        if (t >= W) break;
+        while (g[t].y != e) {
+          __builtin_amdgcn_s_sleep(1);
+          if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > ar.timeout_ticks) {
+            __hip_atomic_fetch_or(ar.err, 1u << t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          g[t] = __builtin_amdgcn_raw_buffer_load_b64(
+              __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(mine) + t * ar.row_bytes, 0, (int)ar.row_bytes,
+                                                0x00020000), wi * 8, 0, GAR_SYS);
+        }
+        lo += lo_bf(g[t].x);
+        hi += hi_bf(g[t].x);
+      }
+      if (res != nullptr) {
+        const uint32_t rv = res[wi];
+        lo += lo_bf(rv);
+        hi += hi_bf(rv);
+      }
+      o[wi] = pack_bf2(lo, hi);
+    }
+    return;
+  }
+
   if (KW > 1) {  // combine the K parts of the waves sharing these rows
     __shared__ float kred[NWV][NR][M];
     if (lane == 0) {
@@ -488,11 +591,11 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
   const bf16_t* gw = (const bf16_t*)nw;
 #define G4(MM, RR, EE, F8, KK, NTT)                                                                            \
   if (mode == 1) gemv_kernel<MM, RR, EE, 1, F8, KK, NTT><<<grid, NTT, lds, stream>>>(                          \
-      out, part, xx, ww, N_out, K, ks, half_rows, ri, ro, gw, eps, wscale);                                      \
+      out, part, xx, ww, N_out, K, ks, half_rows, ri, ro, gw, eps, wscale, GemvAr{});                            \
   else if (mode == 2) gemv_kernel<MM, RR, EE, 2, F8, KK, NTT><<<grid, NTT, lds, stream>>>(                     \
-      out, part, xx, ww, N_out, K, ks, half_rows, ri, ro, gw, eps, wscale);                                      \
+      out, part, xx, ww, N_out, K, ks, half_rows, ri, ro, gw, eps, wscale, GemvAr{});                            \
   else gemv_kernel<MM, RR, EE, 0, F8, KK><<<grid, 256, lds, stream>>>(out, part, xx, ww, N_out, K, ks,          \
-                                                                       half_rows, ri, ro, gw, eps, wscale)
+                                                                       half_rows, ri, ro, gw, eps, wscale, GemvAr{})
 #define G3(MM, RR, EE, F8, KK)                  \
   if constexpr (KK == 2 && MM <= 4) {           \
     G4(MM, RR, EE, F8, KK, 512);                \
@@ -570,3 +673,48 @@ extern "C" int k8s_gemv_fp8(void* out, void* partial, const void* x, const void*
   if (wscale == nullptr) return -1;
   return k8s_gemv_norm_w(out, partial, x, W, wscale, M, N_out, K, epi, res_in, res_out, nw, eps, stream);
 }
+
+// Row-parallel projection with the tensor-parallel all-reduce (and the residual add) in its epilogue:
+// out[M, N_out] = residual + sum over ranks of x . W^T (see GemvAr).  Every rank must issue the same sequence of
+// these calls with the same shapes (the group epochs advance per call).  Two-row waves, one K slice (the whole
+// row of x in LDS), 4-wave workgroups.  Returns -5 where the shape does not fit that plan (the caller then runs
+// the GEMV and a separate all-reduce).
+extern "C" int k8s_gemv_allreduce(void* out, const void* x, const void* W, const float* wscale, int M, int N_out,
+                                  int K, const void* residual, void* const* bases, long long row_bytes,
+                                  uint32_t* epochs, uint32_t* tickets, uint32_t* err, int rank, int world,
+                                  long long timeout_ticks, hipStream_t stream) {
+  constexpr int ROWS_WG = 8;  // 4 waves x 2 rows
+  if (M < 1 || M > 8 || K % 16 != 0 || N_out <= 0 || world < 2 || world > GAR_MAX_WORLD || rank < 0 || rank >= world)
+    return -1;
+  if (N_out % ROWS_WG != 0 || (long long)M * K * 2 > 65536 || (long long)M * N_out * 4 > row_bytes) return -5;
+  const int nwg = N_out / ROWS_WG;
+  const int group = (nwg + 31) / 32;  // ~32 arrival groups: one waiting workgroup per group
+  if ((nwg + group - 1) / group > GAR_MAX_GROUPS) return -5;
+  GemvAr a;
+  for (int i = 0; i < GAR_MAX_WORLD; ++i) a.base[i] = i < world ? static_cast<char*>(bases[i]) : nullptr;
+  a.row_bytes = row_bytes; a.epochs = epochs; a.tickets = tickets; a.err = err;
+  a.res = static_cast<const bf16_t*>(residual); a.timeout_ticks = timeout_ticks;
+  a.rank = rank; a.world = world; a.group = group;
+  const bool fp8 = wscale != nullptr;
+  const size_t lds = (size_t)M * K * 2;
+  const bf16_t* xx = static_cast<const bf16_t*>(x);
+#define GAR(MM)                                                                                                     \
+  if (fp8) gemv_kernel<MM, 2, EPI_BF16, 0, true, 1, 256, true><<<nwg, 256, lds, stream>>>(                          \
+      out, nullptr, xx, W, N_out, K, K, 0, nullptr, nullptr, nullptr, 0.f, wscale, a);                               \
+  else gemv_kernel<MM, 2, EPI_BF16, 0, false, 1, 256, true><<<nwg, 256, lds, stream>>>(                             \
+      out, nullptr, xx, W, N_out, K, K, 0, nullptr, nullptr, nullptr, 0.f, wscale, a)
+  switch (M) {
+    case 1: GAR(1); break;
+    case 2: GAR(2); break;
+    case 3: GAR(3); break;
+    case 4: GAR(4); break;
+    case 5: GAR(5); break;
+    case 6: GAR(6); break;
+    case 7: GAR(7); break;
+    case 8: GAR(8); break;
+  }
+#undef GAR
+  return (int)hipGetLastError();
+}
+
+extern "C" int k8s_gemv_allreduce_max_groups() { return GAR_MAX_GROUPS; }

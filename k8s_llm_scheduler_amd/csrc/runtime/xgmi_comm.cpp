@@ -19,6 +19,11 @@ int k8s_xgmi_allreduce_2shot_bf16(void* const* bases, uint32_t* counters, uint32
 int k8s_xgmi_allgather(void* const* bases, uint32_t* counters, uint32_t* err, const void* in, void* out,
                        long long bytes, long long slot_bytes, int rank, int world, int blocks,
                        long long timeout_ticks, hipStream_t s);
+int k8s_gemv_allreduce(void* out, const void* x, const void* W, const float* wscale, int M, int N_out, int K,
+                       const void* residual, void* const* bases, long long row_bytes, uint32_t* epochs,
+                       uint32_t* tickets, uint32_t* err, int rank, int world, long long timeout_ticks,
+                       hipStream_t stream);
+int k8s_gemv_allreduce_max_groups();
 }
 
 namespace k8sllm {
@@ -39,7 +44,9 @@ XgmiComm::XgmiComm(int world, int rank, long long slot_bytes, int blocks, double
   if (world < 2 || world > 8 || rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad world/rank");
   if (slot_bytes <= 0 || (slot_bytes & 4095)) throw std::invalid_argument("XgmiComm: slot_bytes must be a multiple of 4096");
   if (blocks < 1 || blocks > k8s_xgmi_max_blocks()) throw std::invalid_argument("XgmiComm: bad block count");
-  region_bytes_ = k8s_xgmi_flag_bytes() + 8LL * world * slot_bytes;  // flagged + LL + two-shot (2 phases)
+  // flagged + LL + two-shot (2 phases) + the fused GEMV all-reduce's LL rows (gemv.hip GemvAr)
+  fused_off_ = k8s_xgmi_flag_bytes() + 8LL * world * slot_bytes;
+  region_bytes_ = fused_off_ + 2LL * world * slot_bytes;
   if (region_bytes_ > 0x7fffffffLL) throw std::invalid_argument("XgmiComm: region larger than 2 GiB");
   timeout_ticks_ = static_cast<long long>(timeout_s * 100e6);  // s_memrealtime runs at 100 MHz
   ck(hipGetDevice(&device_), "hipGetDevice");
@@ -47,6 +54,9 @@ XgmiComm::XgmiComm(int world, int rank, long long slot_bytes, int blocks, double
   ck(hipMemset(region_, 0, region_bytes_), "hipMemset");
   ck(hipMalloc(&counters_, (k8s_xgmi_max_blocks() + 1) * sizeof(uint32_t)), "hipMalloc");
   ck(hipMemset(counters_, 0, (k8s_xgmi_max_blocks() + 1) * sizeof(uint32_t)), "hipMemset");
+  ck(hipExtMallocWithFlags(reinterpret_cast<void**>(&fused_state_), 2 * k8s_gemv_allreduce_max_groups() * sizeof(uint32_t),
+                           hipDeviceMallocUncached), "hipExtMallocWithFlags(fused state)");
+  ck(hipMemset(fused_state_, 0, 2 * k8s_gemv_allreduce_max_groups() * sizeof(uint32_t)), "hipMemset");
   ck(hipHostMalloc(reinterpret_cast<void**>(&host_err_), sizeof(uint32_t), hipHostMallocDefault), "hipHostMalloc");
   *host_err_ = 0;
   ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
@@ -60,6 +70,7 @@ XgmiComm::~XgmiComm() {
     if (mapped_[i] && bases_[i]) (void)hipIpcCloseMemHandle(bases_[i]);
   if (region_) (void)hipFree(region_);
   if (counters_) (void)hipFree(counters_);
+  if (fused_state_) (void)hipFree(fused_state_);
   if (host_err_) (void)hipHostFree(host_err_);
 }
 
@@ -104,6 +115,19 @@ void XgmiComm::all_reduce_bf16(const void* in, void* out, long long bytes, hipSt
        "xgmi all_reduce");
 }
 
+int XgmiComm::gemv_allreduce(void* out, const void* x, const void* w, const float* wscale, int M, int N, int K,
+                             const void* residual, hipStream_t s) {
+  if (!opened_) throw std::runtime_error("XgmiComm: not open");
+  void* fb[8];
+  for (int i = 0; i < world_; ++i) fb[i] = static_cast<char*>(bases_[i]) + fused_off_;
+  const int rc = k8s_gemv_allreduce(out, x, w, wscale, M, N, K, residual, fb, slot_bytes_, fused_state_,
+                                    fused_state_ + k8s_gemv_allreduce_max_groups(), counters_ + k8s_xgmi_max_blocks(),
+                                    rank_, world_, timeout_ticks_, s);
+  if (rc == -5) return rc;  // shape outside the fused plan: the caller runs GEMV + all-reduce
+  ckrc(rc, "xgmi gemv_allreduce");
+  return 0;
+}
+
 void XgmiComm::all_gather(const void* in, void* out, long long bytes, hipStream_t s) {
   if (!opened_) throw std::runtime_error("XgmiComm: not open");
   ckrc(k8s_xgmi_allgather(bases_.data(), counters_, counters_ + k8s_xgmi_max_blocks(), in, out, bytes, slot_bytes_,
@@ -129,6 +153,7 @@ void XgmiComm::reset() {
   ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
   ck(hipMemset(region_, 0, region_bytes_), "hipMemset(region)");
   ck(hipMemset(counters_, 0, (k8s_xgmi_max_blocks() + 1) * sizeof(uint32_t)), "hipMemset(counters)");
+  ck(hipMemset(fused_state_, 0, 2 * k8s_gemv_allreduce_max_groups() * sizeof(uint32_t)), "hipMemset(fused state)");
   *host_err_ = 0;
   ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
 }

@@ -22,6 +22,11 @@ class XgmiComm {
   // out = sum over ranks of in (+ residual, a bf16 tensor of the same size, when given)
   void all_reduce_bf16(const void* in, void* out, long long bytes, hipStream_t s, const void* residual = nullptr);
   void all_gather(const void* in, void* out, long long bytes_per_rank, hipStream_t s);
+  // out[M, N] = residual + sum over ranks of x[M, K] . W[N, K]^T: the row-parallel decode projection with the
+  // all-reduce in its epilogue (kernels/gemv.hip GemvAr); W bf16, or fp8 e4m3 with per-row scales wscale.
+  // Returns -5 (nothing launched) where the shape does not fit the fused plan.
+  int gemv_allreduce(void* out, const void* x, const void* w, const float* wscale, int M, int N, int K,
+                     const void* residual, hipStream_t s);
   uint32_t error();                                   // poll-timeout bitmask (synchronizes the device)
   // Health check without an extra sync: enqueue a copy of the error word to pinned host memory on
   // `s`; after the caller's own synchronization of `s`, last_error() is that word.
@@ -53,6 +58,8 @@ class XgmiComm {
   int device_ = 0;
   void* region_ = nullptr;      // own IPC region (uncached)
   uint32_t* counters_ = nullptr;  // [max_blocks] epochs + 1 error word
+  uint32_t* fused_state_ = nullptr;  // gemv_allreduce: [max groups] epochs + [max groups] tickets (uncached)
+  long long fused_off_ = 0;          // byte offset of the gemv_allreduce LL rows in every region
   uint32_t* host_err_ = nullptr;  // pinned copy of the error word (snapshot_error)
   std::vector<void*> bases_;    // every rank's region in this address space
   std::vector<bool> mapped_;    // true where bases_[i] came from hipIpcOpenMemHandle

@@ -255,6 +255,7 @@ class LLMEngine:
         self._inbox_lock = threading.Lock()
         self._wake = threading.Condition(self._inbox_lock)
         self._bg_thread: Optional[threading.Thread] = None
+        self._abort_thread: Optional[threading.Thread] = None   # recover(): RCCL abort in flight
         self._bg_stop = False
         self._bg_error: Optional[BaseException] = None
         self.finished_log: Deque[tuple] = deque(maxlen=4096)
@@ -399,11 +400,17 @@ class LLMEngine:
                 return True
             tp = self.model.tp
             if not self._drained(drain_timeout):
-                if tp.rccl is not None and not tp.rccl.aborted:
-                    tp.abort_rccl()
-                    if self._drained(min(5.0, max(drain_timeout, 0.5))):
-                        return self._reset_all(announce=True)
+                # ncclCommAbort can block until the device work queued behind the stalled collective drains, so it
+                # runs on a helper thread: this call (and every retry until the device drains) returns at once
+                if tp.rccl is not None and not tp.rccl.aborted and self._abort_thread is None:
+                    self._abort_thread = threading.Thread(target=tp.abort_rccl, name="rccl-abort", daemon=True)
+                    self._abort_thread.start()
                 return False
+            if self._abort_thread is not None:
+                self._abort_thread.join(timeout=max(drain_timeout, 1.0))
+                if self._abort_thread.is_alive():
+                    return False
+                self._abort_thread = None
             return self._reset_all(announce=True)
 
     def _reset_all(self, announce: bool) -> bool:

@@ -440,18 +440,24 @@ class LlamaModel:
         single rounding: SURVEY K14 + K2), so the residual stream IS the all-reduce outputs and the
         norm-GEMV prologues read one tensor (no residual read, no residual write)."""
         c, kv = self.cfg, self.kv_cache
+        B = h.shape[0]
         g1 = None if self.norm_folded else (lambda w: w.ln1)
         g2 = None if self.norm_folded else (lambda w: w.ln2)
         x = h
         for l, w in enumerate(self.layers):
             qkv = ops.linear_norm(x, w.wqkv, g1(w) if g1 else None, c.rms_eps, None, None)
-            # attention + O projection: one launch (the W_o stream overlaps attention) where the shapes allow
-            o = ops.decode_attention_oproj(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
-                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D, w.wo)
-            self.tp.all_reduce_(o, residual=x)                 # o = x + attention branch
+            if ops.attn_oproj_fusable(B, w.wo, max_context, self.nq, self.nkv, self.D):
+                # attention + O projection: one launch (the W_o stream overlaps attention; opt-in)
+                o = ops.decode_attention_oproj(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
+                                               self.scale, self.block_size, max_context, self.nq, self.nkv, self.D,
+                                               w.wo)
+                self.tp.all_reduce_(o, residual=x)             # o = x + attention branch
+            else:
+                a = ops.decode_attention_fused(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
+                                               self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
+                o = self.tp.linear_all_reduce(a, w.wo, residual=x)   # o = x + attention branch (AR in the GEMV)
             g = ops.linear_norm(o, w.wgu, g2(w) if g2 else None, c.rms_eps, None, None, epi=ops.EPI_SWIGLU)
-            x = ops.linear(g, w.wdown)
-            self.tp.all_reduce_(x, residual=o)                 # x = o + MLP branch
+            x = self.tp.linear_all_reduce(g, w.wdown, residual=o)    # x = o + MLP branch
         logits = ops.linear_norm(x, self.lm_head, None if self.norm_folded else self.norm, c.rms_eps, None, None,
                                  epi=ops.EPI_F32)
         return self.tp.all_gather_shards(logits)

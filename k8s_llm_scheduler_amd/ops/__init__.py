@@ -291,6 +291,22 @@ def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0
 
 
 
+def gemv_allreduce(comm, x: torch.Tensor, w, residual: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """residual + sum over TP ranks of x @ w.T in one kernel (gemv.hip GemvAr: the all-reduce rides in the GEMV
+    epilogue over the xGMI peer regions of ``comm``, a native XgmiComm).  None where the shape does not fit the fused
+    plan (nothing was launched: the caller runs GEMV + all-reduce)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if residual is not None and (residual.dtype != BF16 or tuple(residual.shape) != (M, N)):
+        raise ValueError("residual must be a bf16 [M, N] tensor")
+    out = torch.empty(M, N, dtype=BF16, device=x.device)
+    fp8 = _is_fp8(w)
+    rc = comm.gemv_allreduce(out.data_ptr(), _chk(x, BF16, "x"), w.q.data_ptr() if fp8 else _chk(w, BF16, "w"),
+                             w.scale.data_ptr() if fp8 else 0, M, N, K,
+                             _chk(residual, BF16, "residual") if residual is not None else 0, -1)
+    return out if rc == 0 else None
+
+
 # Row counts of the library GEMMs in the tuned table (engine/assets/tunableop_gfx950.csv, written by
 # tools/tune_gemms.py): the engine's batched-decode buckets and the prefill buckets.  With the table
 # loaded, a library GEMM of M rows in (8, 1024] is padded to the next bucket so that it runs the

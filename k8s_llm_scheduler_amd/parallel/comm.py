@@ -94,6 +94,23 @@ class TPGroup:
                 t.add_(residual)
         return t
 
+    fused_ar: bool = os.environ.get("K8S_FUSED_AR", "1") != "0"
+
+    def linear_all_reduce(self, x: torch.Tensor, w, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``residual + all_reduce(x @ w.T)`` for a row-parallel projection (o_proj / down).  Decode rows on the
+        xGMI transport run ONE kernel: the GEMV pushes its partial rows to every peer in its epilogue and reduces
+        them there (kernels/gemv.hip GemvAr; ``K8S_FUSED_AR=0`` restores GEMV + separate all-reduce kernel).  The
+        result has the bits of the separate path."""
+        from .. import ops
+
+        if (self.fused_ar and self.world > 1 and not self.simulate and self.xgmi is not None and x.is_cuda
+                and x.dim() == 2 and x.shape[0] <= ops.GEMV_MAX_M and (residual is None or residual.is_contiguous())):
+            y = ops.gemv_allreduce(self.xgmi, x, w, residual)
+            if y is not None:
+                return y
+        y = ops.linear(x, w)
+        return self.all_reduce_(y, residual=residual)
+
     def all_gather_shards(self, t: torch.Tensor) -> torch.Tensor:
         """[..] local -> [world, ..] (shard-major)."""
         if self.world == 1:

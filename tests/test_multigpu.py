@@ -50,6 +50,7 @@ def _check_collectives(tp, res):
                     f"xgmi {path} all_reduce+residual n={n}"
             xg.ll_max_bytes = keep
         _check_twoshot(tp, res)
+        _check_fused_gemv_ar(tp, res)
         for n in (4, 4096, 2048 * 4):
             src = torch.arange(n, dtype=torch.float32, device="cuda") + 1e6 * tp.rank
             out = tp.all_gather_shards(src)
@@ -87,6 +88,75 @@ def _check_collectives(tp, res):
                 torch.cuda.synchronize()
                 tol = 0 if dt == torch.float32 else 0.02 * float(want.abs().max())
                 assert float((x.float().cpu() - want).abs().max()) <= tol + 1e-3, f"rccl all_reduce {dt} n={n}"
+
+
+def _check_fused_gemv_ar(tp, res):
+    """Row-parallel GEMV with the all-reduce in its epilogue (gemv.hip GemvAr): bit-exact against
+    GEMV + separate xGMI all-reduce where both GEMVs take one K slice, within bf16 rounding of the fp32 oracle
+    (sum over ranks of x_r . W_r^T, + residual) everywhere; bf16 and fp8 weights; graph replays."""
+    from k8s_llm_scheduler_amd import ops
+
+    world = tp.world
+    shapes = [(1, 2048, 256), (2, 2048, 512), (1, 8192, 1024), (4, 1024, 2048), (8, 512, 512), (1, 4096, 3584)]
+    done = []
+    for i, (M, N, K) in enumerate(shapes):
+        xs = [_data(r, M * K, 200 + i).view(M, K) for r in range(world)]
+        ws = [(_data(r, N * K, 300 + i) * 0.05).to(torch.bfloat16).view(N, K) for r in range(world)]
+        resid = _data(99, M * N, 400 + i).view(M, N)
+        x, w, rr = xs[tp.rank].cuda(), ws[tp.rank].cuda(), resid.cuda()
+        y = ops.gemv_allreduce(tp.xgmi, x, w, rr)
+        assert y is not None, f"fused plan refused {(M, N, K)}"
+        base = ops.linear(x, w)
+        tp.all_reduce_(base, residual=rr)
+        torch.cuda.synchronize()
+        ref = sum(xs[r].float() @ ws[r].float().T for r in range(world)) + resid.float()
+        err = float((y.float().cpu() - ref).abs().max())
+        assert err <= 0.02 * float(ref.abs().max()) + 0.05, f"fused gemv all-reduce {(M, N, K)}: err {err}"
+        ks, splits = ops.native().gemv_plan(M, N, K, ops.EPI_BF16, 0)
+        same_kernel = splits == 1 and M <= ops.GEMV_MAX_M   # linear() took the one-slice GEMV too (not mgemm)
+        if same_kernel:
+            assert torch.equal(y.cpu(), base.cpu()), f"fused != GEMV + all-reduce {(M, N, K)}"
+        # fp8 weights (per-row scales applied before the bf16 partial rounding, as the unfused GEMV does)
+        wq = ops.quantize_fp8(w)
+        y8 = ops.gemv_allreduce(tp.xgmi, x, wq, rr)
+        b8 = ops.linear(x, wq)
+        tp.all_reduce_(b8, residual=rr)
+        torch.cuda.synchronize()
+        assert y8 is not None
+        assert float((y8.float() - b8.float()).abs().max()) <= 0.02 * float(ref.abs().max()) + 0.05
+        if same_kernel:
+            assert torch.equal(y8.cpu(), b8.cpu()), f"fp8 fused != GEMV + all-reduce {(M, N, K)}"
+        done.append((M, N, K))
+    # captured and replayed, with the separate all-reduce kernels interleaved (their own epochs)
+    M, N, K = 1, 2048, 512
+    x = _data(tp.rank, M * K, 9).view(M, K).cuda()
+    w = (_data(tp.rank, N * K, 10) * 0.05).to(torch.bfloat16).view(N, K).cuda()
+    r0 = _data(99, M * N, 11).view(M, N).cuda()
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+
+    def step():
+        y = ops.gemv_allreduce(tp.xgmi, x, w, r0)
+        z = ops.gemv_allreduce(tp.xgmi, x, w, y)
+        tp.all_reduce_(z)
+        out.copy_(z)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    want = out.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(3):
+            step()
+    for _ in range(5):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, want), "fused gemv all-reduce graph replay"
+    res["fused_gemv_ar_shapes"] = done
 
 
 def _check_twoshot(tp, res):

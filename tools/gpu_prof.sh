@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 REPO="$GRAFT_REPO_ROOT"
 TAG="${1:-tp8sim}"
-ARGS="${2:---simulate-tp 8}"
+ARGS="${2---simulate-tp 8}"
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/gpurun_out/prof_$TAG" -o run -- python3 "$REPO/bench.py" --steps 2 --warmup 1 $ARGS > "$REPO/gpurun_out/prof_$TAG.log" 2>&1 || { tail -20 "$REPO/gpurun_out/prof_$TAG.log"; exit 1; }
