@@ -256,6 +256,7 @@ class LLMEngine:
         self._wake = threading.Condition(self._inbox_lock)
         self._bg_thread: Optional[threading.Thread] = None
         self._abort_thread: Optional[threading.Thread] = None   # recover(): RCCL abort in flight
+        self.recovery_trace: Deque[tuple] = deque(maxlen=64)     # (monotonic s, event) of recover() / resets
         self._bg_stop = False
         self._bg_error: Optional[BaseException] = None
         self.finished_log: Deque[tuple] = deque(maxlen=4096)
@@ -281,6 +282,7 @@ class LLMEngine:
         ev.record(torch.cuda.current_stream(self.device))
         self._last_event = ev
         if not self._await(ev, what):
+            self.recovery_trace.append((time.monotonic(), f"stalled: {what}"))
             self.stats["stalls"] += 1
             msg = f"engine stalled: {what} did not complete within the deadline (rank {self.model.tp.rank})"
             self._fail(msg)
@@ -395,11 +397,15 @@ class LLMEngine:
         parked operations error out).  Then every rank of the replica -- told through the control channel --
         resets its collectives (xGMI protocol state zeroed, a broken RCCL communicator rebuilt, bounded
         barrier) and drops all in-flight requests and cached prefixes.  Returns True when ready again."""
+        tr = self.recovery_trace
+        tr.append((time.monotonic(), "recover: waiting for the engine lock"))
         with self.lock:
             if self.ready:
                 return True
             tp = self.model.tp
-            if not self._drained(drain_timeout):
+            drained = self._drained(drain_timeout)
+            tr.append((time.monotonic(), f"recover: drained={drained}"))
+            if not drained:
                 # ncclCommAbort can block until the device work queued behind the stalled collective drains, so it
                 # runs on a helper thread: this call (and every retry until the device drains) returns at once
                 if tp.rccl is not None and not tp.rccl.aborted and self._abort_thread is None:
@@ -418,11 +424,13 @@ class LLMEngine:
         committed KV that was never written), reset the collectives.  ``announce``: rank 0 first tells the
         other ranks of the replica to do the same."""
         tp = self.model.tp
+        tr = self.recovery_trace
         try:
             if announce and self.control is not None and self.control.rank == 0:
                 self.control.request_reset()   # releases followers parked in a device wait (_await)
                 self.control.exchange({"new": [], "abort": [], "stop": False, "reset": True})
                 self.control.clear_failures()
+                tr.append((time.monotonic(), "reset: followers told"))
             err = EngineUnavailable(self.health["reason"] or "engine reset")
             for r in list(self.requests.values()) + list(self.waiting) + list(self.prefilling) + \
                     list(self.running.values()):
@@ -447,8 +455,10 @@ class LLMEngine:
             if self.gpu:
                 self.s_ctx.zero_()
                 self.s_steps.zero_()
+                tr.append((time.monotonic(), "reset: collectives"))
                 tp.reset_collectives(self.control, timeout_s=max(10.0, self.watchdog_s))
                 torch.cuda.synchronize(self.device)
+                tr.append((time.monotonic(), "reset: collectives done"))
             else:
                 tp.reset_collectives(self.control, timeout_s=max(10.0, self.watchdog_s))
         except Exception as e:  # noqa: BLE001 -- recovery failed: stay (or exit) not ready
@@ -1390,6 +1400,7 @@ class LLMEngine:
             params = [params or SamplingParams()] * len(prompts)
         if self._bg_thread is not None:
             return self._generate_bg(prompts, params, deadline)
+        self.recovery_trace.append((time.monotonic(), f"generate: ready={self.ready}"))
         if not self.ready and not self.recover(drain_timeout=0.05):
             raise EngineUnavailable(self.health["reason"] or "decision engine not ready")
         with self.lock:

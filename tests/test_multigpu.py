@@ -116,15 +116,18 @@ def _check_fused_gemv_ar(tp, res):
         same_kernel = splits == 1 and M <= ops.GEMV_MAX_M   # linear() took the one-slice GEMV too (not mgemm)
         if same_kernel:
             assert torch.equal(y.cpu(), base.cpu()), f"fused != GEMV + all-reduce {(M, N, K)}"
-        # fp8 weights (per-row scales applied before the bf16 partial rounding, as the unfused GEMV does)
+        # fp8 weights (per-row scales applied before the bf16 partial rounding, as the unfused GEMV does); above
+        # GEMV_MAX_M rows linear() quantizes the activations too (fp8 GEMM), so only the weight error is shared
         wq = ops.quantize_fp8(w)
         y8 = ops.gemv_allreduce(tp.xgmi, x, wq, rr)
-        b8 = ops.linear(x, wq)
-        tp.all_reduce_(b8, residual=rr)
         torch.cuda.synchronize()
         assert y8 is not None
-        assert float((y8.float() - b8.float()).abs().max()) <= 0.02 * float(ref.abs().max()) + 0.05
+        assert float((y8.float().cpu() - ref).abs().max()) <= 0.1 * float(ref.abs().max()) + 0.05, \
+            f"fp8 fused gemv all-reduce {(M, N, K)}"
         if same_kernel:
+            b8 = ops.linear(x, wq)
+            tp.all_reduce_(b8, residual=rr)
+            torch.cuda.synchronize()
             assert torch.equal(y8.cpu(), b8.cpu()), f"fp8 fused != GEMV + all-reduce {(M, N, K)}"
         done.append((M, N, K))
     # captured and replayed, with the separate all-reduce kernels interleaved (their own epochs)

@@ -70,6 +70,7 @@ def _rank(rank, world):
         t0 = time.monotonic()
         d2 = svc.decide(build(1), pods[1], nodes)                # rank 1 stalls under this one
         t_d2 = time.monotonic() - t0
+        trace = [(round(t - t0, 3), what) for t, what in eng.recovery_trace if t >= t0]
         r2 = _probe(port)
         end = time.monotonic() + 30
         while not eng._drained(0.0) and time.monotonic() < end:  # rank 1 resumes after ~6 s
@@ -78,7 +79,7 @@ def _rank(rank, world):
         r3 = _probe(port)
         out = dict(d1=(d1.fallback_needed, d1.reasoning), ready1=r1[0], d2=(d2.fallback_needed, d2.reasoning),
                    t_d2=t_d2, ready2=r2[0], body2=r2[1], d3=(d3.fallback_needed, d3.reasoning), ready3=r3[0],
-                   health=dict(eng.health), stalls=eng.stats["stalls"])
+                   health=dict(eng.health), stalls=eng.stats["stalls"], trace=trace)
         eng.shutdown_workers()
         metrics.stop()
     dist.barrier()
@@ -93,6 +94,7 @@ def test_stalled_peer_falls_back_fast_then_recovers():
     res = run_ranks(_rank, 2, env={"K8S_XGMI_TIMEOUT_S": "600", "K8S_TP_COMM": "xgmi",
                                    "K8S_TEST_PROBE_PORT": str(port)}, timeout_s=150)
     r0 = res[0]
+    print("rank 0 recovery trace (s after the stall was armed):", r0.get("trace"))
     engine_answer = lambda d: (not d[0]) or "JSON" in d[1]   # noqa: E731 -- random weights: the JSON parse fails
     assert engine_answer(r0["d1"]) and r0["ready1"] == 200, r0
     assert r0["d2"][0] and r0["t_d2"] < 3.5 and r0["stalls"] >= 1, r0     # fell back within ~llm.timeout

@@ -84,6 +84,25 @@ def _worker(rank, world, port, q):
         from test_multigpu import _check_twoshot
 
         _check_twoshot(tp, res)                   # world 2: 1 MiB, the two-shot capacity
+        from test_multigpu import _check_fused_gemv_ar
+
+        _check_fused_gemv_ar(tp, res)             # all-reduce in the row-parallel GEMV's epilogue
+        # a peer that never joins a fused call: rank 0's last arrivers give up after the 1 s poll bound and set the
+        # error word instead of hanging (a communicator of its own, so the main one stays in step)
+        from k8s_llm_scheduler_amd import ops
+
+        c = ops.native().XgmiComm(world, rank, 1 << 20, 16, 1.0)
+        hs = [None] * world
+        dist.all_gather_object(hs, c.handle())
+        c.open(hs)
+        if rank == 0:
+            xf = _data(0, 256, 5).view(1, 256).cuda()
+            wf = (_data(0, 2048 * 256, 6) * 0.05).to(torch.bfloat16).view(2048, 256).cuda()
+            assert ops.gemv_allreduce(c, xf, wf, None) is not None
+            torch.cuda.synchronize()
+            res["fused_timeout_err"] = c.error()
+        dist.barrier()
+        del c
         # all-gather (fp32 logits layout, shard-major)
         for n in (4, 4096, 16032 * 4):
             src = torch.arange(n, dtype=torch.float32, device="cuda") + 1e6 * rank
@@ -181,6 +200,8 @@ def test_xgmi_two_ranks_one_gpu():
           f"TP2 vs TP1 max |d logit| prefill {r0['prefill_err']:.3g} decode {r0['decode_err']:.3g} "
           f"(scale {r0['logit_scale']:.3g})")
     assert r0["err"] == 0 and r1["err"] == 0
+    assert r0["fused_timeout_err"] == 1 << 1, r0["fused_timeout_err"]   # rank 1 never arrived
+    assert r0["fused_gemv_ar_shapes"]
     assert r0["twoshot_sizes"] == [1 << 20]
     assert r0["prefill_err"] < 0.05 * r0["logit_scale"] + 0.05
     assert r0["decode_err"] < 0.05 * r0["logit_scale"] + 0.05
