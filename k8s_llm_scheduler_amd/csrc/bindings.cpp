@@ -8,8 +8,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <stdexcept>
 #include <string>
 
@@ -135,6 +137,23 @@ PYBIND11_MODULE(_C, m) {
                                       max_qlen, nq, nkv, D, bs, max_blocks, S(s)),
           "paged_prefill_attention");
   });
+  // Bounded wait for a recorded hipEvent (torch.cuda.Event.cuda_event) with the GIL released: the engine's per-step
+  // device waits must neither block forever (a stalled collective) nor hold the GIL while they poll (the control
+  // plane's watch / worker threads run beside the engine loop).  True once the event completed, False at the timeout.
+  m.def("event_wait", [](uintptr_t ev, double timeout_s) {
+    py::gil_scoped_release nogil;
+    const auto e = reinterpret_cast<hipEvent_t>(ev);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (long spins = 0;; ++spins) {
+      const hipError_t r = hipEventQuery(e);
+      if (r == hipSuccess) return true;
+      if (r != hipErrorNotReady) throw std::runtime_error(std::string("hipEventQuery: ") + hipGetErrorString(r));
+      const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (waited >= timeout_s) return false;
+      if (waited < 0.005) std::this_thread::yield();   // decode steps end within milliseconds: stay responsive
+      else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }, py::arg("event"), py::arg("timeout_s"));
   m.def("gemv_plan", [](int M, int N, int K, int epi, int mode) {
     int ks, sp;
     k8s_gemv_plan(M, N, K, epi, mode, &ks, &sp);

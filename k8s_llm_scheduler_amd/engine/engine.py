@@ -256,7 +256,8 @@ class LLMEngine:
         self._wake = threading.Condition(self._inbox_lock)
         self._bg_thread: Optional[threading.Thread] = None
         self._abort_thread: Optional[threading.Thread] = None   # recover(): RCCL abort in flight
-        self.recovery_trace: Deque[tuple] = deque(maxlen=64)     # (monotonic s, event) of recover() / resets
+        self.recovery_trace: Deque[tuple] = deque(maxlen=512)    # (monotonic s, event) of recover() / resets
+        self._trace_steps = os.environ.get("K8S_ENGINE_TRACE", "0") == "1"   # (tests) per-replay host timeline too
         self._bg_stop = False
         self._bg_error: Optional[BaseException] = None
         self.finished_log: Deque[tuple] = deque(maxlen=4096)
@@ -295,9 +296,19 @@ class LLMEngine:
         until the work completes or the leader requests a reset (then EngineStalled)."""
         worker = self.control is not None and self.control.rank != 0
         limit = self._wait_limit()
-        spins, reported = 0, False
+        reported = False
         next_check = time.monotonic() + 0.2
-        while not ev.query():
+        handle = ev.cuda_event
+        # slices of a native wait that releases the GIL (ops event_wait): the control plane's threads keep running
+        # while the engine waits for its device (a Python poll loop here starved them: round-3 serving regression)
+        while True:
+            now = time.monotonic()
+            if worker:
+                budget = max(0.0, next_check - now)
+            else:
+                budget = 0.05 if limit is None else max(0.0, min(0.05, limit - now))
+            if ops.native().event_wait(handle, budget):
+                return True
             now = time.monotonic()
             if worker:
                 if limit is not None and now > limit and not reported:
@@ -305,16 +316,13 @@ class LLMEngine:
                     self.stats["stalls"] += 1
                     self._fail(f"engine stalled: {what or 'a step'} did not complete within the watchdog "
                                f"(rank {self.model.tp.rank})")
-                if now > next_check:
+                if now >= next_check:
                     next_check = now + 0.05
                     if self.control.reset_generation() > self._reset_seen:
                         raise EngineStalled(f"rank 0 requested a reset while {what or 'a step'} was in flight "
                                             f"(rank {self.model.tp.rank})")
-            elif limit is not None and now > limit:
+            elif limit is not None and now >= limit:
                 return False
-            spins += 1
-            time.sleep(0 if spins < 200 else 2e-5)
-        return True
 
     def _dev(self, x, dtype=torch.int32) -> torch.Tensor:
         """Host data -> the engine's device without ever blocking the host: staged through pinned memory (the caching
@@ -349,6 +357,8 @@ class LLMEngine:
                 self._pinned[key] = buf
             buf.copy_(t, non_blocking=True)
             outs.append(buf)
+        if self._trace_steps:
+            self.recovery_trace.append((time.monotonic(), f"fetch {what}: waiting"))
         self._wait_device(what)
         if self._pf_events:
             self._account_prefill()
@@ -384,12 +394,7 @@ class LLMEngine:
             return True
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
-        end = time.monotonic() + max(0.0, timeout_s)
-        while not ev.query():
-            if time.monotonic() > end:
-                return False
-            time.sleep(1e-3)
-        return True
+        return bool(ops.native().event_wait(ev.cuda_event, max(0.0, timeout_s)))
 
     def recover(self, drain_timeout: float = 0.0) -> bool:
         """Bring a failed engine back.  The device must drain within ``drain_timeout`` s (a
@@ -848,6 +853,8 @@ class LLMEngine:
     def _prefill(self) -> None:
         if not self.prefilling:
             return
+        if self._trace_steps:
+            self.recovery_trace.append((time.monotonic(), f"prefill: {len(self.prefilling)} requests"))
         budget = self.max_prefill_tokens
         chunk = []  # (req, start, end)
         for r in self.prefilling:
@@ -1036,6 +1043,7 @@ class LLMEngine:
         live = list(self.running)
         events: List = []
         ran = 0
+        tr = self.recovery_trace if self._trace_steps else None
         for i in range(steps):
             if graph is not None:
                 graph.replay()
@@ -1043,6 +1051,8 @@ class LLMEngine:
             else:
                 self._decode_step(B, mc, nuc)
             ran += 1
+            if tr is not None:
+                tr.append((time.monotonic(), f"decode: replay {i} enqueued"))
             if early and self.gpu and lag:
                 ev = torch.cuda.Event()
                 ev.record()
@@ -1055,6 +1065,8 @@ class LLMEngine:
                     stop = int(bool(self._done_host[live].any()) or (tp_ctl is None and bool(self._inbox)))
                 else:
                     stop = 2          # deadline: run the chunk out, the fetch raises
+            if tr is not None:
+                tr.append((time.monotonic(), f"decode: replay {i - lag} polled, stop {stop}"))
             if tp_ctl is not None:
                 stop = tp_ctl.decide(stop)
             if stop == 1:
@@ -1065,6 +1077,8 @@ class LLMEngine:
         self.stats["decode_steps"] += ran
         tp = self.model.tp
         tp.snapshot_health()             # rides on the bounded wait below
+        if tr is not None:
+            tr.append((time.monotonic(), "decode: fetch"))
         hist, nsteps = self._fetch(self.s_hist[:B], self.s_steps[:B], what="decode")
         tp.check_health()                # a failed collective raises into the decision service
         self.stats["decode_time"] += time.perf_counter() - t0

@@ -91,7 +91,7 @@ def test_stalled_peer_falls_back_fast_then_recovers():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     port = free_port()
-    res = run_ranks(_rank, 2, env={"K8S_XGMI_TIMEOUT_S": "600", "K8S_TP_COMM": "xgmi",
+    res = run_ranks(_rank, 2, env={"K8S_XGMI_TIMEOUT_S": "600", "K8S_TP_COMM": "xgmi", "K8S_ENGINE_TRACE": "1",
                                    "K8S_TEST_PROBE_PORT": str(port)}, timeout_s=150)
     r0 = res[0]
     print("rank 0 recovery trace (s after the stall was armed):", r0.get("trace"))

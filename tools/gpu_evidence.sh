@@ -16,6 +16,7 @@ step() {  # step <seconds> <log> <cmd...>
 }
 for spec in ${RUNS:-arrivals tp8sim fp8 nodes256 prof256 proffp8b64}; do
   case $spec in
+    default) step 300 bench_default.json python -u bench.py --steps 6 --warmup 2 ;;
     arrivals) step 420 bench_arrivals_rate3.json python -u bench.py --arrival-rate 3 --steps 40 --warmup 5 ;;
     tp8sim) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2 ;;
     fp8) step 300 bench_fp8_tp1.json python -u bench.py --dtype fp8 --steps 6 --warmup 2 ;;
