@@ -118,14 +118,16 @@ def main() -> int:
     t_init = time.perf_counter()
     bs = 16
     per_seq = max(2048, args.max_model_len) + args.gen_tokens + bs   # KV blocks reserved per decision
-    eng = build_engine(args.preset, tp=tp, max_batch=max(1, args.batch), block_size=bs,
-                       num_blocks=max(args.batch, 2) * (per_seq // bs + 2) + 64,
+    # serving (--arrival-rate): the engine's decode batch must hold the pods in flight, not --batch (pods per step)
+    slots = max(1, args.batch, 16 if args.arrival_rate > 0 else 1)
+    eng = build_engine(args.preset, tp=tp, max_batch=slots, block_size=bs,
+                       num_blocks=max(slots, 2) * (per_seq // bs + 2) + 64,
                        max_model_len=args.max_model_len, cuda_graphs=not args.no_graphs,
                        prefix_caching=not args.no_prefix_cache, capture=False, decode_chunk=8,
                        weight_dtype=args.dtype, speculative_tokens=args.speculative, control=control)
     progress("engine built")
     if eng.use_graphs:
-        eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= max(1, args.batch)] or [1],
+        eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= slots] or [1],
                            nucleus=args.top_p < 1)
     if on_gpu:
         torch.cuda.synchronize()

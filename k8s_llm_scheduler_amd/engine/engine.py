@@ -104,6 +104,39 @@ def ngram_draft(seq: Sequence[int], k: int, n_max: int = 3) -> List[int]:
     return []
 
 
+class _HostStage:
+    """Ring of pinned host slots for small host -> device copies (LLMEngine._dev).  A slot is reused only once the copy
+    that last used it has executed (its event); if the device is so far behind that the next slot is still pending,
+    the engine is stalled and EngineStalled is raised instead of waiting.  Larger tensors take a one-off pinned
+    buffer."""
+
+    SLOTS, SLOT_BYTES = 64, 256 << 10
+
+    def __init__(self):
+        self.buf = torch.empty(self.SLOTS * self.SLOT_BYTES, dtype=torch.uint8, pin_memory=True)
+        self.events: List[Optional[torch.cuda.Event]] = [None] * self.SLOTS
+        self.next = 0
+
+    def to_device(self, t: torch.Tensor, device) -> torch.Tensor:
+        t = t.contiguous()
+        n = t.numel() * t.element_size()
+        if n > self.SLOT_BYTES:
+            return t.pin_memory().to(device, non_blocking=True)
+        i = self.next
+        ev = self.events[i]
+        if ev is not None and not ev.query():
+            raise EngineStalled("host staging ring full: the device has not run the last "
+                                f"{self.SLOTS} host-to-device copies")
+        self.next = (i + 1) % self.SLOTS
+        view = self.buf[i * self.SLOT_BYTES:i * self.SLOT_BYTES + n]
+        view.copy_(t.view(-1).view(torch.uint8))
+        out = view.view(t.dtype).view(t.shape).to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self.events[i] = ev
+        return out
+
+
 class EngineStalled(TimeoutError):
     """Device work of an engine step did not complete within the call deadline or the engine watchdog (a
     hung collective or kernel).  The engine stops accepting work until :meth:`LLMEngine.recover` succeeds."""
@@ -256,6 +289,7 @@ class LLMEngine:
         self._wake = threading.Condition(self._inbox_lock)
         self._bg_thread: Optional[threading.Thread] = None
         self._abort_thread: Optional[threading.Thread] = None   # recover(): RCCL abort in flight
+        self._stage: Optional["_HostStage"] = None               # pinned host -> device staging ring (_dev)
         self.recovery_trace: Deque[tuple] = deque(maxlen=512)    # (monotonic s, event) of recover() / resets
         self._trace_steps = os.environ.get("K8S_ENGINE_TRACE", "0") == "1"   # (tests) per-replay host timeline too
         self._bg_stop = False
@@ -325,13 +359,16 @@ class LLMEngine:
                 return False
 
     def _dev(self, x, dtype=torch.int32) -> torch.Tensor:
-        """Host data -> the engine's device without ever blocking the host: staged through pinned memory (the caching
-        host allocator keeps the block until its copy has run), because a copy from pageable memory waits for the
-        stream -- behind a stalled collective that is an unbounded wait."""
+        """Host data -> the engine's device without ever blocking the host.  A copy from pageable memory waits for
+        the stream, and allocating new pinned memory (tensor.pin_memory()) was measured to block until the device
+        drains too -- behind a stalled collective both are unbounded waits (tests/test_recovery_gpu.py).  So small
+        tensors go through a ring of pre-pinned slots (_HostStage), each reused only after its previous copy ran."""
         t = x if isinstance(x, torch.Tensor) else torch.tensor(x, dtype=dtype)
         if not self.gpu:
             return t
-        return t.pin_memory().to(self.device, non_blocking=True)
+        if self._stage is None:
+            self._stage = _HostStage()
+        return self._stage.to_device(t, self.device)
 
     def _poll_event(self, ev=None) -> bool:
         """Wait (bounded by the call deadline / watchdog) for ``ev`` or, without one, for the work enqueued so far;

@@ -25,6 +25,10 @@ for spec in ${RUNS:-arrivals tp8sim fp8 nodes256 prof256 proffp8b64}; do
     nodes256) step 400 bench_nodes256.json python -u bench.py --nodes 256 --max-model-len 32768 --steps 3 --warmup 1 ;;
     prof256) bash tools/gpu_prof.sh tp1_nodes256 "--nodes 256 --max-model-len 32768" > $O/prof256.log 2>&1 || { tail -20 $O/prof256.log; exit 1; }
              head -16 gpurun_out/rocprof_70b_tp1_nodes256_kernels.txt ;;
+    proftp1) bash tools/gpu_prof.sh tp1_default "" > $O/proftp1.log 2>&1 || { tail -20 $O/proftp1.log; exit 1; }
+             cat gpurun_out/lastfwd_tp1_default.txt | head -60 ;;
+    proftp8) bash tools/gpu_prof.sh tp8sim "--simulate-tp 8" > $O/proftp8.log 2>&1 || { tail -20 $O/proftp8.log; exit 1; }
+             cat gpurun_out/lastfwd_tp8sim.txt | head -60 ;;
     proffp8b64) bash tools/gpu_prof.sh tp1_fp8_b64 "--dtype fp8 --batch 64" > $O/proffp8.log 2>&1 || { tail -20 $O/proffp8.log; exit 1; }
              head -16 gpurun_out/rocprof_70b_tp1_fp8_b64_kernels.txt ;;
   esac
