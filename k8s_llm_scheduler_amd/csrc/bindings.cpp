@@ -68,6 +68,7 @@ long long k8s_sample_scratch_bytes(int B);
 long long k8s_sample_nucleus_bytes(int B, int shards);
 int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab, hipStream_t s);
 int k8s_silu_mul(void* out, const void* gu, int T, int I, hipStream_t s);
+int k8s_prefetch(const void* p, long long bytes, int blocks, void* sink, hipStream_t s);
 int k8s_hash_init(void* out, int rows, int cols, long long gcols, long long row0, long long col0, uint32_t seed,
                   uint32_t tensor_id, float scale, float shift, hipStream_t s);
 int k8s_mgemm_num_configs();
@@ -242,6 +243,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("sample_nucleus_bytes", [](int B, int shards) { return k8s_sample_nucleus_bytes(B, shards); });
   m.def("embedding", [](uintptr_t out, uintptr_t ids, uintptr_t table, int T, int H, int vocab, int64_t s) {
     check(k8s_embedding(P(out), P<int>(ids), P(table), T, H, vocab, S(s)), "embedding");
+  });
+  m.def("prefetch", [](uintptr_t p, long long bytes, int blocks, uintptr_t sink, int64_t s) {
+    check(k8s_prefetch(P(p), bytes, blocks, P(sink), S(s)), "prefetch");
   });
   m.def("silu_mul", [](uintptr_t out, uintptr_t gu, int T, int I, int64_t s) {
     check(k8s_silu_mul(P(out), P(gu), T, I, S(s)), "silu_mul");

@@ -45,9 +45,33 @@ __global__ void hash_init_kernel(bf16_t* __restrict__ out, int rows, int cols, l
   }
 }
 
+// Weight prefetch into the Infinity Cache (MALL) on a side stream, while the decode chain is latency-bound (attention):
+// default-policy 16-byte loads of the next projection's weights, so the GEMV that follows reads them from the MALL
+// instead of HBM.  The loaded values feed a never-taken store so the loads are not removed.
+__global__ __launch_bounds__(256) void prefetch_kernel(const u32x4* __restrict__ p, long long nvec,
+                                                       uint32_t* __restrict__ sink) {
+  constexpr int U = 8;   // 16-byte loads in flight per thread
+  uint32_t acc = 0;
+  const long long stride = (long long)gridDim.x * 256 * U;
+  for (long long v = (long long)blockIdx.x * 256 * U + threadIdx.x; v < nvec; v += stride) {
+    u32x4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = v + u * 256 < nvec ? p[v + u * 256] : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= t[u].x ^ t[u].w;
+  }
+  if (acc == 0x9e3779b9u && threadIdx.x >= 1024) sink[threadIdx.x] = acc;   // threadIdx.x < 256: never taken
+}
+
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+extern "C" int k8s_prefetch(const void* p, long long bytes, int blocks, void* sink, hipStream_t stream) {
+  if (bytes < 16 || blocks < 1) return 0;
+  prefetch_kernel<<<blocks, 256, 0, stream>>>((const u32x4*)p, bytes / 16, (uint32_t*)sink);
+  return (int)hipGetLastError();
+}
 
 extern "C" int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab,
                              hipStream_t stream) {

@@ -407,6 +407,35 @@ class LlamaModel:
 
     fused_decode = True
 
+    # ------------------------------------------------------------------ decode weight prefetch (opt-in experiment)
+    # K8S_DECODE_PREFETCH_MB = M > 0: after each layer's QKV GEMV a side stream reads the first M MB of that layer's
+    # O and gate/up weights into the Infinity Cache while attention (latency-bound, a few CUs) runs on the main stream;
+    # the branch joins at the end of the step (captured into the decode graphs as a fork / join).
+    _pf_stream: Optional[torch.cuda.Stream] = None
+
+    @property
+    def prefetch_bytes(self) -> int:
+        return int(float(os.environ.get("K8S_DECODE_PREFETCH_MB", "0")) * (1 << 20))
+
+    def _pf_layer(self, w: LayerWeights, budget: int) -> None:
+        cs = torch.cuda.current_stream(self.device)
+        if self._pf_stream is None:
+            self._pf_stream = torch.cuda.Stream(self.device)
+        ps = self._pf_stream
+        ps.wait_stream(cs)
+        with torch.cuda.stream(ps):
+            for t in (w.wo, w.wgu):
+                if budget <= 0:
+                    break
+                q = t.q if isinstance(t, ops.Fp8Weight) else t
+                n = min(budget, q.numel() * q.element_size())
+                ops.prefetch(t, n)
+                budget -= n
+
+    def _pf_join(self) -> None:
+        if self._pf_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._pf_stream)
+
     def _forward_decode_fused(self, tokens: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
                               max_context: int) -> torch.Tensor:
         """Decode step with 5 kernels per layer: [norm+QKV GEMV] -> [RoPE+KV write+attention] ->
@@ -419,8 +448,11 @@ class LlamaModel:
         res_a = torch.empty_like(h)
         res_b = torch.empty_like(h)
         res_in = None
+        pf = self.prefetch_bytes
         for w_l, w in enumerate(self.layers):
             qkv = ops.linear_norm(h, w.wqkv, None if self.norm_folded else w.ln1, c.rms_eps, res_in, res_b)
+            if pf:
+                self._pf_layer(w, pf)
             a = ops.decode_attention_fused(qkv, self.cos_sin, kv[w_l, 0], kv[w_l, 1], block_tables, context_lens,
                                            self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
             o = ops.linear(a, w.wo)
@@ -430,6 +462,8 @@ class LlamaModel:
             h = ops.linear(g, w.wdown)
             self.tp.all_reduce_(h)
             res_in = res_a
+        if pf:
+            self._pf_join()
         logits = ops.linear_norm(h, self.lm_head, None if self.norm_folded else self.norm, c.rms_eps, res_in, None,
                                  epi=ops.EPI_F32)
         return self.tp.all_gather_shards(logits)
@@ -444,8 +478,11 @@ class LlamaModel:
         g1 = None if self.norm_folded else (lambda w: w.ln1)
         g2 = None if self.norm_folded else (lambda w: w.ln2)
         x = h
+        pf = self.prefetch_bytes
         for l, w in enumerate(self.layers):
             qkv = ops.linear_norm(x, w.wqkv, g1(w) if g1 else None, c.rms_eps, None, None)
+            if pf:
+                self._pf_layer(w, pf)
             if ops.attn_oproj_fusable(B, w.wo, max_context, self.nq, self.nkv, self.D):
                 # attention + O projection: one launch (the W_o stream overlaps attention; opt-in)
                 o = ops.decode_attention_oproj(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
@@ -458,6 +495,8 @@ class LlamaModel:
                 o = self.tp.linear_all_reduce(a, w.wo, residual=x)   # o = x + attention branch (AR in the GEMV)
             g = ops.linear_norm(o, w.wgu, g2(w) if g2 else None, c.rms_eps, None, None, epi=ops.EPI_SWIGLU)
             x = self.tp.linear_all_reduce(g, w.wdown, residual=o)    # x = o + MLP branch
+        if pf:
+            self._pf_join()
         logits = ops.linear_norm(x, self.lm_head, None if self.norm_folded else self.norm, c.rms_eps, None, None,
                                  epi=ops.EPI_F32)
         return self.tp.all_gather_shards(logits)

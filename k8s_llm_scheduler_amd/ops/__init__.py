@@ -291,6 +291,15 @@ def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0
 
 
 
+def prefetch(w, nbytes: Optional[int] = None, blocks: int = 256) -> None:
+    """Read the first ``nbytes`` of weight ``w`` (bf16 tensor or Fp8Weight) with default-policy loads on the current
+    stream, so they sit in the Infinity Cache when the GEMV that streams them runs (misc.hip prefetch_kernel)."""
+    t = w.q if _is_fp8(w) else w
+    n = t.numel() * t.element_size() if nbytes is None else min(int(nbytes), t.numel() * t.element_size())
+    sink = _zeroed_scratch(t.device, "prefetch_sink", 4096)
+    native().prefetch(t.data_ptr(), n & ~15, blocks, sink, -1)
+
+
 def gemv_allreduce(comm, x: torch.Tensor, w, residual: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     """residual + sum over TP ranks of x @ w.T in one kernel (gemv.hip GemvAr: the all-reduce rides in the GEMV
     epilogue over the xGMI peer regions of ``comm``, a native XgmiComm).  None where the shape does not fit the fused

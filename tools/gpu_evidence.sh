@@ -19,6 +19,9 @@ for spec in ${RUNS:-arrivals tp8sim fp8 nodes256 prof256 proffp8b64}; do
     default) step 300 bench_default.json python -u bench.py --steps 6 --warmup 2 ;;
     arrivals) step 420 bench_arrivals_rate3.json python -u bench.py --arrival-rate 3 --steps 40 --warmup 5 ;;
     tp8sim) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2 ;;
+    pf8) K8S_DECODE_PREFETCH_MB=48 step 300 bench_tp8sim_prefetch48.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2 ;;
+    pf8b) K8S_DECODE_PREFETCH_MB=24 step 300 bench_tp8sim_prefetch24.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2 ;;
+    pf1) K8S_DECODE_PREFETCH_MB=64 step 300 bench_tp1_prefetch64.json python -u bench.py --steps 4 --warmup 1 ;;
     fp8) step 300 bench_fp8_tp1.json python -u bench.py --dtype fp8 --steps 6 --warmup 2 ;;
     fp8b64) step 400 bench_fp8_tp1_b64.json python -u bench.py --dtype fp8 --batch 64 --steps 3 --warmup 1 ;;
     b64) step 400 bench_tp1_b64.json python -u bench.py --batch 64 --steps 3 --warmup 1 ;;
