@@ -35,6 +35,7 @@ int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, c
                                 const int* context_lens, const int* block_tables, float scale, int num_seqs,
                                 int max_qlen, int nq, int nkv, int D, int block_size, int max_blocks, hipStream_t s);
 void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* ks_out, int* splits_out);
+int k8s_gemv_set_loop(int wg_per_cu);
 int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out,
                  int K, int epi, const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
 int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s);
@@ -155,6 +156,7 @@ PYBIND11_MODULE(_C, m) {
       else std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
   }, py::arg("event"), py::arg("timeout_s"));
+  m.def("gemv_set_loop", [](int wg) { return k8s_gemv_set_loop(wg); });
   m.def("gemv_plan", [](int M, int N, int K, int epi, int mode) {
     int ks, sp;
     k8s_gemv_plan(M, N, K, epi, mode, &ks, &sp);
@@ -339,6 +341,8 @@ PYBIND11_MODULE(_C, m) {
       .def("all_gather", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int64_t s) {
         c.all_gather(P(send), P(recv), count, dtype, S(s));
       })
+      .def("reduce_scatter", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int red,
+                                int64_t s) { c.reduce_scatter(P(send), P(recv), count, dtype, red, S(s)); })
       .def("broadcast", [](RcclComm& c, uintptr_t buf, size_t count, int dtype, int root, int64_t s) {
         c.broadcast(P(buf), count, dtype, root, S(s));
       })

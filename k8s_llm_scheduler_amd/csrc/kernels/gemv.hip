@@ -107,7 +107,11 @@ __device__ __forceinline__ void norm_row_chunk(const bf16_t* __restrict__ x, con
 // folded into W (W' = W * nw, done once at model load): the prologue only stages r = x + res_in and
 // its sum of squares, and the per-row 1/rms scales the accumulator in the epilogue -- no
 // normalisation pass and no barrier between the row statistics and the weight stream.
-template <int M, int RPW, int EPI, int NORM, bool FP8, int KW, int NT = 256, bool AR = false>
+// LOOP: every wave owns row sets s, s + S, s + 2 S, ... (S = waves in the grid) instead of one: x is staged into
+// LDS once per workgroup for several row sets, and the first weight block of the next row set is in flight while
+// the current one's last block is consumed (one-row-set waves have no such overlap -- an fp8 row of 8192 weights
+// is a single round of loads per lane).  Single K slice, one wave per row set, no fused all-reduce.
+template <int M, int RPW, int EPI, int NORM, bool FP8, int KW, int NT = 256, bool AR = false, bool LOOP = false>
 __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float* __restrict__ partial,
                                                    const bf16_t* __restrict__ x, const void* __restrict__ W,
                                                    int N_out, int K, int KS, int half_rows,
@@ -117,6 +121,7 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
   constexpr int EPC = FP8 ? 16 : 8;  // weights per 16-byte chunk
   constexpr int WB = FP8 ? 1 : 2;    // bytes per weight
   static_assert(!AR || (EPI == EPI_BF16 && RPW == 2 && KW == 1 && NORM == 0), "fused all-reduce: plain 2-row waves");
+  static_assert(!LOOP || (!AR && KW == 1 && NORM != 1), "row-set loop: one wave per row set, no prologue norm");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u32x4* xs = reinterpret_cast<u32x4*>(smem);  // [M][KS/8]
   constexpr int NWV = NT / 64;  // waves per workgroup; NWV / KW row sets
@@ -329,6 +334,107 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
   for (int r = 0; r < NR; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+
+  if constexpr (LOOP) {
+    const int S = (int)gridDim.x * NWV;                 // row sets per sweep of the grid
+    const int nsets = (N_out + RPW - 1) / RPW;
+    const int bpr = (nch + 64 * U - 1) / (64 * U);      // weight blocks per row set
+    int set = (int)blockIdx.x * NWV + wid;
+    if (set >= nsets) return;
+    if (NORM == 2) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) t += nred[w][m];
+        inv[m] = rsqrtf(t / (float)K + eps);
+      }
+    }
+    const char* nrow[NR];
+    for (int j = 0;;) {
+      u32x4 cur[U][NR];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) cur[u][r] = wv[u][r];
+      // issue the next block: the rest of this row set, or the first block of the wave's next row set
+      int nj = j + 1, nset = set;
+      if (nj == bpr) {
+        nj = 0;
+        nset = set + S;
+      }
+      if (nset < nsets) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+          const int n = min(nset * RPW + r, N_out - 1);
+          nrow[r] = Wb + (size_t)n * K * WB;
+          if (EPI == EPI_SWIGLU) nrow[RPW + r] = Wb + ((size_t)(n + half_rows) * K) * WB;
+        }
+        const int cn = nj * 64 * U + lane;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < NR; ++r)
+            wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(nrow[r]) + min(cn + 64 * u, clast));
+      }
+      const int c = j * 64 * U + lane;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (c + 64 * u < nch) {
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            if (FP8) {
+              const u32x4 x0 = xs[m * (KS >> 3) + 2 * (c + 64 * u)];
+              const u32x4 x1 = xs[m * (KS >> 3) + 2 * (c + 64 * u) + 1];
+#pragma unroll
+              for (int r = 0; r < NR; ++r) acc[r][m] = dot16_fp8(cur[u][r], x0, x1, acc[r][m]);
+            } else {
+              const u32x4 xv = xs[m * (KS >> 3) + c + 64 * u];
+#pragma unroll
+              for (int r = 0; r < NR; ++r) acc[r][m] = dot8(cur[u][r], xv, acc[r][m]);
+            }
+          }
+        }
+      }
+      if (nj == 0) {  // row set `set` is complete: reduce, scale, store, start the next one
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            float v = wave_sum(acc[r][m]);
+            if (NORM == 2) v *= inv[m];
+            acc[r][m] = v;
+          }
+        if (lane == 0) {
+#pragma unroll
+          for (int r = 0; r < RPW; ++r) {
+            const int n = set * RPW + r;
+            if (n >= N_out) break;
+            const float sg = FP8 ? wscale[n] : 1.f;
+            const float su = (FP8 && EPI == EPI_SWIGLU) ? wscale[n + half_rows] : 1.f;
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              const float a = acc[r][m] * sg;
+              if (EPI == EPI_F32) {
+                reinterpret_cast<float*>(out)[(size_t)m * N_out + n] = a;
+              } else if (EPI == EPI_SWIGLU) {
+                reinterpret_cast<bf16_t*>(out)[(size_t)m * N_out + n] = f2bf(silu(a) * (acc[RPW + r][m] * su));
+              } else {
+                reinterpret_cast<bf16_t*>(out)[(size_t)m * N_out + n] = f2bf(a);
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+          for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+        if (nset >= nsets) return;
+        set = nset;
+      }
+      j = nj;
+    }
+  }
   for (int c = cb + lane; active && c < ce; c += 64 * U) {
     u32x4 cur[U][NR];
 #pragma unroll
@@ -560,6 +666,15 @@ extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* k
 // may be null when the plan has a single split.
 // wscale != null: W is fp8 (OCP e4m3, one fp32 scale per weight row); K must be a multiple of 16.
 // mode: 0 plain, 1 norm weight nw applied in the prologue, 2 norm weight folded into W (nw unused)
+// Row-set loop (LOOP): workgroups per CU the grid is cut to (0 = one row set per wave).  K8S_GEMV_LOOP sets it at
+// load; k8s_gemv_set_loop changes it (tests, A/B probes).
+static int g_gemv_loop = [] { const char* e = getenv("K8S_GEMV_LOOP"); return e ? atoi(e) : 0; }();
+extern "C" int k8s_gemv_set_loop(int wg_per_cu) {
+  const int old = g_gemv_loop;
+  if (wg_per_cu >= 0) g_gemv_loop = wg_per_cu;
+  return old;
+}
+
 static int gemv_launch(int mode, void* out, void* partial, const void* x, const void* W, const float* wscale, int M,
                        int N_out, int K, int epi, const void* res_in, void* res_out, const void* nw, float eps,
                        hipStream_t stream) {
@@ -589,6 +704,31 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
   const bf16_t* ri = (const bf16_t*)res_in;
   bf16_t* ro = (bf16_t*)res_out;
   const bf16_t* gw = (const bf16_t*)nw;
+  const int loop_wg = g_gemv_loop;
+  if (loop_wg > 0 && splits == 1 && kw == 1 && mode != 1 && M <= 2 && (int)grid.x > 256 * loop_wg) {
+    const int per = ((int)grid.x + 256 * loop_wg - 1) / (256 * loop_wg);   // row sets per wave
+    const dim3 lgrid(((int)grid.x + per - 1) / per, 1);
+#define GL(MM, RR, EE, F8, NN)                                                                                     \
+  gemv_kernel<MM, RR, EE, NN, F8, 1, 256, false, true><<<lgrid, 256, lds, stream>>>(out, nullptr, xx, ww, N_out, K, \
+                                                                                     ks, half_rows, ri, ro, gw, eps, \
+                                                                                     wscale, GemvAr{})
+#define GL2(MM, RR, EE)                                             \
+  if (fp8) { if (mode == 2) { GL(MM, RR, EE, true, 2); } else { GL(MM, RR, EE, true, 0); } }    \
+  else { if (mode == 2) { GL(MM, RR, EE, false, 2); } else { GL(MM, RR, EE, false, 0); } }
+#define GLE(MM, RR)                                      \
+  switch (epi) {                                         \
+    case EPI_BF16: GL2(MM, RR, EPI_BF16); break;         \
+    case EPI_F32: GL2(MM, RR, EPI_F32); break;           \
+    case EPI_SWIGLU: GL2(MM, RR, EPI_SWIGLU); break;     \
+    default: return -2;                                  \
+  }
+    if (M == 1) { if (rpw == 2) { GLE(1, 2) } else { GLE(1, 1) } }
+    else { if (rpw == 2) { GLE(2, 2) } else { GLE(2, 1) } }
+#undef GLE
+#undef GL2
+#undef GL
+    return (int)hipGetLastError();
+  }
 #define G4(MM, RR, EE, F8, KK, NTT)                                                                            \
   if (mode == 1) gemv_kernel<MM, RR, EE, 1, F8, KK, NTT><<<grid, NTT, lds, stream>>>(                          \
       out, part, xx, ww, N_out, K, ks, half_rows, ri, ro, gw, eps, wscale, GemvAr{});                            \

@@ -72,6 +72,11 @@ void RcclComm::all_gather(const void* send, void* recv, size_t count, int dtype,
   ck(ncclAllGather(send, recv, count, dt(dtype), static_cast<ncclComm_t>(comm_), s), "ncclAllGather");
 }
 
+void RcclComm::reduce_scatter(const void* send, void* recv, size_t count, int dtype, int red, hipStream_t s) {
+  if (!comm_) throw std::runtime_error("RCCL communicator aborted");
+  ck(ncclReduceScatter(send, recv, count, dt(dtype), op(red), static_cast<ncclComm_t>(comm_), s), "ncclReduceScatter");
+}
+
 std::string RcclComm::async_error() const {
   if (!comm_) return "communicator aborted";
   ncclResult_t r = ncclSuccess;

@@ -670,6 +670,8 @@ class LLMEngine:
             return True
         if tp.xgmi is None:
             return False
+        if self.model.seq_parallel_at(Tb) and tp.rccl is not None:
+            return False                   # the reduce-scatters run on RCCL: eager, like every RCCL chunk
         ar_bytes = Tb * self.model.cfg.hidden * 2
         gather_bytes = logits_rows * self.model.lm_head.shape[0] * 4
         return ar_bytes <= (tp.xgmi_max_ar or tp.xgmi.max_allreduce_bytes) and gather_bytes <= tp.xgmi.slot_bytes
@@ -682,7 +684,7 @@ class LLMEngine:
 
     def _overlap_split_at(self, T: int) -> int:
         """Token at which a TP > 1 prefill chunk of T tokens splits into two micro-batches (0: no split)."""
-        if T < self.model.prefill_overlap_min or not self.model.prefill_overlap:
+        if T < self.model.prefill_overlap_min or not self.model.prefill_overlap or self.model.seq_parallel_at(T):
             return 0
         return max(16, T // 2 // 16 * 16)
 

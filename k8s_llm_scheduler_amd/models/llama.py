@@ -312,6 +312,48 @@ class LlamaModel:
         wait(pend[1])
         return torch.cat(r)
 
+    # ------------------------------------------------------------------ sequence parallelism (prefill)
+    @property
+    def seq_parallel_min(self) -> int:
+        return int(os.environ.get("K8S_SEQ_PARALLEL_MIN", "2048"))
+
+    def seq_parallel_at(self, T: int) -> bool:
+        """TP > 1 prefill chunks of at least ``K8S_SEQ_PARALLEL_MIN`` tokens run sequence-parallel when
+        ``K8S_SEQ_PARALLEL=1`` (``=sim`` also on a simulated TP rank, for profiling the shapes)."""
+        env = os.environ.get("K8S_SEQ_PARALLEL", "0")
+        if self.tp.world <= 1 or env == "0" or not self.norm_folded or (self.tp.simulate and env != "sim"):
+            return False
+        return T >= self.seq_parallel_min
+
+    def _layers_folded_sp(self, h: torch.Tensor, attn) -> torch.Tensor:
+        """``_layers_folded`` with Megatron sequence parallelism (SURVEY 2.6 P-SP): the residual stream lives as
+        row shards, rank k holding rows [k n, (k + 1) n) of the chunk (n = ceil(T / tp)); every all-reduce becomes
+        a reduce-scatter (residual added on the shard) and the next pre-norm projection's input an all-gather of
+        the un-normalised shards (the RMS statistics are the GEMM prologue, as without SP).  The same bytes cross
+        xGMI as with the all-reduce; what changes is that residual adds and the residual stream itself are 1/tp
+        per rank, and the two halves of each collective are separate operations (docs/ARCHITECTURE.md, "TP = 8
+        prefill communication").  Chunks whose length does not divide by tp carry zero rows at the end, which
+        stay zero through every layer (zero input rows give zero RMS-scaled outputs)."""
+        eps = self.cfg.rms_eps
+        W, rk = self.tp.world, self.tp.rank
+        T, H = h.shape
+        n = -(-T // W)
+        pad = n * W - T
+        if pad:
+            h = torch.cat([h, h.new_zeros(pad, H)])
+        r = h[rk * n:(rk + 1) * n].clone()
+        for l, w in enumerate(self.layers):
+            x = self.tp.all_gather_rows(r)                          # [n W, H] residual stream, un-normalised
+            qkv = ops.linear_rms(x[:T] if pad else x, w.wqkv, eps)
+            a = attn(l, qkv)
+            if pad:
+                a = torch.cat([a, a.new_zeros(pad, a.shape[1])])
+            r = self.tp.reduce_scatter_rows(ops.linear(a, w.wo), residual=r)      # r + attention branch
+            x = self.tp.all_gather_rows(r)
+            g = ops.linear_rms(x, w.wgu, eps, ops.EPI_SWIGLU)
+            r = self.tp.reduce_scatter_rows(ops.linear(g, w.wdown), residual=r)   # r + MLP branch
+        return self.tp.all_gather_rows(r)[:T]
+
     def _logits_folded(self, r: torch.Tensor) -> torch.Tensor:
         logits = ops.linear_rms(r, self.lm_head, self.cfg.rms_eps, ops.EPI_F32)   # final norm folded: [S, Vs]
         return self.tp.all_gather_shards(logits)                               # [tp, S, Vs]
@@ -359,6 +401,9 @@ class LlamaModel:
             return a.view(T, self.nq * self.D)
 
         li = last_idx.long()
+        if self.seq_parallel_at(T):
+            r = self._layers_folded_sp(ops.embedding(ids, self.embed), attn)
+            return self._logits_folded(r.index_select(0, li).contiguous())
         if split is not None and self.prefill_overlap:
             T0 = split[0]
             pieces = ((slice(0, T0), split[1]), (slice(T0, T), split[2]))

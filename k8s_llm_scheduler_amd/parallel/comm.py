@@ -129,6 +129,36 @@ class TPGroup:
             dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         return out
 
+    def reduce_scatter_rows(self, t: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Sequence parallelism (SURVEY 2.6 P-SP): rows [rank * n, (rank + 1) * n) of the sum over the TP group of
+        ``t`` [world * n, ...], plus ``residual`` (this rank's n rows of the residual stream).  RCCL reduce-scatter
+        where a communicator exists; otherwise the all-reduce transports (xGMI, gloo) and this rank's rows -- the
+        same sum.  ``t`` may be overwritten."""
+        T = t.shape[0]
+        if T % self.world:
+            raise ValueError(f"reduce_scatter_rows: {T} rows do not split over {self.world} ranks")
+        n = T // self.world
+        if self.world == 1:
+            out = t
+        elif self.simulate:
+            out = t[:n]                    # one rank's shapes, collective skipped
+        elif self.rccl is not None and t.is_cuda and t.dtype in _DT:
+            t = t.contiguous()
+            out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            self.rccl.reduce_scatter(t.data_ptr(), out.data_ptr(), out.numel(), _DT[t.dtype], 0, -1)
+        else:
+            out = self.all_reduce_(t.contiguous())[self.rank * n:(self.rank + 1) * n]
+        if residual is not None:
+            out.add_(residual)
+        return out
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """[n, ...] row shard of every rank -> [world * n, ...] in rank order (the inverse of reduce_scatter_rows)."""
+        if self.world == 1:
+            return t
+        g = self.all_gather_shards(t)
+        return g.view((g.shape[0] * g.shape[1],) + tuple(g.shape[2:]))
+
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world > 1:
             dist.broadcast(t, src=self.leader + src, group=self.group)

@@ -544,3 +544,46 @@ def test_attention_oproj_fused_matches_separate(nq, nkv, B, monkeypatch):
         ref_o = og.clone() if ref_o is None else ref_o
         assert torch.equal(og, ref_o)
     assert ops.attn_oproj_timeouts(torch.device(DEV)) == 0
+
+
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("epi,folded", [(0, False), (1, True), (2, True), (2, False), (0, True)])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_gemv_row_set_loop_matches_single(M, epi, folded, fp8):
+    """The row-set loop (several row sets per wave, x staged once, the next set's weights in flight) gives the
+    one-row-set GEMV's bits, and both match the fp32 oracle.  N is large enough for the loop to engage at 1-2
+    workgroups per CU; 1283 rows leave a ragged last row set."""
+    K = 8192
+    torch.manual_seed(7 * M + epi + 100 * fp8)
+    N = 4099 if epi != 2 else 2051
+    x, res = rnd(M, K), rnd(M, K)
+    w = rnd(2 * N if epi == 2 else N, K, scale=0.05)
+    ww = ops.quantize_fp8(w) if fp8 else w
+    wd = ref.dequant_fp8(ww.q.cpu(), ww.scale.cpu()) if fp8 else w.cpu().float()
+    ro = torch.zeros(M, K, dtype=torch.bfloat16, device=DEV)
+    out_dtype = torch.float32 if epi == 1 else torch.bfloat16
+
+    def run():
+        if folded:
+            return ops.linear_norm(x, ww, None, 1e-5, res, ro, epi=epi)
+        return ops._gemv(x, ww, epi, out_dtype)
+
+    old = ops.native().gemv_set_loop(0)
+    try:
+        base = run()
+        outs = []
+        for lp in (1, 2):
+            ops.native().gemv_set_loop(lp)
+            outs.append(run())
+    finally:
+        ops.native().gemv_set_loop(old)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, base)
+    h = x.cpu().float()
+    if folded:
+        rf = (x.float() + res.float()).bfloat16().cpu().float()
+        h = rf * torch.rsqrt(rf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    y32 = h @ wd.T
+    want = torch.nn.functional.silu(y32[:, :N]) * y32[:, N:] if epi == 2 else y32
+    close(base, want, 3e-2)

@@ -244,6 +244,15 @@ def _model_and_engine(tp, res, preset="tiny-tp8"):
     res["split_kv_err"] = float((kv_a.float() - kv_b.float()).abs().max())
     res["split_scale"] = float(lg_a.float().abs().max())
     res["split_kv_scale"] = float(kv_a.float().abs().max())
+    # the same chunk sequence-parallel: reduce-scatter + all-gather of row shards in place of each all-reduce
+    os.environ.update(K8S_SEQ_PARALLEL="1", K8S_SEQ_PARALLEL_MIN="16")
+    try:
+        assert m.seq_parallel_at(160)
+        lg_s, kv_s = _run_chunk(m, 0)
+    finally:
+        os.environ["K8S_SEQ_PARALLEL"] = "0"
+    res["sp_err"] = float((lg_a.float() - lg_s.float()).abs().max())
+    res["sp_kv_err"] = float((kv_a.float() - kv_s.float()).abs().max())
     del m
     eng = build_engine(preset, tp=tp, device="cuda", max_batch=4, max_model_len=512, num_blocks=128, seed=1,
                        capture_nucleus=True)   # a top_p < 1 request below: the graphs with the nucleus passes
@@ -316,6 +325,8 @@ def _assert_model(res, world):
     # the halves' GEMMs have other row counts (other tiles / k-split orders): bf16 rounding, not a layout error
     assert r0["split_kv_err"] < 0.02 * r0["split_kv_scale"] + 0.02, r0
     assert r0["split_err"] < 0.02 * r0["split_scale"] + 0.02, r0
+    assert r0["sp_kv_err"] < 0.02 * r0["split_kv_scale"] + 0.02, r0
+    assert r0["sp_err"] < 0.02 * r0["split_scale"] + 0.02, r0
     assert r0["long_graph_replayed"], r0["prefill_graphs"]
     toks, replays, accepted = r0["spec"]
     assert all(res[r]["spec"] == r0["spec"] for r in range(world)), "ranks diverged under speculative decoding"

@@ -1,0 +1,35 @@
+# Round-3 GPU steps on one MI355X, chosen by RUNS (space-separated): tests, smoke, bench, loopprobe, prof, ...
+# Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
+# (any other rc) ends the script.  Logs land in gpurun_out/r3/.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+O=gpurun_out/r3; mkdir -p $O
+step() {  # step <seconds> <log> <cmd...>
+  local t=$1 log=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$O/$log" 2>&1
+  local rc=$?
+  echo "$log rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -30 "$O/$log"; exit $rc; fi
+  return 0
+}
+for spec in ${RUNS:-tests smoke bench}; do
+  case $spec in
+    tests) step 600 gputests.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+           tail -3 $O/gputests.log ;;
+    ktests) step 300 ktests.log python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread
+           tail -3 $O/ktests.log ;;
+    smoke) step 180 smoke.log python -c "import __graft_entry__ as g; g.smoke()"
+           tail -1 $O/smoke.log | cut -c1-300 ;;
+    bench) step 400 bench_default.json python -u bench.py --steps 8 --warmup 2
+           grep -h '"metric"' $O/bench_default.json | cut -c1-600 ;;
+    fp8) step 400 bench_fp8.json python -u bench.py --dtype fp8 --steps 6 --warmup 2
+           grep -h '"metric"' $O/bench_fp8.json | cut -c1-600 ;;
+    fp8loop) K8S_GEMV_LOOP=${LOOPWG:-4} step 400 bench_fp8_loop.json python -u bench.py --dtype fp8 --steps 6 --warmup 2
+           grep -h '"metric"' $O/bench_fp8_loop.json | cut -c1-600 ;;
+    loopprobe) step 400 gemv_loop_probe.txt python -u tools/gemv_loop_probe.py --tp 1 4 8
+           cat $O/gemv_loop_probe.txt | grep -v amdgpu.ids ;;
+    prof) bash tools/gpu_prof.sh tp1_default "" > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+          head -24 gpurun_out/rocprof_70b_tp1_default_kernels.txt ;;
+  esac
+done
