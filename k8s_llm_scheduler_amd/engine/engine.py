@@ -971,10 +971,14 @@ class LLMEngine:
             logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx), bt_d,
                                                 max(e - s for _, s, e in chunk), t(last), split=split)
         self.stats["prefill_tokens"] += len(ids)
+        if self._trace_steps:
+            self.recovery_trace.append((time.monotonic(), "prefill: forward enqueued"))
         done = [(i, r) for i, (r, s, e) in enumerate(chunk) if e == len(r.prompt_ids)]
         for r, s, e in chunk:
             r.computed = e
             self.allocator.commit_prefix(r.blocks, r.prompt_ids, e)
+            if self._trace_steps:
+                self.recovery_trace.append((time.monotonic(), "prefill: committed"))
         if done:
             idx = self._dev([i for i, _ in done], torch.long)
             sub = logits.index_select(1, idx).contiguous()   # [tp, n, Vs]
@@ -982,8 +986,12 @@ class LLMEngine:
             temp = self._dev([r.params.temperature for r in rs], torch.float32)
             top_p = self._dev([r.params.top_p for r in rs], torch.float32)
             seeds = self._dev([r.seed for r in rs])
+            if self._trace_steps:
+                self.recovery_trace.append((time.monotonic(), "prefill: staged"))
             ctr = self._dev([len(r.prompt_ids) for r in rs])
             toks = ops.sample(sub, temp, top_p, seeds, ctr, shards=sub.shape[0], nucleus=self._wants_nucleus(rs))
+            if self._trace_steps:
+                self.recovery_trace.append((time.monotonic(), "prefill: sample enqueued"))
             slots_t = self._dev([r.slot for r in rs], torch.long)
             forced0 = [(k, r.params.forced_output_ids[0]) for k, r in enumerate(rs) if r.params.forced_output_ids]
             if forced0:   # scripted answers replace the sampled first token too
@@ -996,7 +1004,11 @@ class LLMEngine:
             self.s_temp[slots_t] = temp
             self.s_top_p[slots_t] = top_p
             self.s_seeds[slots_t] = seeds
+            if self._trace_steps:
+                self.recovery_trace.append((time.monotonic(), "prefill: state written"))
             self._init_stop_state(rs, slots_t)
+            if self._trace_steps:
+                self.recovery_trace.append((time.monotonic(), "prefill: stop state"))
             for r in rs:
                 row = torch.zeros(self.max_blocks_per_seq, dtype=torch.int32)
                 row[:len(r.blocks)] = torch.tensor(r.blocks, dtype=torch.int32)
@@ -1006,6 +1018,8 @@ class LLMEngine:
                 r.first_token_time = now
                 self.prefilling.remove(r)
                 self.running[r.slot] = r
+        if self._trace_steps:
+            self.recovery_trace.append((time.monotonic(), f"prefill: {len(done)} sampled"))
         if self.gpu:
             # no per-prefill wait: the decode that follows in this step waits (bounded) for both and checks the
             # collectives' health; only a step that prefills and decodes nothing bounds its device work here.
@@ -1083,6 +1097,8 @@ class LLMEngine:
         events: List = []
         ran = 0
         tr = self.recovery_trace if self._trace_steps else None
+        if tr is not None:
+            tr.append((time.monotonic(), f"decode: {steps} steps, graph {graph is not None}"))
         for i in range(steps):
             if graph is not None:
                 graph.replay()

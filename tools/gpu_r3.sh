@@ -27,6 +27,16 @@ for spec in ${RUNS:-tests smoke bench}; do
            grep -h '"metric"' $O/bench_fp8.json | cut -c1-600 ;;
     fp8loop) K8S_GEMV_LOOP=${LOOPWG:-4} step 400 bench_fp8_loop.json python -u bench.py --dtype fp8 --steps 6 --warmup 2
            grep -h '"metric"' $O/bench_fp8_loop.json | cut -c1-600 ;;
+    recov) step 200 recovery.log python -u -m pytest tests/test_recovery_gpu.py -x -q -s --timeout 180 --timeout-method thread
+           grep -E "recovery trace|passed|failed" $O/recovery.log | cut -c1-3000 ;;
+    ab) for i in 1 2; do for lw in 0 ${LOOPWG:-2}; do
+          K8S_GEMV_LOOP=$lw step 400 ab_${AB_TAG:-fp8}_loop${lw}_$i.json python -u bench.py ${AB_ARGS:---dtype fp8} --steps 6 --warmup 2
+          grep -h '"metric"' $O/ab_${AB_TAG:-fp8}_loop${lw}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('loop=$lw', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'), d.get('init_s'))"
+        done; done ;;
+    tp8) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
+           grep -h '"metric"' $O/bench_tp8sim.json | cut -c1-600 ;;
+    pf8) K8S_DECODE_PREFETCH_MB=${PFMB:-24} step 300 bench_tp8sim_pf.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
+           grep -h '"metric"' $O/bench_tp8sim_pf.json | cut -c1-600 ;;
     loopprobe) step 400 gemv_loop_probe.txt python -u tools/gemv_loop_probe.py --tp 1 4 8
            cat $O/gemv_loop_probe.txt | grep -v amdgpu.ids ;;
     prof) bash tools/gpu_prof.sh tp1_default "" > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
