@@ -670,7 +670,8 @@ class LLMEngine:
             return True
         if tp.xgmi is None:
             return False
-        if self.model.seq_parallel_at(Tb) and tp.rccl is not None:
+        sp = getattr(self.model, "seq_parallel_at", None)
+        if sp is not None and sp(Tb) and tp.rccl is not None:
             return False                   # the reduce-scatters run on RCCL: eager, like every RCCL chunk
         ar_bytes = Tb * self.model.cfg.hidden * 2
         gather_bytes = logits_rows * self.model.lm_head.shape[0] * 4
@@ -682,9 +683,14 @@ class LLMEngine:
         return (pk[:Tb], pk[Tm:Tm + Tb], pk[2 * Tm:2 * Tm + Tb], pk[3 * Tm:3 * Tm + 2], pk[3 * Tm + 2:3 * Tm + 3],
                 pk[3 * Tm + 3:3 * Tm + 4])
 
+    def _seq_parallel_at(self, T: int) -> bool:
+        """The model runs a T-token prefill chunk sequence-parallel (LlamaModel.seq_parallel_at)."""
+        f = getattr(self.model, "seq_parallel_at", None)
+        return bool(f(T)) if f is not None else False
+
     def _overlap_split_at(self, T: int) -> int:
         """Token at which a TP > 1 prefill chunk of T tokens splits into two micro-batches (0: no split)."""
-        if T < self.model.prefill_overlap_min or not self.model.prefill_overlap or self.model.seq_parallel_at(T):
+        if T < self.model.prefill_overlap_min or not self.model.prefill_overlap or self._seq_parallel_at(T):
             return 0
         return max(16, T // 2 // 16 * 16)
 
@@ -997,13 +1003,15 @@ class LLMEngine:
             if forced0:   # scripted answers replace the sampled first token too
                 fk = self._dev([k for k, _ in forced0], torch.long)
                 toks = toks.index_copy(0, fk, self._dev([v for _, v in forced0]))
-            self.s_tokens[slots_t] = toks
-            self.s_ctx[slots_t] = ctr + 1
-            self.s_hist[slots_t, 0] = toks
-            self.s_steps[slots_t] = 1
-            self.s_temp[slots_t] = temp
-            self.s_top_p[slots_t] = top_p
-            self.s_seeds[slots_t] = seeds
+            # index_copy_ / index_fill_, not `state[idx] = value`: a Python scalar assigned that way is copied to the
+            # device from pageable memory, which waits for the stream -- behind a stalled collective, for good
+            self._put(self.s_tokens, slots_t, toks)
+            self._put(self.s_ctx, slots_t, ctr + 1)
+            self._put(self.s_hist.select(1, 0), slots_t, toks)
+            self.s_steps.index_fill_(0, slots_t, 1)
+            self._put(self.s_temp, slots_t, temp)
+            self._put(self.s_top_p, slots_t, top_p)
+            self._put(self.s_seeds, slots_t, seeds)
             if self._trace_steps:
                 self.recovery_trace.append((time.monotonic(), "prefill: state written"))
             self._init_stop_state(rs, slots_t)
@@ -1044,6 +1052,11 @@ class LLMEngine:
                 keep.append((a, b))
         self._pf_events = keep
 
+    @staticmethod
+    def _put(dst: torch.Tensor, idx: torch.Tensor, src: torch.Tensor) -> None:
+        """dst[idx] = src along dim 0, enqueued without a host sync."""
+        dst.index_copy_(0, idx, src.to(dst.dtype))
+
     def _init_stop_state(self, rs: Sequence[Request], slots_t: torch.Tensor) -> None:
         """Device stop state of freshly prefilled slots: first token unclassified (-2), stop config (EOS / JSON
         close / max_tokens), the scripted answer of forced requests, done flag clear."""
@@ -1061,9 +1074,9 @@ class LLMEngine:
                 n = min(len(f), self.max_new_cap)
                 self.s_forced[r.slot, :n] = self._dev(f[:n])
             self._done_host[r.slot] = 0
-        self.s_json[slots_t] = -2
-        self.s_cfg[slots_t] = self._dev(cfg)
-        self.s_forced_len[slots_t] = self._dev(flen)
+        self.s_json.index_fill_(0, slots_t, -2)
+        self._put(self.s_cfg, slots_t, self._dev(cfg))
+        self._put(self.s_forced_len, slots_t, self._dev(flen))
 
     def _decode(self, max_steps: Optional[int] = None) -> List[Request]:
         if not self.running:
@@ -1266,9 +1279,9 @@ class LLMEngine:
                     continue
                 # device decode state of the slot, as the one-token decode path leaves it
                 slot = r.slot
-                self.s_tokens[slot] = r.output_ids[-1]
-                self.s_ctx[slot] = len(r.prompt_ids) + len(r.output_ids)
-                self.s_steps[slot] = len(r.output_ids)
+                self.s_tokens[slot:slot + 1].fill_(r.output_ids[-1])     # fill_: no pageable host copy
+                self.s_ctx[slot:slot + 1].fill_(len(r.prompt_ids) + len(r.output_ids))
+                self.s_steps[slot:slot + 1].fill_(len(r.output_ids))
         self.stats["decode_steps"] += 1
         self.stats["decode_time"] += time.perf_counter() - t0
         if self.metrics is not None:
