@@ -4,11 +4,14 @@
 // kernel serve plain prefill, chunked prefill and prefix-cached prompts: query i of sequence s
 // sits at absolute position ctx_s - qlen_s + i and attends keys [0, pos].
 //
-// GQA packing: one workgroup = 4 waves = 64 (query, head) rows = QT = 64 / G consecutive queries x
+// GQA packing: one workgroup = NW waves = 16 NW (query, head) rows = QT = 16 NW / G consecutive queries x
 // the G query heads that share ONE kv head (G = nq / nkv), so every K/V tile is fetched once per
 // group instead of once per query head (8x fewer K/V bytes at Llama-3.3-70B's 8:1 GQA), and the
 // causal key range of a workgroup ends at its QT-th query instead of its 64th.  Row r of the
 // workgroup is query tile * QT + r / G, head kvh * G + r % G.
+// NW = 4 (64 rows) or 8 (128 rows): every K/V byte a workgroup stages feeds 16 NW rows of MFMA work, so at
+// long contexts -- where every workgroup streams the whole causal K/V range through L2 -- the 8-wave form
+// halves the K/V traffic per FLOP.  The host takes it when the grid still has >= 256 such workgroups.
 //
 // Structure:
 //  * "swapped" QK^T: S^T = K . Q^T with v_mfma_f32_16x16x32_bf16, so each lane ends up holding
@@ -22,6 +25,8 @@
 //    t+1 are in flight during tile t's MFMAs), then stored into swizzled LDS images shared by the
 //    4 waves; K fragments are read back with conflict-free ds_read_b128.
 //  * online softmax in the log2 domain (scale * log2(e) folded into S).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace k8sllm {
@@ -30,18 +35,19 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 __device__ __forceinline__ int v_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
-template <int D, int G>
-__global__ void __launch_bounds__(256) paged_prefill_kernel(
+template <int D, int G, int NW>
+__global__ void __launch_bounds__(64 * NW) paged_prefill_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ cu_q, const int* __restrict__ context_lens,
     const int* __restrict__ block_tables, float scale_log2, int nq, int nkv, int block_size, int max_blocks) {
   static_assert(D == 128, "head_dim 128");
   constexpr int KT = 64;             // keys per tile
-  constexpr int CPT = KT * D / 8 / 256;  // 16-byte chunks of one tile per thread (K and V each)
+  constexpr int NT = 64 * NW;        // threads
+  constexpr int CPT = KT * D / 8 / NT;  // 16-byte chunks of one tile per thread (K and V each)
   __shared__ __attribute__((aligned(16))) char klds[KT * D * 2];
   __shared__ __attribute__((aligned(16))) char vlds[KT * D * 2];
 
-  constexpr int QT = 64 / G;  // queries per workgroup
+  constexpr int QT = 16 * NW / G;  // queries per workgroup
   const int s = blockIdx.z, kvh = blockIdx.y, tile = blockIdx.x;
   const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
   if (tile * QT >= qlen) return;
@@ -56,7 +62,7 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   const int kv_end = qstart + last_row + 1;  // keys needed by this workgroup
   const int ntiles = (kv_end + KT - 1) / KT;
 
-  // Tile staging, one tile ahead: thread tid fetches chunks idx = tid + 256c (key row idx/16,
+  // Tile staging, one tile ahead: thread tid fetches chunks idx = tid + NT c (key row idx/16,
   // 16-byte column chunk idx%16) of K and V into registers while the current tile is computed,
   // then stores them swizzled into LDS.  Keys past the context: K clamped (their scores are
   // masked), V zero (P is 0 there, V must be finite).
@@ -64,7 +70,7 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   auto fetch = [&](int t) {
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
-      const int idx = tid + 256 * c;
+      const int idx = tid + NT * c;
       const int key = t * KT + idx / (D / 8), ch = idx % (D / 8);
       const int kc = min(key, ctx - 1);
       const size_t off = (size_t)(bt[kc / block_size] * block_size + kc % block_size) * kv_stride + kvh * D + ch * 8;
@@ -96,7 +102,7 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
     // ---- tile t: registers -> LDS (both images swizzled: 16-byte chunk ch of row r at ch ^ swz(r))
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
-      const int idx = tid + 256 * c;
+      const int idx = tid + NT * c;
       const int kr = idx / (D / 8), ch = idx % (D / 8);
       *reinterpret_cast<u32x4*>(klds + kr * (D * 2) + 16 * (ch ^ (kr & 15))) = kn[c];
       *reinterpret_cast<u32x4*>(vlds + kr * (D * 2) + 16 * (ch ^ v_swz(kr))) = vn[c];
@@ -225,22 +231,29 @@ extern "C" int k8s_paged_prefill_attention(void* out, const void* q, const void*
   if (D != 128 || nq % nkv != 0) return -1;
   const int G = nq / nkv;
   const float sl2 = scale * 1.4426950408889634f;
-#define PF(GG)                                                                                               \
+  // 8 waves per workgroup when that grid still covers every CU (K8S_PREFILL_ATTN_WAVES = 4 / 8 forces one form)
+  static const int waves_env = [] { const char* e = getenv("K8S_PREFILL_ATTN_WAVES"); return e ? atoi(e) : 0; }();
+  const long long wg8 = (long long)((max_qlen + 128 / G - 1) / (128 / G)) * nkv * num_seqs;
+  const int nw = (waves_env == 4 || waves_env == 8) ? waves_env : (wg8 >= 256 && 128 / G >= 1 ? 8 : 4);
+#define PF(GG, NWW)                                                                                          \
   {                                                                                                          \
-    dim3 grid((max_qlen + 64 / GG - 1) / (64 / GG), nkv, num_seqs);                                          \
-    paged_prefill_kernel<128, GG><<<grid, 256, 0, stream>>>((bf16_t*)out, (const bf16_t*)q,                 \
-                                                            (const bf16_t*)k_cache, (const bf16_t*)v_cache, \
-                                                            cu_q, context_lens, block_tables, sl2, nq, nkv,  \
-                                                            block_size, max_blocks);                         \
+    constexpr int QT = 16 * NWW / GG;                                                                        \
+    dim3 grid((max_qlen + QT - 1) / QT, nkv, num_seqs);                                                      \
+    paged_prefill_kernel<128, GG, NWW><<<grid, 64 * NWW, 0, stream>>>(                                       \
+        (bf16_t*)out, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, cu_q, context_lens,  \
+        block_tables, sl2, nq, nkv, block_size, max_blocks);                                                 \
   }
+#define PFW(GG) \
+  if (nw == 8) PF(GG, 8) else PF(GG, 4)
   switch (G) {  // query heads per kv head (Llama-3.3-70B: 8; Llama-3-8B: 4)
-    case 1: PF(1) break;
-    case 2: PF(2) break;
-    case 4: PF(4) break;
-    case 8: PF(8) break;
-    case 16: PF(16) break;
+    case 1: PFW(1) break;
+    case 2: PFW(2) break;
+    case 4: PFW(4) break;
+    case 8: PFW(8) break;
+    case 16: PFW(16) break;
     default: return -1;
   }
+#undef PFW
 #undef PF
   return (int)hipGetLastError();
 }

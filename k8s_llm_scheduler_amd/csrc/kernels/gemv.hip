@@ -184,10 +184,10 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
       }
     }
   }
-  // plain input: the first 4 x chunks per thread (a whole 8192-wide row at 256 threads) are loaded
+  // plain input: the first XP x chunks per thread (XP = 4 at M <= 2: a whole 8192-wide row at 256 threads) are loaded
   // BEFORE the weight stream too, so staging them into LDS waits for x only, not for the first
   // weight block (loads retire in order: a wait for x issued after the weights is a wait for both)
-  constexpr int XP = 4;
+  constexpr int XP = M <= 2 ? 4 : (M <= 4 ? 2 : 1);   // px holds XP x M x 4 registers: cap it at ~32 for any M
   u32x4 px[XP][M];
   if (NORM == 0) {
     // unconditional buffer loads bounded by the slice: a chunk past it reads 0 without a memory access

@@ -102,6 +102,20 @@ def test_paged_decode_attention(nq, nkv, ctxs):
 @pytest.mark.parametrize("nq,nkv", [(8, 1), (64, 8), (4, 2)])
 @pytest.mark.parametrize("qlens,cached", [([37], [0]), ([130, 1, 64], [0, 5, 17]), ([200], [160])])
 def test_paged_prefill_attention(nq, nkv, qlens, cached):
+    _prefill_attention_case(nq, nkv, qlens, cached)
+
+
+@pytest.mark.parametrize("nq,nkv,qlens,cached", [(64, 8, [600, 45], [1200, 30]), (8, 1, [4100], [0]),
+                                                 (64, 8, [513], [3000])])
+def test_paged_prefill_attention_eight_wave(nq, nkv, qlens, cached):
+    """Grids of >= 256 eight-wave workgroups (16 queries x 8 heads each at 8:1 GQA) take the 8-wave form: long
+    contexts, several sequences, a chunk after a long cached prefix."""
+    G = nq // nkv
+    assert -(-max(qlens) // (128 // G)) * nkv * len(qlens) >= 256
+    _prefill_attention_case(nq, nkv, qlens, cached)
+
+
+def _prefill_attention_case(nq, nkv, qlens, cached):
     D, bs = 128, 16
     S = len(qlens)
     ctxs = [q + c for q, c in zip(qlens, cached)]

@@ -33,6 +33,18 @@ for spec in ${RUNS:-tests smoke bench}; do
           K8S_GEMV_LOOP=$lw step 400 ab_${AB_TAG:-fp8}_loop${lw}_$i.json python -u bench.py ${AB_ARGS:---dtype fp8} --steps 6 --warmup 2
           grep -h '"metric"' $O/ab_${AB_TAG:-fp8}_loop${lw}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('loop=$lw', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'), d.get('init_s'))"
         done; done ;;
+    mg) step 500 multigpu.log python -u -m pytest tests/test_multigpu.py -x -q -s --timeout 480 --timeout-method thread
+           grep -E "rehearsal|passed|failed" $O/multigpu.log | cut -c1-600 ;;
+    n256) step 400 bench_nodes256.json python -u bench.py --nodes 256 --max-model-len 32768 --steps 3 --warmup 1
+           grep -h '"metric"' $O/bench_nodes256.json | cut -c1-200; grep -ho '"decode_ms_per_step[^}]*prefill_tokens_per_decision": [0-9.]*' $O/bench_nodes256.json ;;
+    n256w4) K8S_PREFILL_ATTN_WAVES=4 step 400 bench_nodes256_w4.json python -u bench.py --nodes 256 --max-model-len 32768 --steps 3 --warmup 1
+           grep -h '"metric"' $O/bench_nodes256_w4.json | cut -c1-200; grep -ho '"decode_ms_per_step[^}]*prefill_tokens_per_decision": [0-9.]*' $O/bench_nodes256_w4.json ;;
+    tp2) STEPS=3 step 900 tp2_rehearsal.log bash tools/gpu_tp2_rehearsal.sh
+           tail -3 $O/tp2_rehearsal.log | cut -c1-700 ;;
+    gmm) for b in ${GMM_B:-4 8}; do for mm in 2 8; do
+          K8S_GEMV_MAX_M=$mm step 400 gmm_b${b}_m${mm}.json python -u bench.py --batch $b --steps 3 --warmup 1
+          grep -h '"metric"' $O/gmm_b${b}_m${mm}.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('batch $b gemv_max_m=$mm', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
+        done; done ;;
     tp8) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
            grep -h '"metric"' $O/bench_tp8sim.json | cut -c1-600 ;;
     pf8) K8S_DECODE_PREFETCH_MB=${PFMB:-24} step 300 bench_tp8sim_pf.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
