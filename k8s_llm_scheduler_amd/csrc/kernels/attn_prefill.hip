@@ -9,9 +9,9 @@
 // group instead of once per query head (8x fewer K/V bytes at Llama-3.3-70B's 8:1 GQA), and the
 // causal key range of a workgroup ends at its QT-th query instead of its 64th.  Row r of the
 // workgroup is query tile * QT + r / G, head kvh * G + r % G.
-// NW = 4 (64 rows) or 8 (128 rows): every K/V byte a workgroup stages feeds 16 NW rows of MFMA work, so at
-// long contexts -- where every workgroup streams the whole causal K/V range through L2 -- the 8-wave form
-// halves the K/V traffic per FLOP.  The host takes it when the grid still has >= 256 such workgroups.
+// NW = 4, 8 or 16 (64 / 128 / 256 rows): every K/V byte a workgroup stages feeds 16 NW rows of MFMA work, so at
+// long contexts -- where every workgroup streams the whole causal K/V range through L2 -- wider workgroups cut
+// the K/V traffic per FLOP.  The host takes the widest form whose grid still has >= 256 workgroups.
 //
 // Structure:
 //  * "swapped" QK^T: S^T = K . Q^T with v_mfma_f32_16x16x32_bf16, so each lane ends up holding
@@ -231,10 +231,11 @@ extern "C" int k8s_paged_prefill_attention(void* out, const void* q, const void*
   if (D != 128 || nq % nkv != 0) return -1;
   const int G = nq / nkv;
   const float sl2 = scale * 1.4426950408889634f;
-  // 8 waves per workgroup when that grid still covers every CU (K8S_PREFILL_ATTN_WAVES = 4 / 8 forces one form)
+  // the widest workgroup whose grid still covers every CU (K8S_PREFILL_ATTN_WAVES = 4 / 8 / 16 forces one form)
   static const int waves_env = [] { const char* e = getenv("K8S_PREFILL_ATTN_WAVES"); return e ? atoi(e) : 0; }();
-  const long long wg8 = (long long)((max_qlen + 128 / G - 1) / (128 / G)) * nkv * num_seqs;
-  const int nw = (waves_env == 4 || waves_env == 8) ? waves_env : (wg8 >= 256 && 128 / G >= 1 ? 8 : 4);
+  auto wgs = [&](int nw) { return (long long)((max_qlen + 16 * nw / G - 1) / (16 * nw / G)) * nkv * num_seqs; };
+  const int nw = (waves_env == 4 || waves_env == 8 || waves_env == 16) ? waves_env
+                 : wgs(16) >= 256 ? 16 : wgs(8) >= 256 ? 8 : 4;
 #define PF(GG, NWW)                                                                                          \
   {                                                                                                          \
     constexpr int QT = 16 * NWW / GG;                                                                        \
@@ -244,7 +245,7 @@ extern "C" int k8s_paged_prefill_attention(void* out, const void* q, const void*
         block_tables, sl2, nq, nkv, block_size, max_blocks);                                                 \
   }
 #define PFW(GG) \
-  if (nw == 8) PF(GG, 8) else PF(GG, 4)
+  if (nw == 16) PF(GG, 16) else if (nw == 8) PF(GG, 8) else PF(GG, 4)
   switch (G) {  // query heads per kv head (Llama-3.3-70B: 8; Llama-3-8B: 4)
     case 1: PFW(1) break;
     case 2: PFW(2) break;

@@ -36,6 +36,7 @@
 //  * RMS prologue (bf16): the un-normalised residual stream is the x operand; the x fragments every wave
 //    already holds give the row sums of squares (v_dot2_f32_bf16, waves 0-3 for QB0, 4-7 for QB1), and the
 //    epilogue scales by 1 / rms (the norm gamma is folded into W at load time).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -113,6 +114,8 @@ struct PgArgs {
   uint32_t kbytes;       // bytes per row of x and W
   int M, N_out, half_rows, K;
   int m_tiles, n_tiles, kt, splits, group_m, nwg;
+  int prio;              // wave priority: 0 = s_setprio 1 around every MFMA section, 1 = waves 4-7 at 1 for the
+                         // whole loop (MI355X_MICROARCH.md "static priority for the younger half"), 2 = none
   float eps;
 };
 
@@ -305,7 +308,7 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     }
     pg_sync_reads();
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+    if (a.prio == 0) __builtin_amdgcn_s_setprio(1);
     if constexpr (j == 0) {
       mma(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
       if (wr == 0) squares(std::integral_constant<int, 0>{});
@@ -317,7 +320,7 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     } else {
       mma(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
     }
-    __builtin_amdgcn_s_setprio(0);
+    if (a.prio == 0) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     pg_barrier();
   };
@@ -335,6 +338,7 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   pg_vm_wait(pg_after<GP, GQ>(0, 1, 1, 2, n));
   pg_barrier();
   if (late) __builtin_amdgcn_s_barrier();   // stagger waves 4-7 by one barrier (wave-uniform branch)
+  if (a.prio == 1 && late) __builtin_amdgcn_s_setprio(1);
 
   for (int t = 0; t < n; ++t) {
     phase(std::integral_constant<int, 0>{}, t);
@@ -343,6 +347,7 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     phase(std::integral_constant<int, 3>{}, t);
   }
   if (!late) __builtin_amdgcn_s_barrier();  // re-align the two wave groups
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(0);
   pg_vmcnt<0>();
 
   // ---- RMS: row sums of squares of this slice -> rss[token row of the tile]
@@ -539,6 +544,14 @@ PgGeom pg_geom(int M, int N_out, int K, int epi, int fp8, int cfg) {
 }
 }  // namespace
 
+// Wave-priority mode of the main loop (PgArgs::prio): K8S_PGEMM_PRIO at load, k8s_pgemm_set_prio for A/B probes.
+static int g_pg_prio = [] { const char* e = getenv("K8S_PGEMM_PRIO"); return e ? atoi(e) : 0; }();
+extern "C" int k8s_pgemm_set_prio(int mode) {
+  const int old = g_pg_prio;
+  if (mode >= 0 && mode <= 2) g_pg_prio = mode;
+  return old;
+}
+
 extern "C" int k8s_pgemm_num_configs() { return kPgNumCfgs; }
 
 extern "C" int k8s_pgemm_config(int cfg, int* bp, int* bq, int* lds_bytes) {
@@ -600,6 +613,7 @@ extern "C" int k8s_pgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.splits = splits;
   a.group_m = group_m > 0 ? group_m : 1;
   a.nwg = nwg;
+  a.prio = g_pg_prio;
   a.eps = eps;
   return fp8 ? pg_cfg<true>(a, cfg, epi, 0, stream) : pg_cfg<false>(a, cfg, epi, rms, stream);
 }

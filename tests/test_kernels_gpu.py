@@ -105,13 +105,14 @@ def test_paged_prefill_attention(nq, nkv, qlens, cached):
     _prefill_attention_case(nq, nkv, qlens, cached)
 
 
-@pytest.mark.parametrize("nq,nkv,qlens,cached", [(64, 8, [600, 45], [1200, 30]), (8, 1, [4100], [0]),
-                                                 (64, 8, [513], [3000])])
-def test_paged_prefill_attention_eight_wave(nq, nkv, qlens, cached):
-    """Grids of >= 256 eight-wave workgroups (16 queries x 8 heads each at 8:1 GQA) take the 8-wave form: long
-    contexts, several sequences, a chunk after a long cached prefix."""
+@pytest.mark.parametrize("nq,nkv,qlens,cached,waves", [(64, 8, [600, 45], [1200, 30], 16), (8, 1, [4100], [0], 8),
+                                                       (64, 8, [513], [3000], 8), (64, 8, [2100], [500], 16)])
+def test_paged_prefill_attention_wide_workgroups(nq, nkv, qlens, cached, waves):
+    """Grids of >= 256 wide workgroups (8 waves: 16 queries x 8 heads at 8:1 GQA; 16 waves: 32 queries) take the
+    widest such form: long contexts, several sequences, a chunk after a long cached prefix."""
     G = nq // nkv
-    assert -(-max(qlens) // (128 // G)) * nkv * len(qlens) >= 256
+    wgs = lambda nw: -(-max(qlens) // (16 * nw // G)) * nkv * len(qlens)   # noqa: E731
+    assert (16 if wgs(16) >= 256 else 8 if wgs(8) >= 256 else 4) == waves
     _prefill_attention_case(nq, nkv, qlens, cached)
 
 

@@ -1,4 +1,4 @@
-# Round-3 GPU steps on one MI355X, chosen by RUNS (space-separated): tests, smoke, bench, loopprobe, prof, ...
+# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
 # (any other rc) ends the script.  Logs land in gpurun_out/r3/.
 set -o pipefail
@@ -37,7 +37,7 @@ for spec in ${RUNS:-tests smoke bench}; do
            grep -E "rehearsal|passed|failed" $O/multigpu.log | cut -c1-600 ;;
     n256) step 400 bench_nodes256.json python -u bench.py --nodes 256 --max-model-len 32768 --steps 3 --warmup 1
            grep -h '"metric"' $O/bench_nodes256.json | cut -c1-200; grep -ho '"decode_ms_per_step[^}]*prefill_tokens_per_decision": [0-9.]*' $O/bench_nodes256.json ;;
-    n256w4) K8S_PREFILL_ATTN_WAVES=4 step 400 bench_nodes256_w4.json python -u bench.py --nodes 256 --max-model-len 32768 --steps 3 --warmup 1
+    n256w4) K8S_PREFILL_ATTN_WAVES=${AW:-4} step 400 bench_nodes256_w4.json python -u bench.py --nodes 256 --max-model-len 32768 --steps 3 --warmup 1
            grep -h '"metric"' $O/bench_nodes256_w4.json | cut -c1-200; grep -ho '"decode_ms_per_step[^}]*prefill_tokens_per_decision": [0-9.]*' $O/bench_nodes256_w4.json ;;
     tp2) STEPS=3 step 900 tp2_rehearsal.log bash tools/gpu_tp2_rehearsal.sh
            tail -3 $O/tp2_rehearsal.log | cut -c1-700 ;;
@@ -45,6 +45,8 @@ for spec in ${RUNS:-tests smoke bench}; do
           K8S_GEMV_MAX_M=$mm step 400 gmm_b${b}_m${mm}.json python -u bench.py --batch $b --steps 3 --warmup 1
           grep -h '"metric"' $O/gmm_b${b}_m${mm}.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('batch $b gemv_max_m=$mm', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
         done; done ;;
+    prio) step 500 pgemm_prio_probe.txt python -u tools/pgemm_prio_probe.py --m 256 2048 8192
+           grep -v amdgpu.ids $O/pgemm_prio_probe.txt ;;
     tp8) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
            grep -h '"metric"' $O/bench_tp8sim.json | cut -c1-600 ;;
     pf8) K8S_DECODE_PREFETCH_MB=${PFMB:-24} step 300 bench_tp8sim_pf.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
