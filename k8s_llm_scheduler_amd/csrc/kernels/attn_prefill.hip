@@ -11,7 +11,7 @@
 // workgroup is query tile * QT + r / G, head kvh * G + r % G.
 // NW = 4, 8 or 16 (64 / 128 / 256 rows): every K/V byte a workgroup stages feeds 16 NW rows of MFMA work, so at
 // long contexts -- where every workgroup streams the whole causal K/V range through L2 -- wider workgroups cut
-// the K/V traffic per FLOP.  The host takes the widest form whose grid still has >= 256 workgroups.
+// the K/V traffic per FLOP.  The host takes 8 waves when that grid still has >= 256 workgroups (16: opt-in).
 //
 // Structure:
 //  * "swapped" QK^T: S^T = K . Q^T with v_mfma_f32_16x16x32_bf16, so each lane ends up holding
@@ -231,11 +231,11 @@ extern "C" int k8s_paged_prefill_attention(void* out, const void* q, const void*
   if (D != 128 || nq % nkv != 0) return -1;
   const int G = nq / nkv;
   const float sl2 = scale * 1.4426950408889634f;
-  // the widest workgroup whose grid still covers every CU (K8S_PREFILL_ATTN_WAVES = 4 / 8 / 16 forces one form)
+  // 8 waves when that grid still covers every CU, else 4.  The 16-wave form measured no faster than 8 on the 256-node
+  // prompts (profiles/bench_r3_nodes256_attn_waves_ab.jsonl) and stays opt-in: K8S_PREFILL_ATTN_WAVES = 4 / 8 / 16.
   static const int waves_env = [] { const char* e = getenv("K8S_PREFILL_ATTN_WAVES"); return e ? atoi(e) : 0; }();
   auto wgs = [&](int nw) { return (long long)((max_qlen + 16 * nw / G - 1) / (16 * nw / G)) * nkv * num_seqs; };
-  const int nw = (waves_env == 4 || waves_env == 8 || waves_env == 16) ? waves_env
-                 : wgs(16) >= 256 ? 16 : wgs(8) >= 256 ? 8 : 4;
+  const int nw = (waves_env == 4 || waves_env == 8 || waves_env == 16) ? waves_env : wgs(8) >= 256 ? 8 : 4;
 #define PF(GG, NWW)                                                                                          \
   {                                                                                                          \
     constexpr int QT = 16 * NWW / GG;                                                                        \

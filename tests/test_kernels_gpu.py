@@ -2,6 +2,7 @@
 at Llama-3 shapes per TP slice."""
 
 import math
+import os
 
 import pytest
 import torch
@@ -105,15 +106,27 @@ def test_paged_prefill_attention(nq, nkv, qlens, cached):
     _prefill_attention_case(nq, nkv, qlens, cached)
 
 
-@pytest.mark.parametrize("nq,nkv,qlens,cached,waves", [(64, 8, [600, 45], [1200, 30], 16), (8, 1, [4100], [0], 8),
-                                                       (64, 8, [513], [3000], 8), (64, 8, [2100], [500], 16)])
-def test_paged_prefill_attention_wide_workgroups(nq, nkv, qlens, cached, waves):
-    """Grids of >= 256 wide workgroups (8 waves: 16 queries x 8 heads at 8:1 GQA; 16 waves: 32 queries) take the
-    widest such form: long contexts, several sequences, a chunk after a long cached prefix."""
+@pytest.mark.parametrize("nq,nkv,qlens,cached", [(64, 8, [600, 45], [1200, 30]), (8, 1, [4100], [0]),
+                                                 (64, 8, [513], [3000]), (64, 8, [2100], [500])])
+def test_paged_prefill_attention_wide_workgroups(nq, nkv, qlens, cached):
+    """Grids of >= 256 eight-wave workgroups (16 queries x 8 heads at 8:1 GQA) take the 8-wave form: long contexts,
+    several sequences, a chunk after a long cached prefix."""
     G = nq // nkv
-    wgs = lambda nw: -(-max(qlens) // (16 * nw // G)) * nkv * len(qlens)   # noqa: E731
-    assert (16 if wgs(16) >= 256 else 8 if wgs(8) >= 256 else 4) == waves
+    assert -(-max(qlens) // (128 // G)) * nkv * len(qlens) >= 256
     _prefill_attention_case(nq, nkv, qlens, cached)
+
+
+def test_paged_prefill_attention_sixteen_wave_subprocess():
+    """The opt-in 16-wave form (32 queries x 8 heads per workgroup) against the fp32 oracle, in a child process
+    (the wave count is read from K8S_PREFILL_ATTN_WAVES once per process)."""
+    import subprocess
+    import sys
+
+    code = (f"import sys; sys.path.insert(0, {os.path.dirname(os.path.abspath(__file__))!r}); import test_kernels_gpu as t; "
+            "t._prefill_attention_case(64, 8, [600, 45], [1200, 30]); t._prefill_attention_case(8, 1, [300], [20])")
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "K8S_PREFILL_ATTN_WAVES": "16"},
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
 
 
 def _prefill_attention_case(nq, nkv, qlens, cached):
