@@ -671,6 +671,8 @@ extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* k
 // profiles/bench_r3_gemv_loop_ab.txt): fp8 GEMVs -3.4 % per layer (QKV 17.6 -> 15.6 us), bf16 end to end -1.3 %.
 // K8S_GEMV_LOOP sets it at load; k8s_gemv_set_loop changes it (tests, A/B probes).
 static int g_gemv_loop = [] { const char* e = getenv("K8S_GEMV_LOOP"); return e ? atoi(e) : -1; }();
+// default for bf16 weights with the plain bf16 epilogue (QKV, O, down -- not gate/up nor the LM head)
+static int g_gemv_loop_bf16 = [] { const char* e = getenv("K8S_GEMV_LOOP_BF16"); return e ? atoi(e) : 0; }();
 extern "C" int k8s_gemv_set_loop(int wg_per_cu) {   // returns the previous setting; < -1 only reads it
   const int old = g_gemv_loop;
   if (wg_per_cu >= -1) g_gemv_loop = wg_per_cu;
@@ -706,7 +708,7 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
   const bf16_t* ri = (const bf16_t*)res_in;
   bf16_t* ro = (bf16_t*)res_out;
   const bf16_t* gw = (const bf16_t*)nw;
-  const int loop_wg = g_gemv_loop >= 0 ? g_gemv_loop : (fp8 ? 2 : 0);
+  const int loop_wg = g_gemv_loop >= 0 ? g_gemv_loop : (fp8 ? 2 : (epi == EPI_BF16 ? g_gemv_loop_bf16 : 0));
   if (loop_wg > 0 && splits == 1 && kw == 1 && mode != 1 && M <= 2 && (int)grid.x > 256 * loop_wg) {
     const int per = ((int)grid.x + 256 * loop_wg - 1) / (256 * loop_wg);   // row sets per wave
     const dim3 lgrid(((int)grid.x + per - 1) / per, 1);

@@ -15,7 +15,7 @@ and device; BASELINE allows random-init weights) or a HuggingFace safetensors ch
 loaded shard-by-shard with ``safetensors`` (no pickle).  ``weight_dtype="fp8"`` (BASELINE
 config 5) stores the four projection matrices of every layer as row-scaled OCP e4m3
 (:class:`ops.Fp8Weight`, quantized on the device right after each layer is built); embedding,
-norms and the LM head stay bf16.
+norms and the LM head stay bf16 (``K8S_FP8_LM_HEAD=1``: the LM head too).
 """
 
 from __future__ import annotations
@@ -90,6 +90,10 @@ class LlamaModel:
         if self.norm_folded:
             self.lm_head = self._fold(self.lm_head, self.norm)
             self.norm = self._ones()
+        if weight_dtype == "fp8" and os.environ.get("K8S_FP8_LM_HEAD", "0") == "1":
+            # opt-in: the LM head as row-scaled e4m3 too (half its 2.1 GB stream per decode step at TP = 1); the
+            # logits then carry e4m3 weight rounding, which sampling at temperature > 0 does not resolve
+            self.lm_head = ops.quantize_fp8(self.lm_head)
         self.kv_cache: Optional[torch.Tensor] = None
         self.block_size = 16
 

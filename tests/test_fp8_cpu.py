@@ -57,3 +57,22 @@ def test_tiny_model_fp8_tracks_bf16():
                        weight_dtype="fp8")
     out = eng.generate(["fp8 weights"], SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))[0]
     assert len(out.token_ids) == 4
+
+
+def test_fp8_lm_head_option_tracks_bf16_head(monkeypatch):
+    """K8S_FP8_LM_HEAD=1 quantizes the (norm-folded) LM head too; prefill and decode logits stay close to the
+    bf16-head fp8 model's."""
+    ids = [7, 100, 2000, 31, 32, 33, 900, 12]
+    m8 = LlamaModel(PRESETS["tiny"], device="cpu", seed=3, max_model_len=256, weight_dtype="fp8")
+    monkeypatch.setenv("K8S_FP8_LM_HEAD", "1")
+    mh = LlamaModel(PRESETS["tiny"], device="cpu", seed=3, max_model_len=256, weight_dtype="fp8")
+    assert isinstance(mh.lm_head, ops.Fp8Weight) and not isinstance(m8.lm_head, ops.Fp8Weight)
+    assert mh.weight_bytes() < m8.weight_bytes() - 0.9 * m8.lm_head.numel()   # ~1 byte per head weight saved
+    a, bt_a = _prefill(m8, ids)
+    b, bt_b = _prefill(mh, ids)
+    cos = torch.nn.functional.cosine_similarity(a.flatten().float(), b.flatten().float(), dim=0)
+    assert float(cos) > 0.995
+    ctx = torch.tensor([len(ids) + 1], dtype=torch.int32)
+    da = m8.forward_decode(torch.tensor([77], dtype=torch.int32), ctx, bt_a, 256)
+    db = mh.forward_decode(torch.tensor([77], dtype=torch.int32), ctx, bt_b, 256)
+    assert float(torch.nn.functional.cosine_similarity(da.flatten().float(), db.flatten().float(), dim=0)) > 0.995

@@ -1,4 +1,4 @@
-# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof.
+# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
 # (any other rc) ends the script.  Logs land in gpurun_out/r3/.
 set -o pipefail
@@ -47,12 +47,22 @@ for spec in ${RUNS:-tests smoke bench}; do
         done; done ;;
     prio) step 500 pgemm_prio_probe.txt python -u tools/pgemm_prio_probe.py --m 256 2048 8192
            grep -v amdgpu.ids $O/pgemm_prio_probe.txt ;;
+    fp8head) for i in 1 2; do for h in 0 1; do
+          K8S_FP8_LM_HEAD=$h step 400 fp8head${h}_$i.json python -u bench.py --dtype fp8 --steps 6 --warmup 2
+          grep -h '"metric"' $O/fp8head${h}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('fp8 lm_head=$h', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
+        done; done ;;
+    loopbf) for i in 1 2; do for lw in 0 2 4; do
+          K8S_GEMV_LOOP_BF16=$lw step 400 loopbf${lw}_$i.json python -u bench.py --steps 6 --warmup 2
+          grep -h '"metric"' $O/loopbf${lw}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('bf16 plain-epilogue loop=$lw', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
+        done; done ;;
     tp8) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
            grep -h '"metric"' $O/bench_tp8sim.json | cut -c1-600 ;;
     pf8) K8S_DECODE_PREFETCH_MB=${PFMB:-24} step 300 bench_tp8sim_pf.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
            grep -h '"metric"' $O/bench_tp8sim_pf.json | cut -c1-600 ;;
     loopprobe) step 400 gemv_loop_probe.txt python -u tools/gemv_loop_probe.py --tp 1 4 8
            cat $O/gemv_loop_probe.txt | grep -v amdgpu.ids ;;
+    proffp8) bash tools/gpu_prof.sh tp1_fp8 "--dtype fp8" > $O/proffp8.log 2>&1 || { tail -20 $O/proffp8.log; exit 1; }
+          head -20 gpurun_out/rocprof_70b_tp1_fp8_kernels.txt; cat gpurun_out/lastfwd_tp1_fp8.txt ;;
     prof) bash tools/gpu_prof.sh tp1_default "" > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
           head -24 gpurun_out/rocprof_70b_tp1_default_kernels.txt ;;
   esac
