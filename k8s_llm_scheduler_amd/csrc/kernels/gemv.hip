@@ -667,12 +667,14 @@ extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* k
 // wscale != null: W is fp8 (OCP e4m3, one fp32 scale per weight row); K must be a multiple of 16.
 // mode: 0 plain, 1 norm weight nw applied in the prologue, 2 norm weight folded into W (nw unused)
 // Row-set loop (LOOP): workgroups per CU the grid is cut to (0 = one row set per wave; -1 = default: 2 for fp8
-// weights, off for bf16).  Measured on the 70B decode (profiles/gemv_loop_probe_r3.txt, bench A/B in
-// profiles/bench_r3_gemv_loop_ab.txt): fp8 GEMVs -3.4 % per layer (QKV 17.6 -> 15.6 us), bf16 end to end -1.3 %.
+// weights; for bf16 weights 2 on the plain bf16 epilogue (QKV, O, down) and off for SwiGLU / fp32 (gate/up, LM
+// head)).  Measured on the 70B decode (profiles/gemv_loop_probe_r3.txt, bench A/B in
+// profiles/bench_r3_gemv_loop_ab.txt): fp8 decode -0.6 %; bf16 with the loop everywhere +1.3 % (slower), on the
+// plain-epilogue projections only -0.3 %.
 // K8S_GEMV_LOOP sets it at load; k8s_gemv_set_loop changes it (tests, A/B probes).
 static int g_gemv_loop = [] { const char* e = getenv("K8S_GEMV_LOOP"); return e ? atoi(e) : -1; }();
 // default for bf16 weights with the plain bf16 epilogue (QKV, O, down -- not gate/up nor the LM head)
-static int g_gemv_loop_bf16 = [] { const char* e = getenv("K8S_GEMV_LOOP_BF16"); return e ? atoi(e) : 0; }();
+static int g_gemv_loop_bf16 = [] { const char* e = getenv("K8S_GEMV_LOOP_BF16"); return e ? atoi(e) : 2; }();
 extern "C" int k8s_gemv_set_loop(int wg_per_cu) {   // returns the previous setting; < -1 only reads it
   const int old = g_gemv_loop;
   if (wg_per_cu >= -1) g_gemv_loop = wg_per_cu;
