@@ -36,6 +36,7 @@ int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, c
                                 int max_qlen, int nq, int nkv, int D, int block_size, int max_blocks, hipStream_t s);
 void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* ks_out, int* splits_out);
 int k8s_gemv_set_loop(int wg_per_cu);
+int k8s_gemv_set_wide(int on);
 int k8s_pgemm_set_prio(int mode);
 int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out,
                  int K, int epi, const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
@@ -158,6 +159,7 @@ PYBIND11_MODULE(_C, m) {
     }
   }, py::arg("event"), py::arg("timeout_s"));
   m.def("pgemm_set_prio", [](int mode) { return k8s_pgemm_set_prio(mode); });
+  m.def("gemv_set_wide", [](int on) { return k8s_gemv_set_wide(on); });
   m.def("gemv_set_loop", [](int wg) { return k8s_gemv_set_loop(wg); });
   m.def("gemv_plan", [](int M, int N, int K, int epi, int mode) {
     int ks, sp;

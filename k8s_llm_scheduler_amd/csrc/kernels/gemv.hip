@@ -673,6 +673,12 @@ extern "C" void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* k
 // plain-epilogue projections only -0.3 %.
 // K8S_GEMV_LOOP sets it at load; k8s_gemv_set_loop changes it (tests, A/B probes).
 static int g_gemv_loop = [] { const char* e = getenv("K8S_GEMV_LOOP"); return e ? atoi(e) : -1; }();
+static int g_gemv_wide = [] { const char* e = getenv("K8S_GEMV_WIDE"); return e ? atoi(e) : 1; }();
+extern "C" int k8s_gemv_set_wide(int on) {
+  const int old = g_gemv_wide;
+  if (on >= 0) g_gemv_wide = on;
+  return old;
+}
 // default for bf16 weights with the plain bf16 epilogue (QKV, O, down -- not gate/up nor the LM head)
 static int g_gemv_loop_bf16 = [] { const char* e = getenv("K8S_GEMV_LOOP_BF16"); return e ? atoi(e) : 2; }();
 extern "C" int k8s_gemv_set_loop(int wg_per_cu) {   // returns the previous setting; < -1 only reads it
@@ -712,6 +718,27 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
   const bf16_t* gw = (const bf16_t*)nw;
   const int loop_wg = g_gemv_loop >= 0 ? g_gemv_loop : (fp8 ? 2 : (epi == EPI_BF16 ? g_gemv_loop_bf16 : 0));
   if (loop_wg > 0 && splits == 1 && kw == 1 && mode != 1 && M <= 2 && (int)grid.x > 256 * loop_wg) {
+    // wide: 8-wave workgroups for the plain bf16-epilogue projections whose x slice takes >= 32 KiB of LDS (the
+    // down projection, K = 28672: 56 KiB): LDS, not waves, bounds those at 2 workgroups per CU, so twice the waves
+    // per workgroup put twice the weight loads in flight per CU (K8S_GEMV_WIDE = 0 turns it off)
+    const bool wide = g_gemv_wide && mode == 0 && epi == EPI_BF16 && (long long)M * K * 2 >= 32768;
+    if (wide) {
+      const int wgs = (N_out + 8 * rpw - 1) / (8 * rpw);
+      {
+        const int per = (wgs + 256 * loop_wg - 1) / (256 * loop_wg);   // >= 1
+        const dim3 wgrid((wgs + per - 1) / per, 1);
+#define GW(MM, RR, F8)                                                                                              \
+  gemv_kernel<MM, RR, EPI_BF16, 0, F8, 1, 512, false, true><<<wgrid, 512, lds, stream>>>(                           \
+      out, nullptr, xx, ww, N_out, K, ks, half_rows, ri, ro, gw, eps, wscale, GemvAr{})
+#define GW2(MM, RR) \
+  if (fp8) { GW(MM, RR, true); } else { GW(MM, RR, false); }
+        if (M == 1) { if (rpw == 2) { GW2(1, 2) } else { GW2(1, 1) } }
+        else { if (rpw == 2) { GW2(2, 2) } else { GW2(2, 1) } }
+#undef GW2
+#undef GW
+        return (int)hipGetLastError();
+      }
+    }
     const int per = ((int)grid.x + 256 * loop_wg - 1) / (256 * loop_wg);   // row sets per wave
     const dim3 lgrid(((int)grid.x + per - 1) / per, 1);
 #define GL(MM, RR, EE, F8, NN)                                                                                     \

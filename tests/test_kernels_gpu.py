@@ -615,3 +615,31 @@ def test_gemv_row_set_loop_matches_single(M, epi, folded, fp8):
     y32 = h @ wd.T
     want = torch.nn.functional.silu(y32[:, :N]) * y32[:, N:] if epi == 2 else y32
     close(base, want, 3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_gemv_wide_loop_large_k_matches_single(M, fp8):
+    """The 8-wave row-set loop of the large-K plain projections (down: x takes >= 32 KiB of LDS) gives the bits of
+    the 4-wave loop and of one row set per wave, and matches the fp32 oracle."""
+    K, N = 28672, 4103
+    torch.manual_seed(11 * M + fp8)
+    x = rnd(M, K)
+    w = rnd(N, K, scale=0.05)
+    ww = ops.quantize_fp8(w) if fp8 else w
+    wd = ref.dequant_fp8(ww.q.cpu(), ww.scale.cpu()) if fp8 else w.cpu().float()
+    old_loop, old_wide = ops.native().gemv_set_loop(0), ops.native().gemv_set_wide(1)
+    try:
+        base = ops._gemv(x, ww, ops.EPI_BF16, torch.bfloat16)
+        outs = []
+        for lp, wide in ((1, 1), (2, 1), (2, 0)):
+            ops.native().gemv_set_loop(lp)
+            ops.native().gemv_set_wide(wide)
+            outs.append(ops._gemv(x, ww, ops.EPI_BF16, torch.bfloat16))
+    finally:
+        ops.native().gemv_set_loop(old_loop)
+        ops.native().gemv_set_wide(old_wide)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, base)
+    close(base, x.cpu().float() @ wd.T, 3e-2)
