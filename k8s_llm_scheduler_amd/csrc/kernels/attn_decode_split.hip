@@ -23,8 +23,6 @@
 // At most 64 chunks (contexts up to 4096 tokens; longer ones use attn_decode_fused.hip).
 // Workspace: part [B, nkv, pmax, G*D + 2*G] f32; counters [B * nkv] u32, zero before the first
 // launch and restored to zero by every launch.
-#include <cstdlib>
-
 #include "common.h"
 
 namespace k8sllm {
@@ -77,7 +75,7 @@ __device__ __forceinline__ void signal_done(uint32_t* done, int lane) {
 // The split-attention work of workgroup (chunk c, kv head kvh, sequence b).  SIGNAL: the workgroup
 // that writes a pair's final output publishes it (store_pair_sc1 + signal_done on `done`), for the
 // O-projection workgroups of decode_split_oproj_kernel.
-template <int G, bool SIGNAL, int QBW = 64>
+template <int G, bool SIGNAL>
 __device__ __forceinline__ void split_body(
     bf16_t* __restrict__ out, float* __restrict__ part, uint32_t* __restrict__ counters,
     const bf16_t* __restrict__ qkv, const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache,
@@ -334,9 +332,7 @@ __device__ __forceinline__ void split_body(
   constexpr int LPH = 64 / G, DPL = D / LPH;  // lanes per head, d per lane (DPL = 2G)
   constexpr int VW = (DPL % 4 == 0) ? 4 : 2;  // floats per load
   constexpr int NV = DPL / VW;                // loads per chunk
-  // chunks merged per round trip: QBW / NV (QBW = 64: 16 at G = 8, so contexts <= 1024 merge in ONE round trip of
-  // L2 loads; the merging wave has the register file to itself -- one wave per workgroup, a few dozen workgroups)
-  constexpr int QB = (QBW / NV) > 0 ? QBW / NV : 1;
+  constexpr int QB = (32 / NV) > 0 ? 32 / NV : 1;
   const int h = lane / LPH, d0 = (lane % LPH) * DPL;
   float buf[QB][DPL];
   auto load_batch = [&](int q0) {
@@ -405,13 +401,13 @@ __device__ __forceinline__ void split_body(
   TR(7);
 }
 
-template <int G, int QBW>
+template <int G>
 __global__ void __launch_bounds__(64) decode_split_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part, uint32_t* __restrict__ counters,
     const bf16_t* __restrict__ qkv, const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache,
     bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
     float scale, int max_blocks, int nkv, int pmax) {
-  split_body<G, false, QBW>(out, part, counters, qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale,
+  split_body<G, false>(out, part, counters, qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale,
                        max_blocks, nkv, pmax, blockIdx.x, blockIdx.y, blockIdx.z, nullptr);
 }
 
@@ -576,13 +572,10 @@ extern "C" int k8s_decode_attention_split(void* out, void* part, uint32_t* count
   const long long G = nq / nkv;
   if ((long long)pmax * (G * 128 + 2 * G) * 4 > 0x7fffffffLL) return -5;  // 32-bit merge offsets per pair
   dim3 grid(pmax, nkv, B);
-  // K8S_ATTN_MERGE_WIDE = 0: the round-2 merge (32 loads per round trip) -- A/B only
-  static const int wide_env = [] { const char* e = getenv("K8S_ATTN_MERGE_WIDE"); return e ? atoi(e) : 1; }();
-#define L1(GG, QW)                                                                                             \
-  decode_split_kernel<GG, QW><<<grid, 64, 0, stream>>>((bf16_t*)out, (float*)part, counters, (const bf16_t*)qkv, \
-                                                       cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, block_tables, \
-                                                       context_lens, scale, max_blocks, nkv, pmax)
-#define L(GG) if (wide_env) { L1(GG, 64); } else { L1(GG, 32); }
+#define L(GG)                                                                                                 \
+  decode_split_kernel<GG><<<grid, 64, 0, stream>>>((bf16_t*)out, (float*)part, counters, (const bf16_t*)qkv, \
+                                                   cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, block_tables, \
+                                                   context_lens, scale, max_blocks, nkv, pmax)
   switch (G) {
     case 1: L(1); break;
     case 2: L(2); break;
@@ -592,6 +585,5 @@ extern "C" int k8s_decode_attention_split(void* out, void* part, uint32_t* count
     default: return -2;
   }
 #undef L
-#undef L1
   return (int)hipGetLastError();
 }

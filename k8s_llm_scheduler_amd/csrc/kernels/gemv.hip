@@ -679,6 +679,12 @@ extern "C" int k8s_gemv_set_wide(int on) {
   if (on >= 0) g_gemv_wide = on;
   return old;
 }
+// bf16 SwiGLU (gate/up) GEMVs take the loop (2 workgroups per CU) when their one-row-set grid has at most this many
+// workgroups, i.e. at TP > 1 shapes (K8S_GEMV_LOOP_SWIGLU_MAX; TP = 1 gate/up measured no faster with it)
+static int g_gemv_loop_swiglu_max = [] {
+  const char* e = getenv("K8S_GEMV_LOOP_SWIGLU_MAX");
+  return e ? atoi(e) : 0;
+}();
 // default for bf16 weights with the plain bf16 epilogue (QKV, O, down -- not gate/up nor the LM head)
 static int g_gemv_loop_bf16 = [] { const char* e = getenv("K8S_GEMV_LOOP_BF16"); return e ? atoi(e) : 2; }();
 extern "C" int k8s_gemv_set_loop(int wg_per_cu) {   // returns the previous setting; < -1 only reads it
@@ -716,7 +722,9 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
   const bf16_t* ri = (const bf16_t*)res_in;
   bf16_t* ro = (bf16_t*)res_out;
   const bf16_t* gw = (const bf16_t*)nw;
-  const int loop_wg = g_gemv_loop >= 0 ? g_gemv_loop : (fp8 ? 2 : (epi == EPI_BF16 ? g_gemv_loop_bf16 : 0));
+  const bool swiglu_loop = epi == EPI_SWIGLU && (int)grid.x <= g_gemv_loop_swiglu_max;
+  const int loop_wg = g_gemv_loop >= 0 ? g_gemv_loop
+                                       : (fp8 ? 2 : (epi == EPI_BF16 ? g_gemv_loop_bf16 : (swiglu_loop ? 2 : 0)));
   if (loop_wg > 0 && splits == 1 && kw == 1 && mode != 1 && M <= 2 && (int)grid.x > 256 * loop_wg) {
     // wide: 8-wave workgroups for the plain bf16-epilogue projections whose x slice takes >= 32 KiB of LDS (the
     // down projection, K = 28672: 56 KiB): LDS, not waves, bounds those at 2 workgroups per CU, so twice the waves

@@ -1,4 +1,4 @@
-# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge.
+# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
 # (any other rc) ends the script.  Logs land in gpurun_out/r3/.
 set -o pipefail
@@ -62,6 +62,10 @@ for spec in ${RUNS:-tests smoke bench}; do
     merge) for i in 1 2; do for mw in 0 1; do
           K8S_ATTN_MERGE_WIDE=$mw step 300 merge${mw}_$i.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
           grep -h '"metric"' $O/merge${mw}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('tp8sim merge_wide=$mw', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
+        done; done ;;
+    swl) for i in 1 2; do for sm in 0 2048; do
+          K8S_GEMV_LOOP_SWIGLU_MAX=$sm step 300 swl${sm}_$i.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
+          grep -h '"metric"' $O/swl${sm}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('tp8sim swiglu_loop_max=$sm', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
         done; done ;;
     tp8) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
            grep -h '"metric"' $O/bench_tp8sim.json | cut -c1-600 ;;
