@@ -680,10 +680,11 @@ extern "C" int k8s_gemv_set_wide(int on) {
   return old;
 }
 // bf16 SwiGLU (gate/up) GEMVs take the loop (2 workgroups per CU) when their one-row-set grid has at most this many
-// workgroups, i.e. at TP > 1 shapes (K8S_GEMV_LOOP_SWIGLU_MAX; TP = 1 gate/up measured no faster with it)
+// workgroups: TP = 4 / 8 shapes (K8S_GEMV_LOOP_SWIGLU_MAX).  At one TP = 8 rank's shapes decode 4.554 -> 4.466
+// ms/token (profiles/bench_r3_gemv_loop_ab.txt); at TP = 1 (7168 workgroups) the loop measured slower.
 static int g_gemv_loop_swiglu_max = [] {
   const char* e = getenv("K8S_GEMV_LOOP_SWIGLU_MAX");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : 2048;
 }();
 // default for bf16 weights with the plain bf16 epilogue (QKV, O, down -- not gate/up nor the LM head)
 static int g_gemv_loop_bf16 = [] { const char* e = getenv("K8S_GEMV_LOOP_BF16"); return e ? atoi(e) : 2; }();
