@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
   constexpr int EPC = FP8 ? 16 : 8;  // weights per 16-byte chunk
   constexpr int WB = FP8 ? 1 : 2;    // bytes per weight
   static_assert(!AR || (EPI == EPI_BF16 && RPW == 2 && KW == 1 && NORM == 0), "fused all-reduce: plain 2-row waves");
-  static_assert(!LOOP || (!AR && KW == 1 && NORM != 1), "row-set loop: one wave per row set, no prologue norm");
+  static_assert(!LOOP || (KW == 1 && NORM != 1), "row-set loop: one wave per row set, no prologue norm");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u32x4* xs = reinterpret_cast<u32x4*>(smem);  // [M][KS/8]
   constexpr int NWV = NT / 64;  // waves per workgroup; NWV / KW row sets
@@ -137,7 +137,11 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
 
   constexpr int NR = (EPI == EPI_SWIGLU) ? 2 * RPW : RPW;  // weight rows per wave
   constexpr int U = (NR >= 4) ? 2 : ((NR >= 2) ? 4 : 8);  // chunks per lane in flight per row
-  const int r0 = (blockIdx.x * (NWV / KW) + wid / KW) * RPW;  // first output row of this wave
+  // LOOP: lper row sets per wave; workgroup b owns the contiguous row sets [b NWV lper, (b + 1) NWV lper), its wave w
+  // the sets b NWV lper + w + NWV j (contiguous bands keep the fused all-reduce's arrival groups contiguous)
+  int lper = 1;
+  if constexpr (LOOP) lper = ((N_out + RPW - 1) / RPW + (int)gridDim.x * NWV - 1) / ((int)gridDim.x * NWV);
+  const int r0 = ((int)blockIdx.x * (NWV / KW) * lper + wid / KW) * RPW;  // first output row of this wave
   const bool active = r0 < N_out;
   const int kpart = wid % KW;                                // this wave's share of the K chunks
   const int per = (nch + KW - 1) / KW;
@@ -336,11 +340,10 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
 
   if constexpr (LOOP) {
-    const int S = (int)gridDim.x * NWV;                 // row sets per sweep of the grid
     const int nsets = (N_out + RPW - 1) / RPW;
+    const int set_end = min(nsets, ((int)blockIdx.x + 1) * NWV * lper);
     const int bpr = (nch + 64 * U - 1) / (64 * U);      // weight blocks per row set
-    int set = (int)blockIdx.x * NWV + wid;
-    if (set >= nsets) return;
+    int set = (int)blockIdx.x * NWV * lper + wid;
     if (NORM == 2) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
@@ -351,7 +354,7 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
       }
     }
     const char* nrow[NR];
-    for (int j = 0;;) {
+    for (int j = 0; set < set_end;) {
       u32x4 cur[U][NR];
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -361,9 +364,9 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
       int nj = j + 1, nset = set;
       if (nj == bpr) {
         nj = 0;
-        nset = set + S;
+        nset = set + NWV;
       }
-      if (nset < nsets) {
+      if (nset < set_end) {
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
           const int n = min(nset * RPW + r, N_out - 1);
@@ -405,7 +408,21 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
             if (NORM == 2) v *= inv[m];
             acc[r][m] = v;
           }
-        if (lane == 0) {
+        if constexpr (AR) {   // push this row set's partial words to every peer (see the non-loop push below)
+          typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+          const uint32_t e = ar_state[0];
+          if (lane < ar.world) {
+            const int rr = set * RPW, nwd = N_out >> 1;
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                ar.base[lane] + ((long long)(e & 1) * ar.world + ar.rank) * ar.row_bytes, 0, (int)ar.row_bytes, 0x00020000);
+            const float s0 = FP8 ? wscale[rr] : 1.f, s1 = FP8 ? wscale[rr + 1] : 1.f;
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              const u32x2 g = u32x2{pack_bf2(acc[0][m] * s0, acc[1][m] * s1), e};
+              __builtin_amdgcn_raw_buffer_store_b64(g, rs, (m * nwd + (rr >> 1)) * 8, 0, GAR_SYS);
+            }
+          }
+        } else if (lane == 0) {
 #pragma unroll
           for (int r = 0; r < RPW; ++r) {
             const int n = set * RPW + r;
@@ -429,12 +446,13 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
         for (int r = 0; r < NR; ++r)
 #pragma unroll
           for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
-        if (nset >= nsets) return;
         set = nset;
       }
       j = nj;
     }
+    if constexpr (!AR) return;
   }
+  if constexpr (!LOOP) {
   for (int c = cb + lane; active && c < ce; c += 64 * U) {
     u32x4 cur[U][NR];
 #pragma unroll
@@ -472,14 +490,16 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
   for (int r = 0; r < NR; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+  }
 
   if constexpr (AR) {
     typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
     const uint32_t e = ar_state[0];
     const int W = ar.world, nwd = N_out >> 1;  // LL words per input row
     const long long par = (long long)(e & 1) * W;
-    // 1. push: lane t < W sends this wave's M words to rank t (row `rank` of its parity-(e & 1) slot)
-    if (active && lane < W) {
+    // 1. push: lane t < W sends this wave's M words to rank t (row `rank` of its parity-(e & 1) slot); the loop
+    // variant pushed every row set's words as it finished them
+    if (!LOOP && active && lane < W) {
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(ar.base[lane] + (par + ar.rank) * ar.row_bytes, 0,
                                                         (int)ar.row_bytes, 0x00020000);
       const float s0 = FP8 ? wscale[r0] : 1.f, s1 = FP8 ? wscale[r0 + 1] : 1.f;
@@ -504,7 +524,7 @@ __global__ void __launch_bounds__(NT) gemv_kernel(void* __restrict__ out, float*
       __hip_atomic_store(ar.epochs + grp, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // 3. words [w0, w1) of every input row, summed over the W sources in rank order, + residual, one rounding
-    constexpr int ROWS_WG = (NT / 64) * RPW;
+    const int ROWS_WG = (NT / 64) * RPW * lper;
     const int w0 = g0 * ROWS_WG / 2, w1 = min(nwd, gn * ROWS_WG / 2), nw = w1 - w0;
     const char* mine = ar.base[ar.rank] + par * ar.row_bytes;
     const uint32_t* res = reinterpret_cast<const uint32_t*>(ar.res);
@@ -869,7 +889,12 @@ extern "C" int k8s_gemv_allreduce(void* out, const void* x, const void* W, const
   if (M < 1 || M > 8 || K % 16 != 0 || N_out <= 0 || world < 2 || world > GAR_MAX_WORLD || rank < 0 || rank >= world)
     return -1;
   if (N_out % ROWS_WG != 0 || (long long)M * K * 2 > 65536 || (long long)M * N_out * 4 > row_bytes) return -5;
-  const int nwg = N_out / ROWS_WG;
+  // row-set loop (K8S_GEMV_LOOP_AR = workgroups per CU, 0 = one row set per wave): each workgroup streams a
+  // contiguous band of row sets and pushes each set's words as it finishes it
+  static const int loop_ar = [] { const char* e = getenv("K8S_GEMV_LOOP_AR"); return e ? atoi(e) : 0; }();
+  const int nwg1 = N_out / ROWS_WG;
+  const int per = (loop_ar > 0 && M <= 2 && nwg1 > 256 * loop_ar) ? (nwg1 + 256 * loop_ar - 1) / (256 * loop_ar) : 1;
+  const int nwg = (nwg1 + per - 1) / per;
   const int group = (nwg + 31) / 32;  // ~32 arrival groups: one waiting workgroup per group
   if ((nwg + group - 1) / group > GAR_MAX_GROUPS) return -5;
   GemvAr a;
@@ -880,11 +905,18 @@ extern "C" int k8s_gemv_allreduce(void* out, const void* x, const void* W, const
   const bool fp8 = wscale != nullptr;
   const size_t lds = (size_t)M * K * 2;
   const bf16_t* xx = static_cast<const bf16_t*>(x);
-#define GAR(MM)                                                                                                     \
-  if (fp8) gemv_kernel<MM, 2, EPI_BF16, 0, true, 1, 256, true><<<nwg, 256, lds, stream>>>(                          \
+#define GAR1(MM, LP)                                                                                                \
+  if (fp8) gemv_kernel<MM, 2, EPI_BF16, 0, true, 1, 256, true, LP><<<nwg, 256, lds, stream>>>(                      \
       out, nullptr, xx, W, N_out, K, K, 0, nullptr, nullptr, nullptr, 0.f, wscale, a);                               \
-  else gemv_kernel<MM, 2, EPI_BF16, 0, false, 1, 256, true><<<nwg, 256, lds, stream>>>(                             \
+  else gemv_kernel<MM, 2, EPI_BF16, 0, false, 1, 256, true, LP><<<nwg, 256, lds, stream>>>(                         \
       out, nullptr, xx, W, N_out, K, K, 0, nullptr, nullptr, nullptr, 0.f, wscale, a)
+#define GAR(MM)                                   \
+  if constexpr (MM <= 2) {                        \
+    if (per > 1) { GAR1(MM, true); }              \
+    else { GAR1(MM, false); }                     \
+  } else {                                        \
+    GAR1(MM, false);                              \
+  }
   switch (M) {
     case 1: GAR(1); break;
     case 2: GAR(2); break;
@@ -896,6 +928,7 @@ extern "C" int k8s_gemv_allreduce(void* out, const void* x, const void* W, const
     case 8: GAR(8); break;
   }
 #undef GAR
+#undef GAR1
   return (int)hipGetLastError();
 }
 

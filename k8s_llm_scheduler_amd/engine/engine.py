@@ -106,16 +106,25 @@ def ngram_draft(seq: Sequence[int], k: int, n_max: int = 3) -> List[int]:
 
 class _HostStage:
     """Ring of pinned host slots for small host -> device copies (LLMEngine._dev).  A slot is reused only once the copy
-    that last used it has executed (its event); if the device is so far behind that the next slot is still pending,
-    the engine is stalled and EngineStalled is raised instead of waiting.  Larger tensors take a one-off pinned
-    buffer."""
+    that last used it has executed (its event).  When the device is that far behind -- a step that admits many
+    requests behind a long prefill enqueues hundreds of copies -- the ring waits for the slot with a bounded event wait
+    that releases the GIL (``wait_limit()``: the engine's call deadline / watchdog, as for every device wait) and
+    raises EngineStalled only when that expires.  Larger tensors take a one-off pinned buffer."""
 
-    SLOTS, SLOT_BYTES = 64, 256 << 10
+    SLOTS, SLOT_BYTES = 512, 256 << 10
 
-    def __init__(self):
+    def __init__(self, wait_limit=None):
         self.buf = torch.empty(self.SLOTS * self.SLOT_BYTES, dtype=torch.uint8, pin_memory=True)
         self.events: List[Optional[torch.cuda.Event]] = [None] * self.SLOTS
         self.next = 0
+        self.wait_limit = wait_limit     # () -> absolute time.monotonic() limit, or None (no limit set: 60 s)
+
+    def _slot_free(self, ev: torch.cuda.Event) -> bool:
+        if ev.query():
+            return True
+        lim = self.wait_limit() if self.wait_limit is not None else None
+        budget = (lim - time.monotonic()) if lim is not None else 60.0
+        return bool(ops.native().event_wait(ev.cuda_event, max(0.0, budget)))
 
     def to_device(self, t: torch.Tensor, device) -> torch.Tensor:
         t = t.contiguous()
@@ -124,9 +133,9 @@ class _HostStage:
             return t.pin_memory().to(device, non_blocking=True)
         i = self.next
         ev = self.events[i]
-        if ev is not None and not ev.query():
+        if ev is not None and not self._slot_free(ev):
             raise EngineStalled("host staging ring full: the device has not run the last "
-                                f"{self.SLOTS} host-to-device copies")
+                                f"{self.SLOTS} host-to-device copies within the deadline")
         self.next = (i + 1) % self.SLOTS
         view = self.buf[i * self.SLOT_BYTES:i * self.SLOT_BYTES + n]
         view.copy_(t.view(-1).view(torch.uint8))
@@ -367,7 +376,7 @@ class LLMEngine:
         if not self.gpu:
             return t
         if self._stage is None:
-            self._stage = _HostStage()
+            self._stage = _HostStage(self._wait_limit)
         return self._stage.to_device(t, self.device)
 
     def _poll_event(self, ev=None) -> bool:

@@ -206,3 +206,17 @@ def test_engine_gpu_mixed_steps_match_split_path():
     # bf16 GPU numerics: the decode rows of a mixed step run the prefill kernels; sampled tokens agree
     same = sum(a == b for x, y in zip(mixed, split) for a, b in zip(x, y))
     assert same >= 0.9 * 60, (mixed, split)
+
+
+def test_engine_gpu_many_admissions_wrap_the_staging_ring(monkeypatch):
+    """A step that admits many requests enqueues more host-to-device copies than the pinned staging ring has slots
+    (64 requests, an 8-slot ring here): the ring must wait (bounded) for the device to free a slot, not fail the step
+    -- the failure mode `bench.py --batch 64` hit when the ring raised on the first pending slot."""
+    from k8s_llm_scheduler_amd.engine import engine as engine_mod
+
+    monkeypatch.setattr(engine_mod._HostStage, "SLOTS", 8)
+    eng = build_engine("tiny", device="cuda:0", max_batch=64, num_blocks=1024, max_model_len=512, seed=3)
+    prompts = [f"pod-{i} requests {i % 7} cpus on node {i % 5}" for i in range(64)]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))
+    assert [len(o.token_ids) for o in outs] == [4] * 64
+    assert eng.stats["stalls"] == 0

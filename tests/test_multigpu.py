@@ -350,6 +350,17 @@ def test_tp_rehearsal_ranks_share_one_gpu(world):
               f"(kv scale {res[0]['split_kv_scale']:.3g}), overlapped chunks {res[0]['overlap_chunks']}")
 
 
+def test_tp_rehearsal_fused_ar_row_set_loop():
+    """The fused GEMV all-reduce with the row-set loop (K8S_GEMV_LOOP_AR: each workgroup streams a contiguous band
+    of row sets and pushes every set's words as it finishes it): the collective checks, including the fused path's
+    bit-exact comparison against GEMV + all-reduce, at 4 ranks on one GPU."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = run_ranks(_rehearsal_rank, 4, env={"K8S_TP_BACKEND": "gloo", "K8S_TP_COMM": "xgmi", "K8S_TEST_MODEL": "0",
+                                             "K8S_GEMV_LOOP_AR": "1"}, timeout_s=300)
+    _assert_model(res, 4)
+
+
 def _multi_gpu_rank(rank, world):
     import torch.distributed as dist
 

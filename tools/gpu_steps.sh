@@ -1,4 +1,4 @@
-# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl.
+# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
 # (any other rc) ends the script.  Logs land in gpurun_out/r3/.
 set -o pipefail
@@ -66,6 +66,18 @@ for spec in ${RUNS:-tests smoke bench}; do
     swl) for i in 1 2; do for sm in 0 2048; do
           K8S_GEMV_LOOP_SWIGLU_MAX=$sm step 300 swl${sm}_$i.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
           grep -h '"metric"' $O/swl${sm}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('tp8sim swiglu_loop_max=$sm', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
+        done; done ;;
+    b8b) step 300 bench_8b.json python -u bench.py --preset llama-3-8b --steps 10 --warmup 2
+           grep -h '"metric"' $O/bench_8b.json | cut -c1-300 ;;
+    b64) step 400 bench_b64.json python -u bench.py --batch 64 --steps 2 --warmup 1
+           grep -h '"metric"' $O/bench_b64.json | cut -c1-300 ;;
+    tp8b64) step 400 bench_tp8sim_b64.json python -u bench.py --simulate-tp 8 --batch 64 --steps 3 --warmup 1
+           grep -h '"metric"' $O/bench_tp8sim_b64.json | cut -c1-300 ;;
+    tp8plain) K8S_GEMV_LOOP_BF16=0 step 300 bench_tp8sim_noplainloop.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
+           grep -h '"metric"' $O/bench_tp8sim_noplainloop.json | cut -c1-200; grep -ho '"decode_ms_per_step": [0-9.]*' $O/bench_tp8sim_noplainloop.json ;;
+    ab8b) for i in 1 2; do for lw in 0 2; do
+          K8S_GEMV_LOOP_BF16=$lw step 300 ab8b_loop${lw}_$i.json python -u bench.py --preset llama-3-8b --steps 10 --warmup 2
+          grep -h '"metric"' $O/ab8b_loop${lw}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('8b plain loop=$lw', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
         done; done ;;
     tp8) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
            grep -h '"metric"' $O/bench_tp8sim.json | cut -c1-600 ;;
