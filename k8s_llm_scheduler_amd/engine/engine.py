@@ -1121,6 +1121,12 @@ class LLMEngine:
         tr = self.recovery_trace if self._trace_steps else None
         if tr is not None:
             tr.append((time.monotonic(), f"decode: {steps} steps, graph {graph is not None}"))
+        # decode_time on the GPU: from an event behind the work already queued (a prefill this step did not wait
+        # for) to one after the last replay -- host time would charge that prefill to the decode
+        ev_t = None
+        if self.gpu:
+            ev_t = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev_t[0].record()
         for i in range(steps):
             if graph is not None:
                 graph.replay()
@@ -1152,13 +1158,16 @@ class LLMEngine:
             if stop == 2:
                 early = False
         self.stats["decode_steps"] += ran
+        if ev_t is not None:
+            ev_t[1].record()
         tp = self.model.tp
         tp.snapshot_health()             # rides on the bounded wait below
         if tr is not None:
             tr.append((time.monotonic(), "decode: fetch"))
         hist, nsteps = self._fetch(self.s_hist[:B], self.s_steps[:B], what="decode")
         tp.check_health()                # a failed collective raises into the decision service
-        self.stats["decode_time"] += time.perf_counter() - t0
+        self.stats["decode_time"] += (ev_t[0].elapsed_time(ev_t[1]) / 1e3) if ev_t is not None \
+            else time.perf_counter() - t0
         finished = []
         for slot, r in list(self.running.items()):
             n = int(nsteps[slot])
