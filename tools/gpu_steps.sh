@@ -1,4 +1,4 @@
-# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b.
+# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b tune8b.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
 # (any other rc) ends the script.  Logs land in gpurun_out/r3/.
 set -o pipefail
@@ -79,6 +79,8 @@ for spec in ${RUNS:-tests smoke bench}; do
           K8S_GEMV_LOOP_BF16=$lw step 300 ab8b_loop${lw}_$i.json python -u bench.py --preset llama-3-8b --steps 10 --warmup 2
           grep -h '"metric"' $O/ab8b_loop${lw}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('8b plain loop=$lw', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
         done; done ;;
+    tune8b) step 900 tune8b.txt python -u tools/pgemm_tune.py --model 8b --tp 1 --m 256 512 2048 8192 --only qkv o_proj gate_up down --write --json-out $O/tune8b.json
+           grep -v amdgpu.ids $O/tune8b.txt | tail -20; cp k8s_llm_scheduler_amd/engine/assets/pgemm_gfx950.json $O/pgemm_gfx950.json ;;
     tp8) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
            grep -h '"metric"' $O/bench_tp8sim.json | cut -c1-600 ;;
     pf8) K8S_DECODE_PREFETCH_MB=${PFMB:-24} step 300 bench_tp8sim_pf.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2

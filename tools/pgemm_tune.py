@@ -6,7 +6,7 @@ torch._scaled_mm) and with mgemm.hip's tuned plan.
 Every candidate (tile config x split-K x group_m) is timed as a captured hipGraph of REPS launches cycling over
 enough weight copies to exceed the 256 MiB Infinity Cache (prefill weights are cold).
 
-    python tools/pgemm_tune.py --tp 1 8 --m 256 512 2048 8192 [--fp8] [--write] [--json-out f.json]
+    python tools/pgemm_tune.py --tp 1 8 --m 256 512 2048 8192 [--fp8] [--model 8b] [--write] [--json-out f.json]
 
 --write merges the winners into engine/assets/pgemm_gfx950.json (the table ops.gemm_route reads; a shape where
 mgemm's own tuned plan was faster is recorded as "mgemm").
@@ -70,7 +70,9 @@ def main() -> int:
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--model", choices=["70b", "8b"], default="70b", help="projection shapes of Llama-3.3-70B / 3-8B")
     a = ap.parse_args()
+    dims = {} if a.model == "70b" else dict(hidden=4096, inter=14336, nq=32, nkv=8)
 
     torch.manual_seed(0)
     lib_table = _load_gemm_table()
@@ -80,7 +82,7 @@ def main() -> int:
     rows, plans = [], {}
     t0 = time.time()
     for tp in a.tp:
-        for name, N, K, epi in shapes(tp):
+        for name, N, K, epi in shapes(tp, **dims):
             if a.only and name not in a.only:
                 continue
             wrows = 2 * N if epi == ops.EPI_SWIGLU else N
