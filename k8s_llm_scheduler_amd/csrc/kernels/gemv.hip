@@ -744,10 +744,12 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
   bf16_t* ro = (bf16_t*)res_out;
   const bf16_t* gw = (const bf16_t*)nw;
   const bool swiglu_loop = epi == EPI_SWIGLU && (int)grid.x <= g_gemv_loop_swiglu_max;
-  // the plain-epilogue loop only on the 70B-size matrices (>= 64 Mi weights): on Llama-3-8B's it measured slower
-  const bool plain_loop = epi == EPI_BF16 && (long long)N_out * K >= (64LL << 20);
+  // the loop only on matrices of >= 64 Mi weights (the 70B's at TP = 1, gate/up at TP = 4): on the smaller ones
+  // (Llama-3-8B, fp8 at TP = 4) it measured slower
+  const bool big = (long long)(epi == EPI_SWIGLU ? 2 * N_out : N_out) * K >= (64LL << 20);
+  const bool plain_loop = epi == EPI_BF16 && big;
   const int loop_wg = g_gemv_loop >= 0 ? g_gemv_loop
-                                       : (fp8 ? 2 : (plain_loop ? g_gemv_loop_bf16 : (swiglu_loop ? 2 : 0)));
+                                       : (fp8 ? (big ? 2 : 0) : (plain_loop ? g_gemv_loop_bf16 : (swiglu_loop ? 2 : 0)));
   if (loop_wg > 0 && splits == 1 && kw == 1 && mode != 1 && M <= 2 && (int)grid.x > 256 * loop_wg) {
     // wide: 8-wave workgroups for the plain bf16-epilogue projections whose x slice takes >= 32 KiB of LDS (the
     // down projection, K = 28672: 56 KiB): LDS, not waves, bounds those at 2 workgroups per CU, so twice the waves

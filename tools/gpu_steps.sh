@@ -1,4 +1,4 @@
-# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b tune8b.
+# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b tune8b proftp8 fp8tp4 tunefp8.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
 # (any other rc) ends the script.  Logs land in gpurun_out/r3/.
 set -o pipefail
@@ -81,6 +81,12 @@ for spec in ${RUNS:-tests smoke bench}; do
         done; done ;;
     tune8b) step 900 tune8b.txt python -u tools/pgemm_tune.py --model 8b --tp 1 --m 256 512 2048 8192 --only qkv o_proj gate_up down --write --json-out $O/tune8b.json
            grep -v amdgpu.ids $O/tune8b.txt | tail -20; cp k8s_llm_scheduler_amd/engine/assets/pgemm_gfx950.json $O/pgemm_gfx950.json ;;
+    proftp8) bash tools/gpu_prof.sh tp8sim "--simulate-tp 8" > $O/proftp8.log 2>&1 || { tail -20 $O/proftp8.log; exit 1; }
+          grep -A12 "last decode" gpurun_out/lastfwd_tp8sim.txt ;;
+    fp8tp4) step 300 bench_fp8_tp4sim.json python -u bench.py --dtype fp8 --simulate-tp 4 --steps 10 --warmup 2
+           grep -h '"metric"' $O/bench_fp8_tp4sim.json | cut -c1-200; grep -ho '"decode_ms_per_step": [0-9.]*, "prefill_ms_per_step": [0-9.]*' $O/bench_fp8_tp4sim.json ;;
+    tunefp8) step 1100 tunefp8.txt python -u tools/pgemm_tune.py --fp8 --tp 1 4 --m 192 256 384 512 768 1024 2048 4096 8192 --only qkv o_proj gate_up down --write --json-out $O/tunefp8.json
+           grep -v amdgpu.ids $O/tunefp8.txt | tail -8; cp k8s_llm_scheduler_amd/engine/assets/pgemm_gfx950.json $O/pgemm_gfx950.json ;;
     tp8) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
            grep -h '"metric"' $O/bench_tp8sim.json | cut -c1-600 ;;
     pf8) K8S_DECODE_PREFETCH_MB=${PFMB:-24} step 300 bench_tp8sim_pf.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
