@@ -706,6 +706,8 @@ static int g_gemv_loop_swiglu_max = [] {
   const char* e = getenv("K8S_GEMV_LOOP_SWIGLU_MAX");
   return e ? atoi(e) : 2048;
 }();
+// smallest matrix (Mi weights) the fp8 / plain-epilogue loop takes (K8S_GEMV_LOOP_MIN_MI)
+static int g_gemv_loop_min_mi = [] { const char* e = getenv("K8S_GEMV_LOOP_MIN_MI"); return e ? atoi(e) : 64; }();
 // default for bf16 weights with the plain bf16 epilogue (QKV, O, down -- not gate/up nor the LM head)
 static int g_gemv_loop_bf16 = [] { const char* e = getenv("K8S_GEMV_LOOP_BF16"); return e ? atoi(e) : 2; }();
 extern "C" int k8s_gemv_set_loop(int wg_per_cu) {   // returns the previous setting; < -1 only reads it
@@ -746,7 +748,7 @@ static int gemv_launch(int mode, void* out, void* partial, const void* x, const 
   const bool swiglu_loop = epi == EPI_SWIGLU && (int)grid.x <= g_gemv_loop_swiglu_max;
   // the loop only on matrices of >= 64 Mi weights (the 70B's at TP = 1, gate/up at TP = 4): on the smaller ones
   // (Llama-3-8B, fp8 at TP = 4) it measured slower
-  const bool big = (long long)(epi == EPI_SWIGLU ? 2 * N_out : N_out) * K >= (64LL << 20);
+  const bool big = (long long)(epi == EPI_SWIGLU ? 2 * N_out : N_out) * K >= ((long long)g_gemv_loop_min_mi << 20);
   const bool plain_loop = epi == EPI_BF16 && big;
   const int loop_wg = g_gemv_loop >= 0 ? g_gemv_loop
                                        : (fp8 ? (big ? 2 : 0) : (plain_loop ? g_gemv_loop_bf16 : (swiglu_loop ? 2 : 0)));
