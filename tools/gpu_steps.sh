@@ -88,7 +88,7 @@ for spec in ${RUNS:-tests smoke bench}; do
     tunefp8) step 1100 tunefp8.txt python -u tools/pgemm_tune.py --fp8 --tp 1 4 --m 192 256 384 512 768 1024 2048 4096 8192 --only qkv o_proj gate_up down --write --json-out $O/tunefp8.json
            grep -v amdgpu.ids $O/tunefp8.txt | tail -8; cp k8s_llm_scheduler_amd/engine/assets/pgemm_gfx950.json $O/pgemm_gfx950.json ;;
     minmi) for i in 1 2; do for mm in ${MINMI:-64 65}; do
-          K8S_GEMV_LOOP_MIN_MI=$mm step 400 minmi${mm}_$i.json python -u bench.py --steps 8 --warmup 2
+          K8S_GEMV_LOOP_MIN_MI=$mm step 400 minmi${mm}_$i.json python -u bench.py --steps 8 --warmup 2 ${MINMI_ARGS:-}
           grep -h '"metric"' $O/minmi${mm}_$i.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('bf16 loop_min_mi=$mm', d['value'], d.get('decode_ms_per_step'), d.get('prefill_ms_per_decision'))"
         done; done ;;
     tp8) step 300 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps 10 --warmup 2
