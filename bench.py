@@ -15,8 +15,12 @@ tensor parallel over RCCL; decisions are made by all ranks together, so the job 
 decision rate itself.  Scaling is "strong" (fixed work per decision, more GPUs).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--preset llama-3.3-70b] [--gen-tokens 64]
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
-    torchrun --nproc-per-node 8 ... bench.py --gpus 8 --tp 4 --dtype fp8   # 2 half-node replicas (config 5)
+    python bench.py --gpus 8                        # launches the 8 ranks itself (torch.distributed.run child)
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8   # the same, launched from outside
+    python bench.py --gpus 8 --tp 4 --dtype fp8     # 2 half-node replicas (config 5)
+
+--gpus N must equal the launcher's WORLD_SIZE (the run refuses otherwise); without a launcher, N > 1 ranks are
+started here before anything touches the GPU.
 
 Default: one TP=N engine (strong scaling).  With --tp T < N, N/T replicas each decide their own
 pods (data parallelism, weak scaling) and the value is the sum over replicas.
@@ -74,6 +78,16 @@ def main() -> int:
     args = ap.parse_args()
     t_start = time.perf_counter()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and args.simulate_tp <= 1:
+        # `python bench.py --gpus N` without a launcher: start the N rank processes ourselves (one per GPU) before
+        # anything in this process touches the GPU, and exit with the launcher's code; rank 0 prints the JSON line
+        return self_launch(args.gpus)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.simulate_tp <= 1 and world_env != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}: refusing to report a {world_env}-rank run as "
+              f"{args.gpus} GPUs", file=sys.stderr)
+        return 2
+
     def progress(msg: str) -> None:
         # stage lines on stderr (stdout carries only the JSON line): shows where a slow start is spent
         print(f"[bench rank {os.environ.get('RANK', '0')} +{time.perf_counter() - t_start:.1f}s] {msg}",
@@ -94,9 +108,7 @@ def main() -> int:
     if args.verbose:
         logging.getLogger("k8s_llm_scheduler_amd").setLevel(logging.INFO)
     progress("imports done")
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    world = world_env
     local = int(os.environ.get("LOCAL_RANK", "0"))
     on_gpu = torch.cuda.is_available()   # CPU: reference ops, for trying the harness without a GPU
     if on_gpu:
@@ -190,6 +202,7 @@ def main() -> int:
         svc.decide_many(make_items())
     progress("warmup done")
     eng.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in eng.stats.items()})
+    tp.rccl_calls = 0
     lat = []
     barrier()
     t0 = time.perf_counter()
@@ -202,7 +215,8 @@ def main() -> int:
     barrier()
     elapsed = time.perf_counter() - t0
     if distributed:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cuda" if on_gpu and tp.backend == "nccl" else "cpu",
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -244,11 +258,13 @@ def main() -> int:
         "prefill_ms_per_decision": round(1000 * st["prefill_time"] / max(1, args.steps * args.batch), 2),
         "prefill_tokens_per_decision": round(st["prefill_tokens"] / max(1, args.steps * args.batch), 1),
         "prefill_graph_replays": st.get("prefill_graph_replays", 0),
+        "rccl_calls_timed": tp.rccl_calls,
         "prefill_overlap_chunks": st.get("prefill_overlap_chunks", 0),
         "speculative": {"tokens": args.speculative, "steps": st.get("spec_steps", 0),
                         "drafted": st.get("spec_drafted", 0), "accepted": st.get("spec_accepted", 0)},
         "fallback_rate": round(fallbacks / (args.steps * args.batch), 3),
         "init_s": round(init_s, 1),
+        "physical_gpus": torch.cuda.device_count() if on_gpu else 0,
         "tp_comm": tp.comm_info,
         "baseline_note": "BASELINE.md publishes no numbers; vs_baseline uses the implied 0.3 decisions/s of test_e2e.py",
     }
@@ -262,6 +278,27 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def self_launch(n: int) -> int:
+    """Run this same command line as an N-rank job: ``torch.distributed.run`` as a CHILD process (one rank per GPU,
+    rendezvous on 127.0.0.1), this process never initialises the GPU and exits with the launcher's code.  Ranks
+    r >= device_count share GPU r % device_count (the one-GPU rehearsal)."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    print(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    rc = subprocess.call(cmd, env=env)
+    if rc != 0:
+        print(f"[bench] the {n}-rank job failed (exit {rc})", file=sys.stderr, flush=True)
+    return rc
 
 
 def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp, router=None) -> int:

@@ -235,6 +235,12 @@ class LLMEngine:
             control.start_monitor()
         # prompt-lookup speculative decoding (_spec_decode): drafted tokens per step, 0 = off
         self.speculative_tokens = max(0, int(speculative_tokens))
+        if self.speculative_tokens:
+            # the verify steps emit tokens on the host without advancing the sampler's device stop state (JSON
+            # depth, done flag), so a later one-token decode would see a stale brace depth and could end an answer
+            # early: stop detection stays on the host (_emit) and prefills carry no decode rows
+            self.device_stop = False
+            self.mixed_steps = False
         # also capture decode graphs with the top-p passes (config llm.top_p < 1); otherwise chunks
         # holding a top_p < 1 request decode eagerly
         self.capture_nucleus = capture_nucleus
@@ -602,8 +608,13 @@ class LLMEngine:
         passes; without them a chunk holding a top_p < 1 request decodes eagerly."""
         if not self.use_graphs:
             return
-        with trace("engine.capture_graphs"):
-            self._capture_graphs(buckets, self.capture_nucleus if nucleus is None else nucleus)
+        tp = self.model.tp
+        keep, tp.capture_on_xgmi = tp.capture_on_xgmi, True   # RCCL stays out of the graphs (TPGroup._xgmi_ok)
+        try:
+            with trace("engine.capture_graphs"):
+                self._capture_graphs(buckets, self.capture_nucleus if nucleus is None else nucleus)
+        finally:
+            tp.capture_on_xgmi = keep
 
     def _capture_graphs(self, buckets: Optional[Sequence[int]], nucleus: bool) -> None:
         assert not self.running and not self.prefilling, "capture needs an idle engine"
@@ -684,7 +695,8 @@ class LLMEngine:
             return False                   # the reduce-scatters run on RCCL: eager, like every RCCL chunk
         ar_bytes = Tb * self.model.cfg.hidden * 2
         gather_bytes = logits_rows * self.model.lm_head.shape[0] * 4
-        return ar_bytes <= (tp.xgmi_max_ar or tp.xgmi.max_allreduce_bytes) and gather_bytes <= tp.xgmi.slot_bytes
+        # captured with tp.capture_on_xgmi: every all-reduce that fits the capacity stays on xGMI
+        return ar_bytes <= tp.xgmi.max_allreduce_bytes and gather_bytes <= tp.xgmi.slot_bytes
 
     def _p_views(self, Tb: int):
         Tm = PREFILL_GRAPH_BUCKETS[-1]
@@ -806,8 +818,11 @@ class LLMEngine:
         if msg.get("reset"):
             self._reset_seen = self.control.reset_generation()
             if not self._drained(max(5.0, self.watchdog_s)):
+                # no reset with the device busy (reset_collectives would block in a synchronize): stay not ready,
+                # the leader's bounded barrier times out and it retries (or exits, engine.on_unrecoverable)
                 self._fail("reset: device did not drain")
                 self._unrecoverable("device did not drain for the reset")
+                return "reset"
             self._reset_all(announce=False)
             return "reset"
         for rid, ids, pd, seed in msg["new"]:
@@ -1409,6 +1424,12 @@ class LLMEngine:
                 self.step()
             except StopIteration:
                 return
+            except RequestRejected as e:
+                # the leader rejected the same request at the same point of its step (it replays this schedule):
+                # finish it here too and keep following
+                r = e.request
+                r.error = e
+                self._finish(r, "error")
             except (CollectiveError, EngineStalled) as e:
                 log.error(f"TP worker rank {self.control.rank}: {e}; waiting for rank 0's reset")
 

@@ -755,12 +755,30 @@ def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
     if y is not None:
         pass
     elif _is_fp8(w):
+        _library_allowed("linear", x2, w, out_dtype)
         y = _fp8_gemm(x2, w, out_dtype)
     else:
+        _library_allowed("linear", x2, w, out_dtype)
         y = _lib_linear(x2, w)
         if out_dtype is not None and out_dtype != y.dtype:
             y = y.to(out_dtype)
     return y.view(*x.shape[:-1], y.shape[-1])
+
+
+class NoKernelForShape(RuntimeError):
+    """No hand-written kernel accepts this GEMM (and K8S_GEMM is not ``library``)."""
+
+
+def _library_allowed(op: str, x2: torch.Tensor, w, out_dtype=None) -> None:
+    """The library GEMMs (hipBLASLt / torch._scaled_mm) run only under K8S_GEMM=library, the A/B oracle: on the
+    default route a shape no hand-written kernel accepts is an error, never a silent switch to the library."""
+    if GEMM_BACKEND == "library":
+        return
+    t = w.q if _is_fp8(w) else w
+    raise NoKernelForShape(
+        f"{op}: no hand-written kernel for x {tuple(x2.shape)} @ w {tuple(t.shape)}^T ({'fp8' if _is_fp8(w) else 'bf16'}"
+        f" weights, out {out_dtype or 'bf16'}; the GEMMs need N % 4 == 0 and 128-byte k-steps) under K8S_GEMM="
+        f"{GEMM_BACKEND}; K8S_GEMM=library runs the library GEMMs")
 
 
 def linear_norm(x: torch.Tensor, w, norm_w: Optional[torch.Tensor], eps: float,
@@ -916,8 +934,10 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     if y is not None:
         pass
     elif _is_fp8(w_gate_up):
+        _library_allowed("linear_swiglu", x2, w_gate_up)
         y = silu_mul(_fp8_gemm(x2, w_gate_up))
     else:
+        _library_allowed("linear_swiglu", x2, w_gate_up)
         y = silu_mul(_lib_linear(x2, w_gate_up))
     return y.view(*x.shape[:-1], y.shape[-1])
 

@@ -58,12 +58,19 @@ class TPGroup:
 
     xgmi_max_ar: int = 0            # all-reduces up to this size use xGMI (autotune_comm; 0 = capacity)
 
+    # while a graph is being captured every all-reduce that fits the xGMI capacity runs on xGMI even where the
+    # autotune found RCCL faster eagerly: a captured prefill chunk beats an eager one by far more than the
+    # transport difference, and RCCL stays out of captured graphs (engine._prefill_bucket_capturable)
+    capture_on_xgmi: bool = False
+    rccl_calls: int = 0             # RCCL collectives issued from the host (a graph replay issues none)
+
     def _xgmi_ok(self, t: torch.Tensor, reduce: bool = False) -> bool:
         n = t.numel() * t.element_size()
         if self.xgmi is None or not t.is_cuda or n % 16 or n <= 0:
             return False
         if reduce:
-            return n <= (self.xgmi_max_ar or self.xgmi.max_allreduce_bytes)
+            cap = self.xgmi.max_allreduce_bytes
+            return n <= (cap if self.capture_on_xgmi else (self.xgmi_max_ar or cap))
         return n <= self.xgmi.slot_bytes
 
     @property
@@ -83,6 +90,7 @@ class TPGroup:
                 self.xgmi.all_reduce_bf16(t.data_ptr(), t.data_ptr(), t.numel() * 2, -1, rp)
                 return t
             elif self.rccl is not None and t.is_cuda:
+                self.rccl_calls += 1
                 self.rccl.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], 0, -1)
             elif self.backend == "gloo" and t.dtype == torch.bfloat16:
                 f = t.float()
@@ -122,6 +130,7 @@ class TPGroup:
         if self._xgmi_ok(t):
             self.xgmi.all_gather(t.data_ptr(), out.data_ptr(), t.numel() * t.element_size(), -1)
         elif self.rccl is not None and t.is_cuda:
+            self.rccl_calls += 1
             self.rccl.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], -1)
         elif self.backend == "gloo":
             dist.all_gather(list(out.unbind(0)), t.contiguous(), group=self.group)
@@ -145,6 +154,7 @@ class TPGroup:
         elif self.rccl is not None and t.is_cuda and t.dtype in _DT:
             t = t.contiguous()
             out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            self.rccl_calls += 1
             self.rccl.reduce_scatter(t.data_ptr(), out.data_ptr(), out.numel(), _DT[t.dtype], 0, -1)
         else:
             out = self.all_reduce_(t.contiguous())[self.rank * n:(self.rank + 1) * n]
@@ -210,18 +220,24 @@ class TPGroup:
         if self.world <= 1 or self.simulate:
             self.failed = None
             return
-        if self.xgmi is not None or self.rccl is not None:
+        if (self.xgmi is not None or self.rccl is not None) and torch.cuda.is_initialized():
             torch.cuda.synchronize()
         if self.xgmi is not None:
             self.xgmi.reset()
-        if self.rccl is not None and (self.rccl.aborted or self.rccl.async_error()):
+        rebuild = self.rccl is not None and bool(self.rccl.aborted or self.rccl.async_error())
+        if control is not None:
+            # one decision for the whole replica: a rank whose own communicator looks healthy (it never saw the
+            # stall) must still take part in the rebuild the others need, or the collectives below do not match
+            control.barrier(timeout_s)
+            rebuild = control.any_rank(rebuild)
+        if rebuild:
             from .. import ops
 
+            if control is None:
+                raise CollectiveError("RCCL communicator rebuild needs the control channel")
             if not self.rccl.aborted:
                 self.rccl.abort()
             uid = ops.native().RcclComm.unique_id() if self.rank == 0 else None
-            if control is None:
-                raise CollectiveError("RCCL communicator rebuild needs the control channel")
             uid = control.broadcast_object(uid)
             self.rccl = ops.native().RcclComm(self.world, self.rank, uid)
         if control is not None:
@@ -383,6 +399,14 @@ class ControlChannel:
         dist.recv(buf, src=self.src, group=self.group, tag=3)
         return int(buf[0])
 
+    def any_rank(self, flag: bool) -> bool:
+        """True on every rank of the replica iff ``flag`` is true on any of them (every rank must call this)."""
+        if self.world <= 1:
+            return bool(flag)
+        flags = [None] * self.world
+        dist.all_gather_object(flags, bool(flag), group=self.group)
+        return any(flags)
+
     def broadcast_object(self, obj):
         box = [obj]
         dist.broadcast_object_list(box, src=self.src, group=self.group)
@@ -499,13 +523,24 @@ def _agree(tp: TPGroup, ok: bool) -> bool:
     return all(flags)
 
 
+XGMI_AR_CAPACITY = 8 << 20   # the largest all-reduce on the xGMI transports: a 512-token chunk of 70B (8192 x bf16)
+
+
+def default_slot_bytes(world: int) -> int:
+    """Per-peer slot of the xGMI region: every all-reduce up to XGMI_AR_CAPACITY fits (two-shot capacity is world x
+    slot), so a decision's prefill chunk (<= 512 tokens, 8 MiB per all-reduce at 70B) stays on the graph-capturable
+    peer-memory path at every TP degree; at least 512 KiB (one-shot decode all-reduces up to batch 32).  The region
+    holds 10 x world slots: ~80 MiB of the 288 GB."""
+    return max(512 * 1024, (XGMI_AR_CAPACITY // max(1, world) + 4095) // 4096 * 4096)
+
+
 def make_xgmi_comm(tp: TPGroup, slot_bytes: Optional[int] = None, blocks: Optional[int] = None,
                    timeout_s: float = 60.0):
     """Map every rank's IPC region into every process and self-test the one-shot collectives.
     Returns None (on every rank alike) when any rank cannot take part."""
     from .. import ops
 
-    slot_bytes = int(slot_bytes or os.environ.get("K8S_XGMI_MAX_BYTES", 512 * 1024))
+    slot_bytes = int(slot_bytes or os.environ.get("K8S_XGMI_MAX_BYTES", 0) or default_slot_bytes(tp.world))
     slot_bytes = (slot_bytes + 4095) // 4096 * 4096
     blocks = int(blocks or os.environ.get("K8S_XGMI_BLOCKS", 16))
     timeout_s = float(os.environ.get("K8S_XGMI_TIMEOUT_S", timeout_s))
@@ -604,7 +639,7 @@ def comm_thresholds(table: dict, cap: int):
     return ll_max, two_min, xgmi_max
 
 
-def autotune_comm(tp: TPGroup, sizes=(16384, 65536, 262144, 1 << 20, 4 << 20)) -> None:
+def autotune_comm(tp: TPGroup, sizes=(16384, 65536, 262144, 1 << 20, 4 << 20, 8 << 20)) -> None:
     """Graph-time every all-reduce transport at every message size class the engine issues (decode B=1:
     16 KiB; batched decode: up to 1 MiB at B=64; prefill chunks: MiBs), max over ranks, and set the
     thresholds: the LL protocol up to the largest size it wins, the two-shot kernel from the smallest

@@ -24,7 +24,9 @@ import datetime
 import itertools
 import logging
 import threading
+import time
 from concurrent.futures import Future, ThreadPoolExecutor
+from concurrent.futures import TimeoutError as FutureTimeout
 from typing import Dict, List, Optional, Sequence
 
 import torch.distributed as dist
@@ -52,6 +54,7 @@ class ReplicaLink:
         self._plock = threading.Lock()
         self._rx: Optional[threading.Thread] = None
         self.inflight = 0           # requests sent and not answered yet (router load)
+        self.dead: Optional[str] = None   # set when the link failed: every later submit fails at once
 
     @staticmethod
     def _bcast(obj, src: int, group):
@@ -65,33 +68,48 @@ class ReplicaLink:
             return
 
         def run():
-            while True:
-                msg = self._bcast(None, self.leader, self.up)
-                if msg == _STOP:
-                    break
-                with self._plock:
-                    fut = self._pending.pop(msg["id"], None)
-                if fut is None:
-                    continue
-                if "error" in msg:
-                    fut.set_exception(RuntimeError(f"replica {self.replica}: {msg['error']}"))
-                else:
-                    fut.set_result(list(msg["texts"]))
-            with self._plock:   # the link is closed: nothing more will be answered
-                left, self._pending = self._pending, {}
-            for fut in left.values():
-                fut.set_exception(RuntimeError(f"replica {self.replica} link closed"))
+            why = f"replica {self.replica} link closed"
+            try:
+                while True:
+                    msg = self._bcast(None, self.leader, self.up)
+                    if msg == _STOP:
+                        break
+                    with self._plock:
+                        fut = self._pending.pop(msg["id"], None)
+                    if fut is None:
+                        continue
+                    if "error" in msg:
+                        fut.set_exception(RuntimeError(f"replica {self.replica}: {msg['error']}"))
+                    else:
+                        fut.set_result(list(msg["texts"]))
+            except Exception as e:  # noqa: BLE001 -- the remote leader died or the gloo link broke
+                why = f"replica {self.replica} link failed: {type(e).__name__}: {e}"
+                log.error(f" {why}")
+            self._close(why)
 
         self._rx = threading.Thread(target=run, name=f"replica{self.replica}-rx", daemon=True)
         self._rx.start()
 
+    def _close(self, why: str) -> None:
+        """Nothing more will be answered on this link: fail every pending future and every later submit."""
+        with self._plock:
+            self.dead = self.dead or why
+            left, self._pending = self._pending, {}
+        for fut in left.values():
+            if not fut.done():
+                fut.set_exception(RuntimeError(why))
+
     def submit(self, requests) -> Future:
-        """Send a share of chat requests; the future resolves to their texts (request order)."""
+        """Send a share of chat requests; the future resolves to their texts (request order), or fails when the
+        link is (or becomes) dead."""
         self._start_rx()
         fut: Future = Future()
         rid = next(self._ids)
         n = len(requests)
         with self._plock:
+            if self.dead:
+                fut.set_exception(RuntimeError(self.dead))
+                return fut
             self._pending[rid] = fut
             self.inflight += n
 
@@ -100,8 +118,11 @@ class ReplicaLink:
                 self.inflight -= n
 
         fut.add_done_callback(done)
-        with self._send_lock:
-            self._bcast({"id": rid, "requests": list(requests)}, 0, self.down)
+        try:
+            with self._send_lock:
+                self._bcast({"id": rid, "requests": list(requests)}, 0, self.down)
+        except Exception as e:  # noqa: BLE001
+            self._close(f"replica {self.replica} link failed on send: {type(e).__name__}: {e}")
         return fut
 
     def request(self, payload):
@@ -144,6 +165,8 @@ def make_replica_links(tp: TPGroup) -> List[ReplicaLink]:
 
 class ReplicaRouterBackend:
     """Decision backend of rank 0 that sends every request to the least-loaded engine replica."""
+
+    reply_grace_s = 5.0
 
     def __init__(self, local, links: Sequence[ReplicaLink]):
         self.local = local
@@ -201,10 +224,16 @@ class ReplicaRouterBackend:
         finally:
             with self._lock:
                 self._local_inflight -= len(shares[0])
+        # a remote share is waited for no longer than the call's deadline (plus a grace period for the reply)
+        limits = [float(r.deadline_s) for r in requests if getattr(r, "deadline_s", None)]
+        end = time.monotonic() + min(limits) + self.reply_grace_s if limits else None
         for i, fut in futs.items():
             try:
-                for j, text in zip(shares[i], fut.result()):
+                left = None if end is None else max(0.0, end - time.monotonic())
+                for j, text in zip(shares[i], fut.result(timeout=left)):
                     out[j] = text
+            except FutureTimeout:
+                err = err or TimeoutError(f"replica {i} did not answer within the call deadline")
             except BaseException as e:  # noqa: BLE001
                 err = err or e
         if err is not None:

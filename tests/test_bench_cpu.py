@@ -63,3 +63,28 @@ def test_bench_arrival_mode_with_replicas():
     assert d["bound"] == 12 and d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp2-tp2"
     disp = d["config"]["replica_dispatch"]
     assert sum(disp) == 13 and min(disp) >= 3, disp
+
+
+def test_bench_self_launches_ranks_for_gpus_n():
+    """`python bench.py --gpus N` with no launcher starts the N ranks itself (a
+    torch.distributed.run child) and reports N GPUs -- never a 1-rank number labelled N."""
+    env = dict(os.environ, PYTHONPATH=ROOT, K8S_TP_BACKEND="gloo", OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--tp", "2", "--preset", "tiny",
+                        "--steps", "2", "--warmup", "1", "--gen-tokens", "8"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout          # rank 0 alone prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp2-tp2" and d["config"]["global_batch"] == 2
+    assert d["scaling"] == "weak" and d["value"] > 0
+
+
+def test_bench_refuses_gpus_that_disagree_with_world_size():
+    env = dict(os.environ, PYTHONPATH=ROOT, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--preset", "tiny",
+                        "--steps", "1", "--warmup", "0"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr and not p.stdout.strip()

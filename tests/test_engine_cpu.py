@@ -362,3 +362,29 @@ def test_mixed_prefill_decode_steps_match_split_path():
     split, n_split = run(False)
     assert n_mixed >= 2 and n_split == 0
     assert mixed == split and all(len(t) == 20 for t in mixed)
+
+
+@pytest.mark.parametrize("tp", [2, 4, 8])
+def test_decision_prefill_buckets_stay_on_captured_xgmi(tp):
+    """with the default slot size every decision-sized prefill bucket (<= 512 tokens, 8 MiB
+    all-reduces at 70B) fits the xGMI transports at TP = 2 / 4 / 8 and is captured -- also when the autotune found
+    RCCL faster for large messages eagerly (xgmi_max_ar below the chunk's size): while capturing, the all-reduces
+    that fit run on xGMI (TPGroup.capture_on_xgmi), so RCCL never enters a graph."""
+    from types import SimpleNamespace
+
+    from k8s_llm_scheduler_amd.engine.engine import PREFILL_GRAPH_BUCKETS, LLMEngine
+    from k8s_llm_scheduler_amd.parallel.comm import TPGroup, default_slot_bytes
+
+    slot = default_slot_bytes(tp)
+    xg = SimpleNamespace(slot_bytes=slot, max_allreduce_bytes=tp * slot)
+    group = TPGroup(0, tp, None, "nccl", xgmi=xg)
+    group.xgmi_max_ar = 1 << 20                     # autotune: RCCL faster from 1 MiB on (eager chunks)
+    fake = SimpleNamespace(model=SimpleNamespace(tp=group, cfg=SimpleNamespace(hidden=8192),
+                                                 lm_head=torch.empty(128256 // tp, 1)))
+    for Tb in PREFILL_GRAPH_BUCKETS:
+        assert LLMEngine._prefill_bucket_capturable(fake, Tb), (tp, Tb)
+    chunk = SimpleNamespace(numel=lambda: 512 * 8192, element_size=lambda: 2, is_cuda=True)
+    assert not group._xgmi_ok(chunk, reduce=True)     # eager: the autotune's RCCL threshold
+    group.capture_on_xgmi = True
+    assert group._xgmi_ok(chunk, reduce=True)         # captured: xGMI
+    assert 10 * tp * slot <= 96 << 20                 # the whole peer region stays small

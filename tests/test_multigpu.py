@@ -170,7 +170,7 @@ def _check_twoshot(tp, res):
     keep = (xg.ll_max_bytes, xg.twoshot_min_bytes)
     xg.ll_max_bytes, xg.twoshot_min_bytes = 0, 16
     cap = xg.max_allreduce_bytes
-    sizes = sorted({n for n in (1 << 20, 2 << 20, 4 << 20, cap) if n <= cap})
+    sizes = sorted({n for n in (1 << 20, 2 << 20, 4 << 20, 8 << 20, cap) if n <= cap})
     try:
         for seed, nbytes in enumerate(sizes):
             n = nbytes // 2
@@ -335,7 +335,7 @@ def _assert_model(res, world):
     assert a >= 1 and b >= a + 1, r0["overlap_chunks"]   # the graph chunk and the eager pair chunk were split
 
 
-@pytest.mark.parametrize("world", [8, 4])
+@pytest.mark.parametrize("world", [8, 4, 2])
 def test_tp_rehearsal_ranks_share_one_gpu(world):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -388,3 +388,27 @@ def test_multi_gpu_tp_rccl_and_xgmi(world):
         pytest.skip(f"needs {world} GPUs (found {torch.cuda.device_count() if torch.cuda.is_available() else 0})")
     res = run_ranks(_multi_gpu_rank, world, env={"K8S_PREFILL_OVERLAP_MIN": "128"}, timeout_s=600)
     _assert_model(res, world)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_self_launch_rehearsal_prefill_on_captured_xgmi(world):
+    """VERDICT r3 items 1 + 4: `python bench.py --gpus N` launches its N ranks itself (here time-sharing the one
+    GPU), reports n_gpus N, and every decision's prefill chunk replays a captured graph on the xGMI transports --
+    no RCCL collective is issued in the timed decisions."""
+    import json
+    import subprocess
+    import sys
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, K8S_TP_BACKEND="gloo", K8S_TP_COMM="xgmi", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--preset", "tiny-tp8",
+                        "--steps", "3", "--warmup", "1", "--gen-tokens", "8"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == world and d["config"]["parallelism"] == f"tp{world}", d
+    assert d["prefill_graph_replays"] >= 3 and d["rccl_calls_timed"] == 0, d

@@ -88,3 +88,34 @@ def test_gemv_threshold_and_kernel_limit():
 
 if __name__ == "__main__":
     pytest.main([__file__])
+
+
+@pytest.mark.parametrize("backend", ["auto", "mgemm", "pgemm"])
+def test_unroutable_shape_raises_instead_of_calling_the_library(monkeypatch, backend):
+    """a shape no hand-written kernel accepts (N % 4 != 0 here) raises under every hand-written
+    route -- linear and linear_swiglu never fall through to hipBLASLt / _scaled_mm silently."""
+    import torch
+
+    monkeypatch.setattr(ops, "GEMM_BACKEND", backend)
+    monkeypatch.setattr(ops, "_gpu", lambda *a: True)           # route as on the GPU, compute nothing
+    called = []
+    monkeypatch.setattr(ops, "_lib_linear", lambda x, w: called.append("lib") or x @ w.t())
+    x = torch.randn(300, 256, dtype=torch.bfloat16)
+    w = torch.randn(130, 256, dtype=torch.bfloat16)              # N = 130: no 4-column output groups
+    assert ops.gemm_route(300, 130, 256, ops.EPI_BF16, False)[0] == "library"
+    with pytest.raises(ops.NoKernelForShape, match="K8S_GEMM=library"):
+        ops.linear(x, w)
+    with pytest.raises(ops.NoKernelForShape):
+        ops.linear_swiglu(x, torch.randn(2 * 130, 256, dtype=torch.bfloat16))
+    assert not called
+
+
+def test_library_route_only_under_k8s_gemm_library(monkeypatch):
+    import torch
+
+    monkeypatch.setattr(ops, "GEMM_BACKEND", "library")
+    monkeypatch.setattr(ops, "_gpu", lambda *a: True)
+    called = []
+    monkeypatch.setattr(ops, "_lib_linear", lambda x, w: called.append("lib") or (x.float() @ w.float().t()).to(x.dtype))
+    y = ops.linear(torch.randn(300, 256, dtype=torch.bfloat16), torch.randn(128, 256, dtype=torch.bfloat16))
+    assert called == ["lib"] and y.shape == (300, 128)

@@ -119,3 +119,58 @@ def test_world_not_multiple_of_tp_is_rejected(monkeypatch):
     monkeypatch.setenv("RANK", "0")
     with pytest.raises(ValueError):
         init_from_env("cpu", backend="gloo", tp_size=3)
+
+
+def test_link_failure_fails_pending_and_later_requests():
+    """when the link's receive side breaks (remote leader died), every pending share fails instead of
+    blocking its caller forever, and later submits fail at once; a remote share that never answers is bounded by
+    the call deadline."""
+    import threading
+    import time as _t
+
+    from k8s_llm_scheduler_amd.control.decision import GenerationRequest
+    from k8s_llm_scheduler_amd.parallel.replicas import ReplicaLink, ReplicaRouterBackend
+
+    gate = threading.Event()
+
+    class _Link(ReplicaLink):
+        sent = []
+
+        def _bcast(self, obj, src, group):
+            if group == "up":          # the receive thread: the peer goes away once a request is out
+                gate.wait(10)
+                raise RuntimeError("connection reset by peer")
+            self.sent.append(obj)
+            gate.set()
+            return obj
+
+    link = _Link(1, 4, "down", "up")
+    fut = link.submit(["req"])
+    try:
+        fut.result(timeout=10)
+        raise AssertionError("a dead link answered")
+    except RuntimeError as e:
+        assert "link failed" in str(e)
+    assert link.dead and link.submit(["again"]).exception(timeout=1) is not None
+
+    class _Silent(ReplicaLink):
+        def _bcast(self, obj, src, group):
+            if group == "up":
+                _t.sleep(30)           # never answers within the test
+            return obj
+
+    class _Local:
+        def complete(self, reqs):
+            return ["local"] * len(reqs)
+
+    router = ReplicaRouterBackend(_Local(), [_Silent(1, 4, "down", "up")])
+    router.reply_grace_s = 0.2
+    reqs = [GenerationRequest(system="s", user=f"u{i}", max_tokens=4, temperature=0.0, deadline_s=0.5)
+            for i in range(2)]
+    t0 = _t.monotonic()
+    try:
+        router.complete(reqs)
+        raise AssertionError("expected a deadline error")
+    except TimeoutError:
+        pass
+    assert _t.monotonic() - t0 < 5
