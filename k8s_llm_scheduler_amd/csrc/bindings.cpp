@@ -35,6 +35,9 @@ int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, c
                                 const int* context_lens, const int* block_tables, float scale, int num_seqs,
                                 int max_qlen, int nq, int nkv, int D, int block_size, int max_blocks, hipStream_t s);
 void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* ks_out, int* splits_out);
+int k8s_sgemv(void* out, void* partial, const void* x, const void* W, const float* wscale, const void* res, int M,
+              int N, int K, int epi, int norm, float eps, hipStream_t s);
+long long k8s_sgemv_workspace(int M, int N, int K, int epi);
 int k8s_gemv_set_loop(int wg_per_cu);
 int k8s_gemv_set_wide(int on);
 int k8s_pgemm_set_prio(int mode);
@@ -188,6 +191,15 @@ PYBIND11_MODULE(_C, m) {
     check(k8s_gemv_norm(P(out), P(partial), P(x), P(W), M, N, K, epi, P(res_in), P(res_out), P(nw), eps, S(s)),
           "gemv_norm");
   });
+  // small-batch decode GEMV (3..8 rows, x in registers): returns -5 (nothing launched) for a combination it does not
+  // instantiate, so the caller can take another kernel
+  m.def("sgemv", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, uintptr_t wscale, uintptr_t res, int M,
+                    int N, int K, int epi, int norm, float eps, int64_t s) {
+    const int rc = k8s_sgemv(P(out), P(partial), P(x), P(W), P<float>(wscale), P(res), M, N, K, epi, norm, eps, S(s));
+    if (rc != -5) check(rc, "sgemv");
+    return rc;
+  });
+  m.def("sgemv_workspace", [](int M, int N, int K, int epi) { return k8s_sgemv_workspace(M, N, K, epi); });
   m.def("gemv_rms", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, uintptr_t wscale, int M, int N,
                        int K, int epi, uintptr_t res_in, uintptr_t res_out, float eps, int64_t s) {
     check(k8s_gemv_rms(P(out), P(partial), P(x), P(W), P<float>(wscale), M, N, K, epi, P(res_in), P(res_out), eps, S(s)),

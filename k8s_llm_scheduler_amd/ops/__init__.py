@@ -135,7 +135,7 @@ def _ref_act_quant(x: torch.Tensor, w) -> torch.Tensor:
     if not isinstance(w, Fp8Weight):
         return x
     x2 = x.reshape(-1, x.shape[-1])
-    if x2.shape[0] <= GEMV_MAX_M:
+    if x2.shape[0] <= max(GEMV_MAX_M, SGEMV_MAX_M):   # GEMV / sgemv: bf16 activations against the fp8 weights
         return x
     q, s = ref.quantize_fp8(x2)
     return ref.dequant_fp8(q, s, torch.float32).to(x.dtype).view(x.shape)
@@ -258,6 +258,33 @@ GEMV_KERNEL_MAX_M = 8   # rows the GEMV kernels (gemv.hip) accept
 GEMV_MAX_M = int(os.environ.get("K8S_GEMV_MAX_M", "2"))
 if not 1 <= GEMV_MAX_M <= GEMV_KERNEL_MAX_M:
     raise ValueError(f"K8S_GEMV_MAX_M must be 1..{GEMV_KERNEL_MAX_M}")
+
+
+# Small decode batches, GEMV_MAX_M < rows <= SGEMV_MAX_M: csrc/kernels/sgemv.hip (x in registers, every weight
+# streamed once, the RMS statistics and the residual add / SwiGLU fused).  K8S_SGEMV=0 sends them to mgemm instead.
+SGEMV_MAX_M = GEMV_KERNEL_MAX_M if os.environ.get("K8S_SGEMV", "1") != "0" else 0
+
+
+def _sgemv(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
+           out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """epi(x2 @ w.T) for GEMV_MAX_M < M <= SGEMV_MAX_M rows on sgemv.hip (``rms_eps``: scaled by 1/rms of each x row,
+    the norm gamma folded into ``w``; ``res``: plus ``res``, written to ``out`` which may be ``res``).  None where
+    sgemv does not take the call (the caller routes it to mgemm)."""
+    M, K = x2.shape
+    if not GEMV_MAX_M < M <= SGEMV_MAX_M:
+        return None
+    fp8 = _is_fp8(w)
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x2.device)
+    ws = native().sgemv_workspace(M, N, K, epi)
+    part = torch.empty(ws, dtype=F32, device=x2.device) if ws > 0 else None
+    rc = native().sgemv(out.data_ptr(), part.data_ptr() if part is not None else 0, _chk(x2, BF16, "x"),
+                        w.q.data_ptr() if fp8 else _chk(w, BF16, "w"), w.scale.data_ptr() if fp8 else 0,
+                        _chk(res, BF16, "res") if res is not None else 0, M, N, K, epi,
+                        1 if rms_eps is not None else 0, float(rms_eps or 0.0), -1)
+    del part
+    return None if rc == -5 else out
 
 
 def _gemv(x: torch.Tensor, w, epi: int, out_dtype, norm_w=None, eps: float = 0.0, res_in=None,
@@ -680,6 +707,10 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
     """Routed hand-written GEMM of M > GEMV_MAX_M rows (None: the library route)."""
     M, K = x2.shape
     fp8 = _is_fp8(w)
+    if M <= SGEMV_MAX_M:
+        y = _sgemv(x2, w, epi, res=res, rms_eps=rms_eps, out=out)
+        if y is not None:
+            return y
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     kern, plan = gemm_route(M, N, K, epi, fp8)
     if kern == "library" or (fp8 and rms_eps is not None):
@@ -697,10 +728,12 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
     load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
     copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM."""
     M, K = r.shape
-    if _gpu(r) and M > GEMV_MAX_M and not _is_fp8(w):
+    if _gpu(r) and M > GEMV_MAX_M and (not _is_fp8(w) or M <= SGEMV_MAX_M):
         y = _gemm(r.contiguous(), w, epi, rms_eps=eps)
         if y is not None:
             return y
+        if _is_fp8(w):   # small fp8 batches never quantize their activations (the CPU oracle assumes it)
+            raise NoKernelForShape(f"linear_rms: sgemv declined fp8 x {tuple(r.shape)} (K needs > 1 k-group)")
     ones = _ones(K, r.device)
     x = rmsnorm(r, ones, eps)
     if epi == EPI_SWIGLU:

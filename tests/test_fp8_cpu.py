@@ -31,7 +31,10 @@ def test_fp8_linear_ops_match_dequantized_math():
     w = ops.quantize_fp8((torch.randn(96, 256, generator=g) * 0.05).bfloat16())
     wd = w.dequant(torch.float32)
     torch.testing.assert_close(ops.linear(x, w).float(), (x.float() @ wd.T).bfloat16().float())
-    xb = torch.randn(ops.GEMV_MAX_M + 3, 256, generator=g).bfloat16()   # GEMM rows: per-token e4m3 activations
+    xs = torch.randn(5, 256, generator=g).bfloat16()   # small-batch sgemv rows (3..8): bf16 activations too
+    torch.testing.assert_close(ops.linear(xs, w).float(), (xs.float() @ wd.T).bfloat16().float())
+    # GEMM rows (above the sgemv range): per-token e4m3 activations
+    xb = torch.randn(max(ops.GEMV_MAX_M, ops.SGEMV_MAX_M) + 3, 256, generator=g).bfloat16()
     q, sc = ref.quantize_fp8(xb)
     xq = ref.dequant_fp8(q, sc, torch.float32)
     torch.testing.assert_close(ops.linear(xb, w).float(), (xq.bfloat16().float() @ wd.T).bfloat16().float())
