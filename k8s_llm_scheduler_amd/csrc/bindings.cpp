@@ -45,6 +45,7 @@ int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const f
                  int K, int epi, const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
 int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s);
 int k8s_quantize_act_fp8(void* q, float* scale, const void* x, int T, int K, hipStream_t s);
+int k8s_quantize_act_fp8_rms(void* q, float* scale, const void* x, int T, int K, int rms, float eps, hipStream_t s);
 int k8s_dequant_fp8_rows(void* w, const void* q, const float* scale, int N, int K, hipStream_t s);
 int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi, hipStream_t s);
 int k8s_gemv_rms(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out, int K,
@@ -180,6 +181,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("quantize_act_fp8", [](uintptr_t q, uintptr_t scale, uintptr_t x, int T, int K, int64_t s) {
     check(k8s_quantize_act_fp8(P(q), P<float>(scale), P(x), T, K, S(s)), "quantize_act_fp8");
+  });
+  m.def("quantize_act_fp8_rms", [](uintptr_t q, uintptr_t scale, uintptr_t x, int T, int K, int rms, float eps,
+                                   int64_t s) {
+    check(k8s_quantize_act_fp8_rms(P(q), P<float>(scale), P(x), T, K, rms, eps, S(s)), "quantize_act_fp8_rms");
   });
   m.def("dequant_fp8_rows", [](uintptr_t w, uintptr_t q, uintptr_t scale, int N, int K, int64_t s) {
     check(k8s_dequant_fp8_rows(P(w), P(q), P<float>(scale), N, K, S(s)), "dequant_fp8_rows");

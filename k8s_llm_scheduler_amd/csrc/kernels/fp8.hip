@@ -69,18 +69,23 @@ __global__ void dequant_fp8_rows_kernel(bf16_t* __restrict__ w, const uint8_t* _
   reinterpret_cast<u32x4*>(w)[2 * i + 1] = o1;
 }
 
-// K16: per-token activation quantization for the fp8 prefill GEMMs (hipBLASLt fp8 MFMA with
-// row-wise scales): one workgroup per row, the row kept in registers between the absmax and the
-// conversion (one read of x).  sx[t] = max|x[t]| / 448, xq[t, k] = e4m3(x[t, k] / sx[t]).
-template <int VPT>
+// K16: per-token activation quantization for the fp8 prefill / batched-decode GEMMs (pgemm / mgemm on the fp8
+// MFMAs, row-wise scales in their epilogues): one workgroup per row, the row kept in registers between the absmax
+// and the conversion (one read of x).  sx[t] = max|x[t]| / 448, xq[t, k] = e4m3(x[t, k] / sx[t]).
+// RMS (K2 fused in, the norm gamma folded into W): the RMSNorm of the row only rescales it, so e4m3(norm(x)[t] / s')
+// with s' = max|norm(x)[t]| / 448 is exactly e4m3(x[t] / sx[t]) -- the same bytes -- and only the scale changes:
+// sx[t] = max|x[t]| / 448 * rsqrt(mean(x[t]^2) + eps), the sum of squares taken in the same pass.  No rmsnorm
+// kernel and no normalised bf16 copy of the residual stream run before an fp8 pre-norm projection.
+template <int VPT, bool RMS>
 __global__ void __launch_bounds__(256) quantize_act_fp8_kernel(uint8_t* __restrict__ q, float* __restrict__ scale,
-                                                               const bf16_t* __restrict__ x, int K) {
+                                                               const bf16_t* __restrict__ x, int K, float eps) {
   __shared__ float red[16];
+  __shared__ float red2[16];
   const int t = blockIdx.x;
   const u32x4* row = reinterpret_cast<const u32x4*>(x + (size_t)t * K);
   const int nvec = K / 16;  // 16 elements per thread-item
   u32x4 va[VPT], vb[VPT];
-  float amax = 0.f;
+  float amax = 0.f, ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = threadIdx.x + i * 256;
@@ -91,16 +96,27 @@ __global__ void __launch_bounds__(256) quantize_act_fp8_kernel(uint8_t* __restri
       for (int j = 0; j < 4; ++j) {
         amax = fmaxf(amax, fmaxf(fabsf(lo_bf(va[i][j])), fabsf(hi_bf(va[i][j]))));
         amax = fmaxf(amax, fmaxf(fabsf(lo_bf(vb[i][j])), fabsf(hi_bf(vb[i][j]))));
+        if constexpr (RMS) {
+          ss += lo_bf(va[i][j]) * lo_bf(va[i][j]) + hi_bf(va[i][j]) * hi_bf(va[i][j]);
+          ss += lo_bf(vb[i][j]) * lo_bf(vb[i][j]) + hi_bf(vb[i][j]) * hi_bf(vb[i][j]);
+        }
       }
     }
   }
   amax = wave_max(amax);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  if constexpr (RMS) {
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red2[threadIdx.x >> 6] = ss;
+  }
   __syncthreads();
   const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   const float s = m > 0.f ? m / FP8_MAX : 1.f;
   const float inv = 1.f / s;
-  if (threadIdx.x == 0) scale[t] = s;
+  if (threadIdx.x == 0) {
+    if constexpr (RMS) scale[t] = s * rsqrtf((red2[0] + red2[1] + red2[2] + red2[3]) / (float)K + eps);
+    else scale[t] = s;
+  }
   auto cl = [&](float v) { return fminf(fmaxf(v * inv, -FP8_MAX), FP8_MAX); };
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
@@ -124,16 +140,24 @@ __global__ void __launch_bounds__(256) quantize_act_fp8_kernel(uint8_t* __restri
 
 using namespace k8sllm;
 
-extern "C" int k8s_quantize_act_fp8(void* q, float* scale, const void* x, int T, int K, hipStream_t s) {
+// rms != 0: the row's 1/rms (eps) is folded into its scale (see quantize_act_fp8_kernel).
+extern "C" int k8s_quantize_act_fp8_rms(void* q, float* scale, const void* x, int T, int K, int rms, float eps,
+                                        hipStream_t s) {
   if (T <= 0) return 0;
   if (K <= 0 || K % 16 != 0 || K > 16 * 256 * 8) return -1;
   const int vpt = (K / 16 + 255) / 256;
   auto* qq = static_cast<uint8_t*>(q);
   auto* xx = static_cast<const bf16_t*>(x);
-  if (vpt <= 2) quantize_act_fp8_kernel<2><<<T, 256, 0, s>>>(qq, scale, xx, K);
-  else if (vpt <= 4) quantize_act_fp8_kernel<4><<<T, 256, 0, s>>>(qq, scale, xx, K);
-  else quantize_act_fp8_kernel<8><<<T, 256, 0, s>>>(qq, scale, xx, K);
+#define QA(V)                                                                               \
+  if (rms) quantize_act_fp8_kernel<V, true><<<T, 256, 0, s>>>(qq, scale, xx, K, eps);       \
+  else quantize_act_fp8_kernel<V, false><<<T, 256, 0, s>>>(qq, scale, xx, K, eps);
+  if (vpt <= 2) { QA(2) } else if (vpt <= 4) { QA(4) } else { QA(8) }
+#undef QA
   return (int)hipGetLastError();
+}
+
+extern "C" int k8s_quantize_act_fp8(void* q, float* scale, const void* x, int T, int K, hipStream_t s) {
+  return k8s_quantize_act_fp8_rms(q, scale, x, T, K, 0, 0.f, s);
 }
 
 extern "C" int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s) {

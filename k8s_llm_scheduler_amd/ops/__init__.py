@@ -108,22 +108,27 @@ def quantize_fp8(w: torch.Tensor) -> Fp8Weight:
     return Fp8Weight(q, s)
 
 
-def quantize_act_fp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Per-token (row) activation quantization: bf16 [T, K] -> (e4m3 bytes [T, K], scale [T] f32)."""
+def quantize_act_fp8(x: torch.Tensor, rms_eps: Optional[float] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-token (row) activation quantization: bf16 [T, K] -> (e4m3 bytes [T, K], scale [T] f32).
+    ``rms_eps``: quantize RMSNorm(x) (gamma folded into the weights) -- the same e4m3 bytes as x's, with each row's
+    1/rms folded into its scale (fp8.hip quantize_act_fp8_kernel): the pre-norm fp8 projections run no rmsnorm."""
     if not x.is_cuda:
-        return ref.quantize_fp8(x)
+        q, sc = ref.quantize_fp8(x)
+        if rms_eps is not None:
+            sc = sc * torch.rsqrt(x.float().pow(2).mean(-1) + rms_eps)
+        return q, sc
     T, K = x.shape
     q = torch.empty(T, K, dtype=torch.uint8, device=x.device)
     s = torch.empty(T, dtype=F32, device=x.device)
-    native().quantize_act_fp8(q.data_ptr(), s.data_ptr(), _chk(x, BF16, "x"), T, K, -1)
+    native().quantize_act_fp8_rms(q.data_ptr(), s.data_ptr(), _chk(x, BF16, "x"), T, K,
+                                  1 if rms_eps is not None else 0, float(rms_eps or 0.0), -1)
     return q, s
 
 
-def _fp8_gemm(x: torch.Tensor, w: "Fp8Weight", out_dtype=None) -> torch.Tensor:
-    """Prefill / batched-decode projection with fp8 weights: per-token e4m3 activations (hand-written
-    quantization kernel) x row-scaled e4m3 weights on the fp8 MFMA path of hipBLASLt (row-wise
-    scaled GEMM), bf16 out.  Reads 1 byte per weight instead of dequantizing to a bf16 copy."""
-    xq, sx = quantize_act_fp8(x.contiguous())
+def _fp8_gemm(x: torch.Tensor, w: "Fp8Weight", out_dtype=None, act=None) -> torch.Tensor:
+    """K8S_GEMM=library only (the A/B oracle): per-token e4m3 activations (``act`` = (q, scale) when already
+    quantized) x row-scaled e4m3 weights on hipBLASLt's row-wise scaled fp8 GEMM (torch._scaled_mm), bf16 out."""
+    xq, sx = act if act is not None else quantize_act_fp8(x.contiguous())
     f8 = torch.float8_e4m3fn
     return torch._scaled_mm(xq.view(f8), w.q.view(f8).t(), scale_a=sx.view(-1, 1), scale_b=w.scale.view(1, -1),
                             out_dtype=out_dtype or BF16)
@@ -494,7 +499,7 @@ def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
 
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
           grid: Optional[int] = None, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
-          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, act: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """Hand-written MFMA GEMM (mgemm.hip): epi(x[M, K] @ w[N, K].T), any M (routed for M > GEMV_MAX_M).  ``w``: bf16 or
     Fp8Weight (activations are then quantized per token by quantize_act_fp8).  SwiGLU: w = [Wg; Wu].
     ``rms_eps``: RMSNorm prologue -- the result is scaled by 1/rms(x row) (the norm gamma must be folded into
@@ -521,7 +526,7 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
     rp = _chk(res, BF16, "res") if res is not None else 0
     rms, eps = (1, float(rms_eps)) if rms_eps is not None else (0, 0.0)
     if fp8:
-        xq, sx = quantize_act_fp8(x.contiguous())
+        xq, sx = act if act is not None else quantize_act_fp8(x.contiguous())
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, xq.data_ptr(), w.q.data_ptr(),
                        sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, nwg, cmax, rp, 0, 0.0, -1)
     else:
@@ -556,7 +561,7 @@ def pgemm_tiles(cfg: int, M: int, N: int, epi: int) -> int:
 
 def pgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: int = 0, splits: int = 1, group_m: int = 4,
           res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
-          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, act: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """Big-tile MFMA GEMM (pgemm.hip): epi(x[M, K] @ w[N, K].T) for prefill-size M.  Same contract as :func:`mgemm`
     (bf16 or Fp8Weight, SwiGLU with w = [Wg; Wu], residual epilogue, RMS prologue with the gamma folded into w);
     ``splits`` k-slices per output tile, ``group_m`` m-tiles per tile-order group."""
@@ -577,7 +582,7 @@ def pgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: int = 0, splits: int = 1
     rp = _chk(res, BF16, "res") if res is not None else 0
     rms, eps = (1, float(rms_eps)) if rms_eps is not None else (0, 0.0)
     if fp8:
-        xq, sx = quantize_act_fp8(x.contiguous())
+        xq, sx = act if act is not None else quantize_act_fp8(x.contiguous())
         native().pgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, xq.data_ptr(), w.q.data_ptr(),
                        sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, splits, group_m, rp, 0, 0.0, -1)
     else:
@@ -703,11 +708,12 @@ def gemm_route(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[str, Option
 
 
 def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
-          out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-    """Routed hand-written GEMM of M > GEMV_MAX_M rows (None: the library route)."""
+          out: Optional[torch.Tensor] = None, act=None) -> Optional[torch.Tensor]:
+    """Routed hand-written GEMM of M > GEMV_MAX_M rows (None: the library route).  ``act``: the fp8 activations
+    (e4m3, per-token scales) when the caller quantized them already."""
     M, K = x2.shape
     fp8 = _is_fp8(w)
-    if M <= SGEMV_MAX_M:
+    if M <= SGEMV_MAX_M and act is None:
         y = _sgemv(x2, w, epi, res=res, rms_eps=rms_eps, out=out)
         if y is not None:
             return y
@@ -716,11 +722,11 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
     if kern == "library" or (fp8 and rms_eps is not None):
         return None   # (fp8: the activations are quantized after the norm, so the caller normalises first)
     if kern == "mgemm":
-        return mgemm(x2, w, epi, res=res, rms_eps=rms_eps, out=out)
+        return mgemm(x2, w, epi, res=res, rms_eps=rms_eps, out=out, act=act)
     cfg, sp, gm = plan
     if kern == "pgemm4":
         return pgemm4(x2, w, epi, cfg=cfg, splits=sp, group_m=gm, res=res, rms_eps=rms_eps, out=out)
-    return pgemm(x2, w, epi, cfg=cfg, splits=sp, group_m=gm, res=res, rms_eps=rms_eps, out=out)
+    return pgemm(x2, w, epi, cfg=cfg, splits=sp, group_m=gm, res=res, rms_eps=rms_eps, out=out, act=act)
 
 
 def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Tensor:
@@ -728,7 +734,22 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
     load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
     copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM."""
     M, K = r.shape
-    if _gpu(r) and M > GEMV_MAX_M and (not _is_fp8(w) or M <= SGEMV_MAX_M):
+    if _is_fp8(w) and M > max(GEMV_MAX_M, SGEMV_MAX_M):
+        # fp8 GEMM rows: e4m3 of the UN-normalised rows with 1/rms folded into the per-token scales (one kernel
+        # reads r once; no rmsnorm kernel, no normalised copy) -> the fp8 GEMM
+        act = quantize_act_fp8(r.contiguous(), rms_eps=eps)
+        if _gpu(r):
+            y = _gemm(r.contiguous(), w, epi, act=act)
+            if y is None:   # K8S_GEMM=library
+                _library_allowed("linear_rms", r, w)
+                y = _fp8_gemm(r, w, F32 if epi == EPI_F32 else BF16, act=act) if epi != EPI_SWIGLU else \
+                    silu_mul(_fp8_gemm(r, w, act=act))
+            return y
+        xa = ref.dequant_fp8(act[0], act[1], torch.float32)
+        if epi == EPI_SWIGLU:
+            return ref.linear_swiglu(xa, w).to(BF16)
+        return ref.linear(xa, w, F32 if epi == EPI_F32 else BF16)
+    if _gpu(r) and M > GEMV_MAX_M:
         y = _gemm(r.contiguous(), w, epi, rms_eps=eps)
         if y is not None:
             return y

@@ -79,3 +79,25 @@ def test_fp8_lm_head_option_tracks_bf16_head(monkeypatch):
     da = m8.forward_decode(torch.tensor([77], dtype=torch.int32), ctx, bt_a, 256)
     db = mh.forward_decode(torch.tensor([77], dtype=torch.int32), ctx, bt_b, 256)
     assert float(torch.nn.functional.cosine_similarity(da.flatten().float(), db.flatten().float(), dim=0)) > 0.995
+
+
+def test_fp8_linear_rms_quantizes_the_unnormalised_rows():
+    """Above the sgemv rows, fp8 pre-norm projections quantize the residual rows themselves and fold 1/rms into
+    the per-token scales (no normalised copy): the same bytes as quantizing x, the result within e4m3 rounding of
+    quantize(RMSNorm(x)) @ W."""
+    g = torch.Generator().manual_seed(3)
+    M = max(ops.GEMV_MAX_M, ops.SGEMV_MAX_M) + 4
+    r = (torch.randn(M, 256, generator=g) * 3).bfloat16()
+    w = ops.quantize_fp8((torch.randn(64, 256, generator=g) * 0.05).bfloat16())
+    q, s = ops.quantize_act_fp8(r, rms_eps=1e-5)
+    q0, s0 = ops.quantize_act_fp8(r)
+    assert torch.equal(q, q0)
+    inv = torch.rsqrt(r.float().pow(2).mean(-1) + 1e-5)
+    torch.testing.assert_close(s, s0 * inv)
+    got = ops.linear_rms(r, w, 1e-5)
+    xn = r.float() * inv[:, None]
+    want = xn @ w.dequant(torch.float32).T
+    assert float((got.float() - want).abs().max() / want.abs().max()) < 0.06
+    gu = ops.quantize_fp8((torch.randn(2 * 32, 256, generator=g) * 0.05).bfloat16())
+    y = ops.linear_rms(r, gu, 1e-5, ops.EPI_SWIGLU)
+    assert y.shape == (M, 32) and y.dtype == torch.bfloat16

@@ -476,6 +476,40 @@ def test_quantize_act_fp8_matches_reference(T, K):
     assert float((diff / b.abs().clamp_min(2 ** -6)).max()) <= 0.125 + 1e-6
 
 
+@pytest.mark.parametrize("T,K", [(1, 8192), (300, 1024), (37, 3584), (64, 8192)])
+def test_quantize_act_fp8_rms_folds_the_norm_into_the_scale(T, K):
+    """K2 fused into K16: the RMSNorm of a row only rescales it, so the quantized bytes are x's own and the scale
+    carries 1/rms -- the dequantized result equals the per-token quantization of RMSNorm(x) (CPU reference)."""
+    x = rnd(T, K, scale=3.0)
+    q, s = ops.quantize_act_fp8(x, rms_eps=1e-5)
+    q0, s0 = ops.quantize_act_fp8(x)
+    assert torch.equal(q, q0)                                  # same bytes
+    inv = torch.rsqrt(x.float().pow(2).mean(-1) + 1e-5)
+    torch.testing.assert_close(s, s0 * inv, rtol=2e-6, atol=0)
+    xn = (x.float() * inv[:, None]).cpu()
+    back = ref.dequant_fp8(q.cpu(), s.cpu())
+    assert float(((back - xn).abs() / xn.abs().amax(-1, keepdim=True)).max()) <= 2 ** -4
+
+
+def test_fp8_linear_rms_runs_no_rmsnorm_kernel(monkeypatch):
+    """fp8 pre-norm projections above the sgemv rows: one quantize (with the norm folded in) + the fp8 GEMM, no
+    rmsnorm kernel; the result tracks quantize(RMSNorm(x)) @ W."""
+    calls = []
+    nat = ops.native()
+    orig = nat.rmsnorm
+    monkeypatch.setattr(nat, "rmsnorm", lambda *a: calls.append("rmsnorm") or orig(*a))
+    M, N, K = 64, 2560, 8192
+    r = rnd(M, K, scale=3.0)
+    w = ops.quantize_fp8(rnd(N, K, scale=0.05))
+    got = ops.linear_rms(r, w, 1e-5)
+    torch.cuda.synchronize()
+    assert not calls
+    xn = r.float() * torch.rsqrt(r.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    want = xn.cpu() @ ref.dequant_fp8(w.q.cpu(), w.scale.cpu()).T
+    rel = float((got.float().cpu() - want).abs().max() / want.abs().max())
+    assert rel < 0.06, rel
+
+
 @pytest.mark.parametrize("M", [9, 64, 300])
 @pytest.mark.parametrize("N,K", [(2560, 8192), (8192, 2048), (96, 512)])
 def test_fp8_prefill_gemm(M, N, K):
