@@ -573,6 +573,11 @@ def make_xgmi_comm(tp: TPGroup, slot_bytes: Optional[int] = None, blocks: Option
     if not _agree(tp, ok):
         log.warning(" xGMI peer-memory collectives disabled: self-test failed")
         return None
+    # the GEMV with the all-reduce in its epilogue (decode O / down projections): bit-exact against GEMV + the LL
+    # all-reduce on this node's links, or the decode falls back to the separate kernels (same bits, one launch more)
+    if not _agree(tp, _fused_ar_selftest(tp, comm, dev)):
+        log.warning(" fused GEMV all-reduce disabled: self-test failed (decode uses GEMV + xGMI all-reduce)")
+        tp.fused_ar = False
     return comm
 
 
@@ -599,6 +604,53 @@ def _xgmi_selftest(tp: TPGroup, comm, dev) -> bool:
         return True
     except Exception as e:  # noqa: BLE001
         log.warning(f" xGMI self-test raised: {e}")
+        return False
+
+
+def _fused_ar_selftest(tp: TPGroup, comm, dev) -> bool:
+    """gemv.hip GemvAr over the mapped peer regions vs GEMV + the LL all-reduce (+ residual), bitwise, twice (both
+    epoch parities); the two-shot kernel at 1 MiB against the fixed-order fp32 sum."""
+    from .. import ops
+
+    try:
+        M, N, K = 1, 1024, 1024
+        g = torch.Generator().manual_seed(17)
+        xs = [torch.randn(M, K, generator=g).to(torch.bfloat16) for _ in range(tp.world)]
+        ws = [(torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16) for _ in range(tp.world)]
+        r = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+        x, w = xs[tp.rank].to(dev), ws[tp.rank].to(dev)
+        keep = comm.ll_max_bytes
+        comm.ll_max_bytes = max(keep, 2 * M * N)
+        try:
+            for _ in range(2):
+                y = ops.gemv_allreduce(comm, x, w, r)
+                if y is None:
+                    return True            # shape outside the fused plan: nothing to check, nothing used
+                base = ops.linear(x, w)
+                comm.all_reduce_bf16(base.data_ptr(), base.data_ptr(), M * N * 2, -1, r.data_ptr())
+                torch.cuda.synchronize(dev)
+                if comm.error() != 0 or not torch.equal(y, base):
+                    return False
+        finally:
+            comm.ll_max_bytes = keep
+        n = (1 << 20) // 2
+        if 2 * n <= comm.max_allreduce_bytes:
+            keep2 = comm.twoshot_min_bytes
+            comm.twoshot_min_bytes = 16
+            try:
+                parts = [(torch.arange(n, dtype=torch.float32) % 97 - 48 + 5 * q).to(torch.bfloat16)
+                         for q in range(tp.world)]
+                t = parts[tp.rank].to(dev)
+                comm.all_reduce_bf16(t.data_ptr(), t.data_ptr(), 2 * n, -1)
+                torch.cuda.synchronize(dev)
+                want = sum(p.float() for p in parts).to(torch.bfloat16)
+                if comm.error() != 0 or not torch.equal(t.cpu(), want):
+                    return False
+            finally:
+                comm.twoshot_min_bytes = keep2
+        return True
+    except Exception as e:  # noqa: BLE001
+        log.warning(f" fused GEMV all-reduce self-test raised: {e}")
         return False
 
 
