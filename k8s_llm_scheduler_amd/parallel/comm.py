@@ -529,9 +529,10 @@ XGMI_AR_CAPACITY = 8 << 20   # the largest all-reduce on the xGMI transports: a 
 def default_slot_bytes(world: int) -> int:
     """Per-peer slot of the xGMI region: every all-reduce up to XGMI_AR_CAPACITY fits (two-shot capacity is world x
     slot), so a decision's prefill chunk (<= 512 tokens, 8 MiB per all-reduce at 70B) stays on the graph-capturable
-    peer-memory path at every TP degree; at least 512 KiB (one-shot decode all-reduces up to batch 32).  The region
-    holds 10 x world slots: ~80 MiB of the 288 GB."""
-    return max(512 * 1024, (XGMI_AR_CAPACITY // max(1, world) + 4095) // 4096 * 4096)
+    peer-memory path at every TP degree; at least 4 MiB, so the decode step's logits all-gather (rows x vocab / TP
+    fp32 per rank: 4.1 MB at TP=8 and 64 rows) stays on xGMI inside the decode graphs too.  The region holds
+    10 x world slots: 80-320 MiB of the 288 GB."""
+    return max(4 << 20, (XGMI_AR_CAPACITY // max(1, world) + 4095) // 4096 * 4096)
 
 
 def make_xgmi_comm(tp: TPGroup, slot_bytes: Optional[int] = None, blocks: Optional[int] = None,

@@ -170,7 +170,7 @@ def _check_twoshot(tp, res):
     keep = (xg.ll_max_bytes, xg.twoshot_min_bytes)
     xg.ll_max_bytes, xg.twoshot_min_bytes = 0, 16
     cap = xg.max_allreduce_bytes
-    sizes = sorted({n for n in (1 << 20, 2 << 20, 4 << 20, 8 << 20, cap) if n <= cap})
+    sizes = sorted({n for n in (1 << 20, 2 << 20, 4 << 20, 8 << 20) if n <= cap})
     try:
         for seed, nbytes in enumerate(sizes):
             n = nbytes // 2
