@@ -1,10 +1,11 @@
-# GPU steps on one MI355X, chosen by RUNS (space-separated): tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b tune8b proftp8 fp8tp4 tunefp8 minmi.
+# GPU steps on one MI355X, chosen by RUNS (space-separated): sgemv sgprobe b4 b8 arr3 sg0b8 proffp8b64 selflaunch
+# tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b tune8b proftp8 fp8tp4 tunefp8 minmi.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
-# (any other rc) ends the script.  Logs land in gpurun_out/r3/.
+# (any other rc) ends the script.  Logs land in gpurun_out/$OUT (default r4).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/r3; mkdir -p $O
+O=gpurun_out/${OUT:-r4}; mkdir -p $O
 step() {  # step <seconds> <log> <cmd...>
   local t=$1 log=$2; shift 2
   timeout -k 10 "$t" "$@" > "$O/$log" 2>&1
@@ -15,6 +16,22 @@ step() {  # step <seconds> <log> <cmd...>
 }
 for spec in ${RUNS:-tests smoke bench}; do
   case $spec in
+    sgemv) step 300 sgemv_tests.log python -u -m pytest tests/test_sgemv_gpu.py -x -q --timeout 200 --timeout-method thread
+           tail -3 $O/sgemv_tests.log ;;
+    sgprobe) step 300 sgemv_probe.txt python -u tools/sgemv_probe.py 5
+           grep -v amdgpu.ids $O/sgemv_probe.txt ;;
+    b4) step 400 bench_b4.json python -u bench.py --batch 4 --steps 4 --warmup 1
+           grep -h '"metric"' $O/bench_b4.json | cut -c1-300; grep -ho '"decode_ms_per_step": [0-9.]*' $O/bench_b4.json ;;
+    b8) step 400 bench_b8.json python -u bench.py --batch 8 --steps 4 --warmup 1
+           grep -h '"metric"' $O/bench_b8.json | cut -c1-300; grep -ho '"decode_ms_per_step": [0-9.]*' $O/bench_b8.json ;;
+    sg0b8) for b in 4 8; do K8S_SGEMV=0 step 400 bench_b${b}_nosgemv.json python -u bench.py --batch $b --steps 4 --warmup 1
+           grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*' $O/bench_b${b}_nosgemv.json | tr '\n' ' '; echo " (batch $b, mgemm)"; done ;;
+    arr3) step 600 bench_arrivals3.json python -u bench.py --arrival-rate 3 --batch 16 --steps 40 --warmup 4
+           grep -h '"metric"' $O/bench_arrivals3.json | cut -c1-900 ;;
+    proffp8b64) bash tools/gpu_prof.sh tp1_fp8_b64 "--dtype fp8 --batch 64" > $O/proffp8b64.log 2>&1 || { tail -20 $O/proffp8b64.log; exit 1; }
+          head -24 gpurun_out/rocprof_70b_tp1_fp8_b64_kernels.txt ;;
+    selflaunch) step 600 selflaunch.log python -u -m pytest tests/test_multigpu.py -x -q -k "self_launch or share_one_gpu" --timeout 500 --timeout-method thread
+           tail -3 $O/selflaunch.log ;;
     tests) step 600 gputests.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
            tail -3 $O/gputests.log ;;
     ktests) step 300 ktests.log python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread
