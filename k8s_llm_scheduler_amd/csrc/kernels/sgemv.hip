@@ -23,7 +23,7 @@ namespace k8sllm {
 
 namespace {
 
-constexpr int SG_BAND = 64;   // output rows per workgroup band (LDS partials: KW x 2*BAND x MT floats)
+constexpr int SG_BAND = 64;   // most output rows per workgroup band (LDS partials: KW x 2*BAND x MT floats)
 enum SgEpi { SG_BF16 = 0, SG_F32 = 1, SG_SWIGLU = 2 };
 
 __device__ __forceinline__ float sg_dot2(uint32_t w, uint32_t x, float acc) {
@@ -94,7 +94,7 @@ template <int MT, int KPW, int KW, int EPI, bool NORM, bool RES, bool FP8>
 __global__ void __launch_bounds__(256) sgemv_kernel(void* __restrict__ out, float* __restrict__ part,
                                                      const bf16_t* __restrict__ x, const void* __restrict__ W,
                                                      const float* __restrict__ wscale, const bf16_t* res, int M,
-                                                     int N, int K, float eps, int half_rows) {
+                                                     int N, int K, float eps, int half_rows, int band_rows) {
   constexpr int EPC = FP8 ? 16 : 8;            // elements per 16-byte weight chunk
   constexpr int CPL = KPW / (64 * EPC);         // chunks per lane
   constexpr int XV = FP8 ? 2 : 1;               // x vectors (u32x4) per chunk and row
@@ -114,8 +114,8 @@ __global__ void __launch_bounds__(256) sgemv_kernel(void* __restrict__ out, floa
   const int nch = K / EPC;                      // chunks per weight row
   const int cb = (g * KW + kw) * (64 * CPL);    // this wave's first chunk
   const bool active = cb < nch;
-  const int b0 = blockIdx.x * SG_BAND;
-  const int band = min(SG_BAND, N - b0);
+  const int b0 = blockIdx.x * band_rows;           // band_rows <= SG_BAND (the LDS partials' capacity)
+  const int band = min(band_rows, N - b0);
   const int nsets = (band + NR - 1) / NR;
   const char* Wb = reinterpret_cast<const char*>(W);
   const long long row_bytes = (long long)K * WB;
@@ -316,14 +316,19 @@ extern "C" int k8s_sgemv(void* out, void* partial, const void* x, const void* W,
   // every (epilogue, norm) pair is instantiated; the residual add only with the plain bf16 epilogue
   if (epi < SG_BF16 || epi > SG_SWIGLU) return -1;
   if (has_res && (epi != SG_BF16 || norm)) return -5;
-  const dim3 grid((N + SG_BAND - 1) / SG_BAND, p.g);
+  // rows per workgroup: enough workgroups to put every CU to work (~512 per k-group, 2 per CU), at most SG_BAND;
+  // fewer rows per wave re-read x (L2-resident) more often, so the band never drops below 4 rows
+  const int nr = epi == SG_SWIGLU ? 1 : 2;
+  int band = (N + 511) / 512;
+  band = min(SG_BAND, max(4, (band + nr - 1) / nr * nr));
+  const dim3 grid((N + band - 1) / band, p.g);
   const int half_rows = epi == SG_SWIGLU ? N : 0;
   float* part = p.g > 1 ? (float*)partial : nullptr;
   const bf16_t* xx = (const bf16_t*)x;
   const bf16_t* rr = (const bf16_t*)res;
 #define SGL(MT, KPW, KW, EE, NN, RR, F8)                                                                     \
   sgemv_kernel<MT, KPW, KW, EE, NN, RR, F8><<<grid, 256, 0, stream>>>(out, part, xx, W, wscale, rr, M, N, K, \
-                                                                       eps, half_rows)
+                                                                       eps, half_rows, band)
 #define SG_COMBO(MT, KPW, KW, F8)                                                           \
   if (epi == SG_BF16 && norm) { SGL(MT, KPW, KW, SG_BF16, true, false, F8); }               \
   else if (epi == SG_BF16 && has_res) { SGL(MT, KPW, KW, SG_BF16, false, true, F8); }       \

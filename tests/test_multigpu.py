@@ -170,7 +170,10 @@ def _check_twoshot(tp, res):
     keep = (xg.ll_max_bytes, xg.twoshot_min_bytes)
     xg.ll_max_bytes, xg.twoshot_min_bytes = 0, 16
     cap = xg.max_allreduce_bytes
-    sizes = sorted({n for n in (1 << 20, 2 << 20, 4 << 20, 8 << 20) if n <= cap})
+    # 8 MiB (a 512-token 70B chunk) where the ranks have a GPU each or share one at world <= 4 (eight ranks
+    # time-sharing one GPU spin through every two-shot phase: keep their largest message at 4 MiB)
+    top = 8 << 20 if world <= 4 or torch.cuda.device_count() >= world else 4 << 20
+    sizes = sorted({n for n in (1 << 20, 2 << 20, 4 << 20, 8 << 20) if n <= min(cap, top)})
     try:
         for seed, nbytes in enumerate(sizes):
             n = nbytes // 2
