@@ -38,23 +38,6 @@ __device__ __forceinline__ float sg_dot8(const u32x4& w, const u32x4& x, float a
   acc = sg_dot2(w.z, x.z, acc);
   return sg_dot2(w.w, x.w, acc);
 }
-// 16 e4m3 weights (one dword = 4 weights -> two exact bf16 pairs) against 16 bf16 activations
-__device__ __forceinline__ float sg_dot16_fp8(const u32x4& w, const u32x4& x0, const u32x4& x1, float acc) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const bf16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[j], 1.0f, false);
-    const bf16x2 hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[j], 1.0f, true);
-    const uint32_t xa = j < 2 ? x0[2 * j] : x1[2 * j - 4];
-    const uint32_t xb = j < 2 ? x0[2 * j + 1] : x1[2 * j - 3];
-    bf16x2 a, b;
-    __builtin_memcpy(&a, &xa, 4);
-    __builtin_memcpy(&b, &xb, 4);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(lo, a, acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(hi, b, acc, false);
-  }
-  return acc;
-}
-
 // Halving butterfly over the 64 lanes for CNT values per lane: at xor offset O a lane keeps half of its values
 // (the lower half if bit O of its lane id is clear) and adds the partner's copy of that half.  Once one value is
 // left, the remaining offsets are plain xor sums.  Afterwards value index (lane >> (6 - log2 V)) & (V - 1) of the
@@ -153,12 +136,32 @@ __global__ void __launch_bounds__(256) sgemv_kernel(void* __restrict__ out, floa
 #pragma unroll
     for (int j = 0; j < CPL; ++j)
 #pragma unroll
-      for (int r = 0; r < NRT; ++r)
+      for (int r = 0; r < NRT; ++r) {
+        if constexpr (FP8) {
+          // the 16 e4m3 weights become 8 exact bf16 pairs ONCE, then meet every x row (not once per row)
+          bf16x2 wp[8];
 #pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          if constexpr (FP8) acc[r * MT + m] = sg_dot16_fp8(w[j][r], xr[j][m][0], xr[j][m][1], acc[r * MT + m]);
-          else acc[r * MT + m] = sg_dot8(w[j][r], xr[j][m][0], acc[r * MT + m]);
+          for (int d = 0; d < 4; ++d) {
+            wp[2 * d] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[j][r][d], 1.0f, false);
+            wp[2 * d + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[j][r][d], 1.0f, true);
+          }
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            float a = acc[r * MT + m];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t xw = e < 4 ? xr[j][m][0][e] : xr[j][m][1][e - 4];
+              bf16x2 xb;
+              __builtin_memcpy(&xb, &xw, 4);
+              a = __builtin_amdgcn_fdot2_f32_bf16(wp[e], xb, a, false);
+            }
+            acc[r * MT + m] = a;
+          }
+        } else {
+#pragma unroll
+          for (int m = 0; m < MT; ++m) acc[r * MT + m] = sg_dot8(w[j][r], xr[j][m][0], acc[r * MT + m]);
         }
+      }
     sg_halve<V, 32>(acc, lane);
     if ((lane & ((1 << (6 - LV)) - 1)) == 0) {
       const int idx = (lane >> (6 - LV)) & (V - 1);
