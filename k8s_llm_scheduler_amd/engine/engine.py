@@ -609,6 +609,12 @@ class LLMEngine:
         if not self.use_graphs:
             return
         tp = self.model.tp
+        if tp.world > 1 and not tp.simulate:
+            # every rank arrives (every rank captures at start-up) before any rank starts the warm-up steps, whose
+            # collectives spin on the GPU until every peer has joined: a rank still in its local set-up (model init,
+            # GEMM warm-up) must not share its GPU with peers that are already spinning (ranks time-sharing one GPU
+            # in the rehearsals stalled for the whole xGMI timeout that way)
+            tp.barrier()
         keep, tp.capture_on_xgmi = tp.capture_on_xgmi, True   # RCCL stays out of the graphs (TPGroup._xgmi_ok)
         try:
             with trace("engine.capture_graphs"):
