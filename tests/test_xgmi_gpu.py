@@ -202,7 +202,8 @@ def test_xgmi_two_ranks_one_gpu():
     assert r0["err"] == 0 and r1["err"] == 0
     assert r0["fused_timeout_err"] == 1 << 1, r0["fused_timeout_err"]   # rank 1 never arrived
     assert r0["fused_gemv_ar_shapes"]
-    assert r0["twoshot_sizes"] == [1 << 20]
+    # the default slots (max(4 MiB, 8 MiB / W)): two-shot capacity 8 MiB at TP=2, so a 512-token 70B chunk fits
+    assert r0["twoshot_sizes"] == [1 << 20, 2 << 20, 4 << 20, 8 << 20]
     assert r0["prefill_err"] < 0.05 * r0["logit_scale"] + 0.05
     assert r0["decode_err"] < 0.05 * r0["logit_scale"] + 0.05
     assert r0["tokens"] == r1["tokens"]          # replicated sampling from identical gathered logits
