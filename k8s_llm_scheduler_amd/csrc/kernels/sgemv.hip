@@ -171,9 +171,24 @@ __global__ void __launch_bounds__(256) sgemv_kernel(void* __restrict__ out, floa
     }
   };
 
+  // the first row set's weights go out right behind the x loads, unconditionally (rows and chunks are clamped, so a
+  // wave with no set or no slice reads valid bytes it ignores): a branch here let the compiler sink them below the
+  // norm prologue, which then waited for every x load before a single weight byte was requested
   u32x4 wa[CPL][NRT], wb[CPL][NRT];
   int q = rg;
-  if (active && q < nsets) load_set(wa, q);
+  asm volatile("" ::: "memory");   // every x load is issued before the first weight load (in-order retirement)
+  load_set(wa, q);
+  asm volatile("" ::: "memory");
+  // and the x registers become opaque only here, so nothing that reads them (the norm's sum of squares) can be
+  // scheduled above the weight loads: its wait is then for the x loads only (counted: the weights stay in flight)
+  if constexpr (NORM) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int v = 0; v < XV; ++v) asm volatile("" : "+v"(xr[j][m][v]));
+  }
 
   if constexpr (NORM) {   // sum of squares of each live x row over this wave's slice (the weights are in flight)
     float ss[MT];
