@@ -17,6 +17,8 @@
 //    logits, SwiGLU of the [gate; up] halves, or the residual add in place) are applied and stored.
 //  * K longer than one workgroup covers (KW x KPW) is split over G = gridDim.y workgroups: fp32 partial slabs and
 //    sgemv_finalize_kernel (fixed order over the slices + epilogue).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace k8sllm {
@@ -266,6 +268,266 @@ __global__ void __launch_bounds__(256) sgemv_kernel(void* __restrict__ out, floa
   }
 }
 
+// 5..16 decode rows on the MATRIX cores.  At 8 rows the v_dot2 form above issues 32 VALU dot2 per 16 weight bytes
+// (fp8: 72 with the conversions): VALU-bound at ~5 TB/s (fp8 ~3 TB/s), and it cannot hold 16 rows of x.  Here the
+// products run on v_mfma_f32_4x4x4bf16_1k -- 16 independent 4x4x4 blocks, lane 4b + i holding row i of block b
+// (A: weights, items = 4 k; B: x, column j = lane & 3; D: item i of lane 4b + j = D[i][j]; checked on the chip by
+// tools/probes/mfma4_layout.hip) -- so the VALU is free and the kernel is a pure weight stream again:
+//  * one 16-byte-per-lane load covers 4 weight rows x 256 contiguous bytes (lane l: row l & 3, chunk l >> 2): the
+//    16 blocks are 16 consecutive chunks of the same 4 rows, each chunk two (bf16) or four (fp8) k-quads.  That
+//    access shape streams at ~6.2 TB/s where the 16x16x32 MFMA's A operand (16 rows x 64 B per load) manages ~5.0
+//    (tools/probes/ldpat.hip, profiles/sgemv_load_patterns_r4.txt);
+//  * x lives in registers for the whole launch (B operand: x row 4 xg + (l & 3), the same chunks), MT / 4 groups
+//    of 4 rows; fp8 weights become bf16 k-quads with v_cvt_scalef32_pk_bf16_fp8 (x stays bf16, the row scale
+//    lands in the epilogue);
+//  * 512 threads = 8 waves, ALL splitting the workgroup's k range (jw steps of 16 chunks each); the workgroup
+//    walks its band in quads of 4 rows (SwiGLU: gate quads then up quads), register sets of 4 loads (4 KiB per
+//    wave) double-buffered -- the shallow queue streams best (the probe: 4-8 KiB per wave beats 16-32 KiB);
+//  * at the end of a quad the 16 blocks' partial products are summed by a halving butterfly (4 x MT / 4 values per
+//    lane, offsets 32..4) and parked in LDS; after the band the 8 k-slices are summed in a fixed order
+//    (deterministic) and the norm / scale / epilogue applied as in the v_dot2 form;
+//  * band sized for about one workgroup per CU and k-group; steps past a wave's slice and rows past the band are
+//    out of range of the load's buffer (0, no traffic) instead of branches, so every wait is a counted one.
+constexpr int SM_KW = 8;   // waves per workgroup
+
+template <int CNT, int O>
+__device__ __forceinline__ void sm_halve(float* v, int lane) {   // sg_halve that stops at offset 4 (j = lane & 3)
+  if constexpr (O >= 4) {
+    if constexpr (CNT > 1) {
+      const bool up = (lane & O) != 0;
+#pragma unroll
+      for (int i = 0; i < CNT / 2; ++i) {
+        const float give = up ? v[i] : v[i + CNT / 2];
+        const float keep = up ? v[i + CNT / 2] : v[i];
+        v[i] = keep + __shfl_xor(give, O, WAVE);
+      }
+      sm_halve<CNT / 2, O / 2>(v, lane);
+    } else {
+      v[0] += __shfl_xor(v[0], O, WAVE);
+      sm_halve<1, O / 2>(v, lane);
+    }
+  }
+}
+
+template <int MT, int JT, int EPI, bool NORM, bool RES, bool FP8>
+__global__ void __launch_bounds__(512) smfma_kernel(void* __restrict__ out, float* __restrict__ part,
+                                                     const bf16_t* __restrict__ x, const void* __restrict__ W,
+                                                     const float* __restrict__ wscale, const bf16_t* res, int M,
+                                                     int N, int K, float eps, int band_rows, int jw) {
+  constexpr int EPC = FP8 ? 16 : 8;                // k per 16-byte weight chunk
+  constexpr int XG = MT / 4;                       // x groups of 4 rows (the B operand's 4 columns)
+  constexpr int KQ = EPC / 4;                      // k-quads per chunk
+  constexpr int XV = FP8 ? 2 : 1;                  // x u32x4 per chunk and row
+  constexpr int Q = 4;                             // loads per register set
+  constexpr int QPU = JT >= Q ? 1 : Q / JT;        // quads per set
+  constexpr int NSB = JT >= Q ? JT / Q : 1;        // sets per quad block
+  constexpr int QMAX = 512 / MT;                   // quads per workgroup (LDS partials: 64 KiB)
+  constexpr int V = 4 * XG;                        // partial products per lane and quad
+  constexpr int LV = sg_log2<V>();
+  constexpr int WB = FP8 ? 1 : 2;
+  static_assert((JT & (JT - 1)) == 0 && JT <= 8 && V <= 16, "bad smfma configuration");
+  __shared__ float red[SM_KW][QMAX][4][MT];
+  __shared__ float ssw[SM_KW][MT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int kw = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: the step masks below are scalar)
+  const int r4 = lane & 3, cb = lane >> 2;         // row in the quad / x row in the group; chunk = block
+  const int g = blockIdx.y;
+  const int C16 = K / (16 * EPC);                  // steps (16 chunks) per weight row
+  const int sb = (g * SM_KW + kw) * jw;            // this wave's first step
+  const int jv = max(0, min(jw, C16 - sb));        // its live steps (0: a slice past K)
+  const int b0 = blockIdx.x * band_rows;
+  const int band = min(band_rows, N - b0);
+  const int qg = (band + 3) >> 2;                  // quads of output rows
+  const int nq = (EPI == SG_SWIGLU) ? 2 * qg : qg;
+  const unsigned row_bytes = (unsigned)K * WB;
+  constexpr unsigned OOB = 0x80000000u;            // past every buffer below: the load returns 0, no traffic
+
+  // ---- x -> registers: xr[s][xg] = x[4 xg + r4][chunk 16 (sb + s) + cb]; rows >= M / dead steps read 0
+  u32x4 xr[JT][XG][XV];
+  {
+    const auto xs = sg_rsrc(x, (long long)M * K * 2);
+#pragma unroll
+    for (int s = 0; s < JT; ++s)
+#pragma unroll
+      for (int xg = 0; xg < XG; ++xg) {
+        const unsigned off =
+            s < jv ? (unsigned)(4 * xg + r4) * K * 2 + (unsigned)(16 * (sb + s) + cb) * EPC * 2 : OOB;
+#pragma unroll
+        for (int v = 0; v < XV; ++v) xr[s][xg][v] = __builtin_amdgcn_raw_buffer_load_b128(xs, off + 16 * v, 0, 0);
+      }
+  }
+
+  // the band's weight rows through one buffer per half (gate rows; SwiGLU: up rows)
+  const char* Wc = reinterpret_cast<const char*>(W);
+  const auto wg = sg_rsrc(Wc + (size_t)b0 * row_bytes, (long long)band * row_bytes);
+  const auto wu = sg_rsrc(Wc + ((EPI == SG_SWIGLU) ? (size_t)(N + b0) * row_bytes : 0),
+                          (EPI == SG_SWIGLU) ? (long long)band * row_bytes : 0);
+  const unsigned lane_off = (unsigned)r4 * row_bytes + (unsigned)(16 * sb + cb) * 16;
+  // element e of set i of quad block qb: (quad, step), both compile-time but the block
+  auto quad_of = [](int qb, int e) { return qb * QPU + (JT >= Q ? 0 : e / JT); };
+  auto step_of = [](int i, int e) { return JT >= Q ? i * Q + e : e % JT; };
+  auto load_set = [&](u32x4 (&w)[Q], int qb, int i) {
+#pragma unroll
+    for (int e = 0; e < Q; ++e) {
+      const int quad = quad_of(qb, e), s = step_of(i, e);
+      const bool up = EPI == SG_SWIGLU && quad >= qg;
+      const unsigned off = s < jv ? (unsigned)(4 * (up ? quad - qg : quad)) * row_bytes + lane_off + 256u * s : OOB;
+      w[e] = __builtin_amdgcn_raw_buffer_load_b128(up ? wu : wg, off, 0, 2);   // (aux 2: non-temporal)
+    }
+  };
+  auto consume = [&](const u32x4 (&w)[Q], int i, f32x4 (&acc)[QPU][XG]) {
+#pragma unroll
+    for (int e = 0; e < Q; ++e) {
+      const int qq = JT >= Q ? 0 : e / JT, s = step_of(i, e);
+#pragma unroll
+      for (int kq = 0; kq < KQ; ++kq) {
+        uint32_t a0, a1;
+        if constexpr (FP8) {
+          a0 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[e][kq], 1.0f, false));
+          a1 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[e][kq], 1.0f, true));
+        } else {
+          a0 = w[e][2 * kq];
+          a1 = w[e][2 * kq + 1];
+        }
+        const bf16x4 a = __builtin_bit_cast(bf16x4, (uint2){a0, a1});
+#pragma unroll
+        for (int xg = 0; xg < XG; ++xg) {
+          const u32x4& xv = xr[s][xg][kq / 2];
+          const bf16x4 b = __builtin_bit_cast(bf16x4, (uint2){xv[2 * (kq & 1)], xv[2 * (kq & 1) + 1]});
+          acc[qq][xg] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(a, b, acc[qq][xg], 0, 0, 0);
+        }
+      }
+    }
+  };
+  auto park = [&](const f32x4 (&acc)[QPU][XG], int qb) {   // sum the 16 blocks, one lane per (row, x row) to LDS
+#pragma unroll
+    for (int qq = 0; qq < QPU; ++qq) {
+      float v[V];
+#pragma unroll
+      for (int xg = 0; xg < XG; ++xg)
+#pragma unroll
+        for (int it = 0; it < 4; ++it) v[xg * 4 + it] = acc[qq][xg][it];
+      sm_halve<V, 32>(v, lane);
+      const int idx = (lane >> (6 - LV)) & (V - 1);
+      if (((lane >> 2) & ((1 << (4 - LV)) - 1)) == 0) red[kw][qb * QPU + qq][idx & 3][4 * (idx >> 2) + r4] = v[0];
+    }
+  };
+
+  u32x4 wbuf[2][Q];
+  asm volatile("" ::: "memory");   // every x load is issued before the first weight load (in-order retirement)
+  load_set(wbuf[0], 0, 0);         // (every launched workgroup has >= 1 quad)
+  asm volatile("" ::: "memory");
+  if constexpr (NORM) {   // sum of squares of each x row over this wave's slice, the first weights in flight
+#pragma unroll
+    for (int s = 0; s < JT; ++s)
+#pragma unroll
+      for (int xg = 0; xg < XG; ++xg)
+#pragma unroll
+        for (int v = 0; v < XV; ++v) asm volatile("" : "+v"(xr[s][xg][v]));
+    float ss[XG];
+#pragma unroll
+    for (int xg = 0; xg < XG; ++xg) {
+      float t = 0.f;
+#pragma unroll
+      for (int s = 0; s < JT; ++s)
+#pragma unroll
+        for (int v = 0; v < XV; ++v)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = lo_bf(xr[s][xg][v][e]), hi = hi_bf(xr[s][xg][v][e]);
+            t += lo * lo + hi * hi;
+          }
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) t += __shfl_xor(t, o, WAVE);
+      ss[xg] = t;
+    }
+    if (lane < 4) {
+#pragma unroll
+      for (int xg = 0; xg < XG; ++xg) ssw[kw][4 * xg + lane] = ss[xg];
+    }
+  }
+
+  // quad blocks two at a time so the register set of every (block, set) pair is a compile-time choice; an odd
+  // count runs a phantom block, and the last block prefetches the (out-of-range) block after it: no load sits
+  // under a branch, so every wait stays a counted one
+  const int nqb = (nq + QPU - 1) / QPU;
+  const int nqbp = (nqb + 1) & ~1;   // (host: nqbp * QPU <= QMAX)
+  for (int qb = 0; qb < nqbp; qb += 2) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int qbc = qb + tt;
+      f32x4 acc[QPU][XG];
+#pragma unroll
+      for (int qq = 0; qq < QPU; ++qq)
+#pragma unroll
+        for (int xg = 0; xg < XG; ++xg) acc[qq][xg] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < NSB; ++i) {
+        const int par = (tt * NSB + i) & 1;
+        const int nb = i + 1 < NSB ? qbc : qbc + 1, ni = i + 1 < NSB ? i + 1 : 0;
+        if (par) load_set(wbuf[0], nb, ni); else load_set(wbuf[1], nb, ni);
+        // the next set's loads go out before this set's MFMAs (and their waits): the barrier keeps the loads
+        // above it, the opaque accumulators (and, for fp8, the current set feeding the conversions) the math below
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int qq = 0; qq < QPU; ++qq)
+#pragma unroll
+          for (int xg = 0; xg < XG; ++xg) asm volatile("" : "+v"(acc[qq][xg]));
+        if constexpr (FP8) {
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            if (par) asm volatile("" : "+v"(wbuf[1][q])); else asm volatile("" : "+v"(wbuf[0][q]));
+          }
+        }
+        if (par) consume(wbuf[1], i, acc); else consume(wbuf[0], i, acc);
+      }
+      park(acc, qbc);
+    }
+  }
+  __syncthreads();
+
+  // ---- combine the 8 k-slices (fixed order), scale, epilogue
+  const int G = gridDim.y;
+  for (int idx = tid; idx < band * M; idx += 512) {
+    const int m = idx / band, lr = idx - m * band;
+    const int n = b0 + lr, qd = lr >> 2, i = lr & 3;
+    float a = 0.f, u = 0.f;
+#pragma unroll
+    for (int k = 0; k < SM_KW; ++k) {
+      a += red[k][qd][i][m];
+      if (EPI == SG_SWIGLU) u += red[k][qg + qd][i][m];
+    }
+    if constexpr (NORM) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < SM_KW; ++k) s += ssw[k][m];
+      const float inv = rsqrtf(s / (float)K + eps);
+      a *= inv;
+      u *= inv;
+    }
+    if constexpr (FP8) {
+      a *= wscale[n];
+      if (EPI == SG_SWIGLU) u *= wscale[N + n];
+    }
+    if (G > 1) {
+      const int wrows = (EPI == SG_SWIGLU) ? 2 * N : N;
+      float* slab = part + ((size_t)g * M + m) * wrows;
+      slab[n] = a;
+      if (EPI == SG_SWIGLU) slab[N + n] = u;
+      continue;
+    }
+    if constexpr (EPI == SG_F32) {
+      reinterpret_cast<float*>(out)[(size_t)m * N + n] = a;
+    } else if constexpr (EPI == SG_SWIGLU) {
+      reinterpret_cast<bf16_t*>(out)[(size_t)m * N + n] = f2bf(a / (1.f + __expf(-a)) * u);
+    } else {
+      if constexpr (RES) a += bf2f(res[(size_t)m * N + n]);
+      reinterpret_cast<bf16_t*>(out)[(size_t)m * N + n] = f2bf(a);
+    }
+  }
+}
+
 template <int EPI, bool RES>
 __global__ void sgemv_finalize_kernel(void* __restrict__ out, const float* __restrict__ part, const bf16_t* res,
                                       int M, int N, int G) {
@@ -311,29 +573,122 @@ SgPlan sg_plan(int K) {
 }
 }  // namespace
 
+// MFMA plan (smfma_kernel): JT register steps per wave (1, 2, 4, 8; a step = 16 chunks of every row of a quad),
+// jw live steps, G k-groups.  Needs whole steps (K % 128 bf16, K % 256 fp8); one k-group covers 8 waves x 8 steps
+// (8192 k) -- fp8 4 steps (8192 k: an fp8 step holds twice the x of a bf16 one).
+struct SmPlan {
+  int jt, jw, g;
+};
+static bool sm_plan(int K, bool fp8, SmPlan& p) {
+  const int epc = fp8 ? 16 : 8;
+  if (K % (16 * epc) != 0) return false;
+  const int c16 = K / (16 * epc), jmax = fp8 ? 4 : 8;
+  const int g = (c16 + SM_KW * jmax - 1) / (SM_KW * jmax);
+  const int jw = (c16 + SM_KW * g - 1) / (SM_KW * g);
+  p = {jw <= 1 ? 1 : (jw <= 2 ? 2 : (jw <= 4 ? 4 : 8)), jw, g};
+  return true;
+}
+// rows from which the matrix-core form takes over from the register dot2 form (K8S_SGEMV_MFMA_MIN_M, default 5;
+// 17 turns it off: 9..16 rows then go back to mgemm)
+static int sm_min_m() {
+  static const int v = [] { const char* e = getenv("K8S_SGEMV_MFMA_MIN_M"); return e ? atoi(e) : 5; }();
+  return v;
+}
+static int sm_cus() {
+  static const int v = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return v;
+}
+static bool sm_take(int M, int K, bool fp8, SmPlan& p) { return M >= sm_min_m() && M <= 16 && sm_plan(K, fp8, p); }
+
 // Workspace floats for the partial slabs (0 when the plan has one k-group).
 extern "C" long long k8s_sgemv_workspace(int M, int N, int K, int epi) {
-  const SgPlan p = sg_plan(K);
-  if (p.g <= 1) return 0;
-  return (long long)p.g * M * (epi == SG_SWIGLU ? 2 : 1) * N;
+  SmPlan sp;
+  int g = sg_plan(K).g;
+  // (the fp8 flag is not known here: size for the larger of the two plans)
+  if (sm_take(M, K, false, sp)) g = sp.g;
+  if (sm_take(M, K, true, sp)) g = max(g, sp.g);
+  if (g <= 1) return 0;
+  return (long long)g * M * (epi == SG_SWIGLU ? 2 : 1) * N;
+}
+
+static void sg_finalize(void* out, float* part, const bf16_t* rr, int M, int N, int G, int epi, bool has_res,
+                        hipStream_t stream) {
+  const int total = M * N, blocks = (total + 255) / 256;
+  if (epi == SG_SWIGLU) sgemv_finalize_kernel<SG_SWIGLU, false><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, G);
+  else if (epi == SG_F32) sgemv_finalize_kernel<SG_F32, false><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, G);
+  else if (has_res) sgemv_finalize_kernel<SG_BF16, true><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, G);
+  else sgemv_finalize_kernel<SG_BF16, false><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, G);
 }
 
 // out [M, N] (bf16, or fp32 for epi 1); x [M, K] bf16; W [N, K] (epi 2: [2N, K], gate rows then up rows) bf16, or
 // e4m3 bytes when wscale != null (fp32 per weight row); res [M, N] bf16 for the residual epilogue (may be out);
-// norm: 1 = multiply by 1/rms of each x row (the norm gamma folded into W).  Returns -5 (nothing launched) for the
-// residual add with another epilogue or with the norm, and for a norm over a K that needs more than one k-group.
+// partial: k8s_sgemv_workspace floats.  norm: scale row m by 1/rms(x[m]) (the gamma folded into W).
+// Returns 0, a negative argument error, or -5 when this kernel does not take the call (the caller routes it to
+// mgemm).
 extern "C" int k8s_sgemv(void* out, void* partial, const void* x, const void* W, const float* wscale, const void* res,
                          int M, int N, int K, int epi, int norm, float eps, hipStream_t stream) {
-  if (M < 1 || M > 8 || N <= 0 || K <= 0) return -1;
+  if (M < 1 || M > 16 || N <= 0 || K <= 0) return -1;
   const bool fp8 = wscale != nullptr;
   if (K % (fp8 ? 16 : 8) != 0) return -1;
-  const SgPlan p = sg_plan(K);
+  if (epi < SG_BF16 || epi > SG_SWIGLU) return -1;
+  const bool has_res = res != nullptr;
+  if (has_res && (epi != SG_BF16 || norm)) return -5;
+  const bf16_t* xx = (const bf16_t*)x;
+  const bf16_t* rr = (const bf16_t*)res;
+  SmPlan sp;
+  if (sm_take(M, K, fp8, sp)) {
+    if (norm && sp.g > 1) return -5;
+    if (sp.g > 1 && partial == nullptr) return -3;
+    // ~one 512-thread workgroup per CU and k-group, at least 16 rows (x is re-read per workgroup), at most the LDS
+    // partials' quads (SwiGLU: gate + up quads, with the phantom rounding)
+    const int mt = M <= 8 ? 8 : 16, qmax = 512 / mt;
+    const int bandmax = 4 * qmax / (epi == SG_SWIGLU ? 2 : 1);
+    const int per = max(1, sm_cus() / sp.g);
+    int band = max(min(16, N), (N + per - 1) / per);
+    if (band > bandmax) {
+      int nb = (N + bandmax - 1) / bandmax;
+      nb = (nb + per - 1) / per * per;   // whole rounds of workgroups
+      band = (N + nb - 1) / nb;
+    }
+    const dim3 grid((N + band - 1) / band, sp.g);
+    float* part = sp.g > 1 ? (float*)partial : nullptr;
+#define SMK(MT, JT, EE, NN, RR, F8)                                                                   \
+  smfma_kernel<MT, JT, EE, NN, RR, F8><<<grid, 512, 0, stream>>>(out, part, xx, W, wscale, rr, M, N, K, \
+                                                                 eps, band, sp.jw)
+#define SMK_COMBO(MT, JT, F8)                                                           \
+  if (epi == SG_BF16 && norm) { SMK(MT, JT, SG_BF16, true, false, F8); }                \
+  else if (epi == SG_BF16 && has_res) { SMK(MT, JT, SG_BF16, false, true, F8); }        \
+  else if (epi == SG_BF16) { SMK(MT, JT, SG_BF16, false, false, F8); }                  \
+  else if (epi == SG_SWIGLU && norm) { SMK(MT, JT, SG_SWIGLU, true, false, F8); }       \
+  else if (epi == SG_SWIGLU) { SMK(MT, JT, SG_SWIGLU, false, false, F8); }              \
+  else if (norm) { SMK(MT, JT, SG_F32, true, false, F8); }                              \
+  else { SMK(MT, JT, SG_F32, false, false, F8); }
+#define SMK_JT(MT)                                           \
+  if (fp8) {   /* (sm_plan keeps fp8 at <= 4 steps) */      \
+    if (sp.jt == 1) { SMK_COMBO(MT, 1, true) }               \
+    else if (sp.jt == 2) { SMK_COMBO(MT, 2, true) }          \
+    else { SMK_COMBO(MT, 4, true) }                          \
+  } else if (sp.jt == 1) { SMK_COMBO(MT, 1, false) }         \
+  else if (sp.jt == 2) { SMK_COMBO(MT, 2, false) }           \
+  else if (sp.jt == 4) { SMK_COMBO(MT, 4, false) }           \
+  else { SMK_COMBO(MT, 8, false) }
+    if (mt == 8) { SMK_JT(8) } else { SMK_JT(16) }
+#undef SMK_JT
+#undef SMK_COMBO
+#undef SMK
+    if (sp.g > 1) sg_finalize(out, part, rr, M, N, sp.g, epi, has_res, stream);
+    return (int)hipGetLastError();
+  }
+  if (M > 8) return -5;
+  SgPlan p = sg_plan(K);
   if (norm && p.g > 1) return -5;
   if (p.g > 1 && partial == nullptr) return -3;
-  const bool has_res = res != nullptr;
-  // every (epilogue, norm) pair is instantiated; the residual add only with the plain bf16 epilogue
-  if (epi < SG_BF16 || epi > SG_SWIGLU) return -1;
-  if (has_res && (epi != SG_BF16 || norm)) return -5;
   // rows per workgroup: enough workgroups to put every CU to work (~512 per k-group, 2 per CU), at most SG_BAND;
   // fewer rows per wave re-read x (L2-resident) more often, so the band never drops below 4 rows
   const int nr = epi == SG_SWIGLU ? 1 : 2;
@@ -342,8 +697,6 @@ extern "C" int k8s_sgemv(void* out, void* partial, const void* x, const void* W,
   const dim3 grid((N + band - 1) / band, p.g);
   const int half_rows = epi == SG_SWIGLU ? N : 0;
   float* part = p.g > 1 ? (float*)partial : nullptr;
-  const bf16_t* xx = (const bf16_t*)x;
-  const bf16_t* rr = (const bf16_t*)res;
 #define SGL(MT, KPW, KW, EE, NN, RR, F8)                                                                     \
   sgemv_kernel<MT, KPW, KW, EE, NN, RR, F8><<<grid, 256, 0, stream>>>(out, part, xx, W, wscale, rr, M, N, K, \
                                                                        eps, half_rows, band)
@@ -367,12 +720,6 @@ extern "C" int k8s_sgemv(void* out, void* partial, const void* x, const void* W,
 #undef SG_PLAN
 #undef SG_COMBO
 #undef SGL
-  if (p.g > 1) {
-    const int total = M * N, blocks = (total + 255) / 256;
-    if (epi == SG_SWIGLU) sgemv_finalize_kernel<SG_SWIGLU, false><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, p.g);
-    else if (epi == SG_F32) sgemv_finalize_kernel<SG_F32, false><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, p.g);
-    else if (has_res) sgemv_finalize_kernel<SG_BF16, true><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, p.g);
-    else sgemv_finalize_kernel<SG_BF16, false><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, p.g);
-  }
+  if (p.g > 1) sg_finalize(out, part, rr, M, N, p.g, epi, has_res, stream);
   return (int)hipGetLastError();
 }

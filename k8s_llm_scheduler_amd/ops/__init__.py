@@ -266,8 +266,10 @@ if not 1 <= GEMV_MAX_M <= GEMV_KERNEL_MAX_M:
 
 
 # Small decode batches, GEMV_MAX_M < rows <= SGEMV_MAX_M: csrc/kernels/sgemv.hip (x in registers, every weight
-# streamed once, the RMS statistics and the residual add / SwiGLU fused).  K8S_SGEMV=0 sends them to mgemm instead.
-SGEMV_MAX_M = GEMV_KERNEL_MAX_M if os.environ.get("K8S_SGEMV", "1") != "0" else 0
+# streamed once, the RMS statistics and the residual add / SwiGLU fused; 3..4 rows on v_dot2, 5..16 on the matrix
+# cores).  K8S_SGEMV=0 sends them to mgemm instead.
+SGEMV_KERNEL_MAX_M = 16
+SGEMV_MAX_M = SGEMV_KERNEL_MAX_M if os.environ.get("K8S_SGEMV", "1") != "0" else 0
 
 
 def _sgemv(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,

@@ -1,4 +1,4 @@
-"""sgemv.hip (small decode batches, 3..8 rows, x in registers) against the fp32 PyTorch oracle: every epilogue
+"""sgemv.hip (small decode batches: 3..4 rows on v_dot2, 5..16 rows on the matrix cores; x in registers) against the fp32 PyTorch oracle: every epilogue
 (bf16, fp32 logits, SwiGLU, residual add in place) with and without the folded-norm 1/rms prologue, bf16 and row-scaled
 e4m3 weights (bf16 activations: sgemv never quantizes them), ragged N / K, every launch plan (1024-element slices,
 2048-element slices split 2 or 4 ways, k-groups with partial slabs + finalize), the Llama-3.3-70B projection shapes at
@@ -66,6 +66,20 @@ def test_every_epilogue_ragged(M, epi, norm, with_res, fp8):
 
 
 @pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("epi,norm,with_res", [(ops.EPI_BF16, False, False), (ops.EPI_BF16, True, False),
+                                               (ops.EPI_BF16, False, True), (ops.EPI_F32, True, False),
+                                               (ops.EPI_SWIGLU, True, False), (ops.EPI_SWIGLU, False, False)])
+@pytest.mark.parametrize("M,K", [(5, 1024), (8, 3584), (9, 8192), (16, 1024), (12, 12288), (16, 28672)])
+def test_matrix_core_rows(M, K, epi, norm, with_res, fp8):
+    """5..16 rows on the matrix-core form: both x layouts (<= 8 rows: odd steps parked in lanes 8..15; 9..16 rows),
+    8 / 16 / 32 register steps, a ragged band (N = 300), masked steps of the last wave (K = 3584) and k-groups with
+    partial slabs (12288, 28672; the norm prologue needs one k-group)."""
+    if norm and (K > 8192 or (fp8 and K > 8192)):
+        pytest.skip("the norm prologue needs one k-group")
+    _run(M, 300, K, epi, fp8, norm, with_res, seed=M + K)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("K", [1024, 3584, 4096, 6144, 8192, 14336, 28672])
 def test_every_plan(K, fp8):
     """1024-element slices (K <= 1024), 2048-element slices split 2 / 4 ways with idle slices (3584, 6144), and the
@@ -87,7 +101,7 @@ def test_every_plan(K, fp8):
 ])
 @pytest.mark.parametrize("fp8", [False, True])
 def test_llama70b_shapes(name, N, K, epi, norm, with_res, fp8):
-    for M in (4, 8):
+    for M in (4, 8, 16):
         _run(M, N, K, epi, fp8, norm, with_res, seed=M)
 
 
@@ -101,8 +115,8 @@ def test_deterministic():
 
 
 def test_ops_route_small_batches_to_sgemv(monkeypatch):
-    """3..8 rows: linear_rms (norm prologue; fp8 too, bf16 activations), linear_residual and linear go to sgemv; 2 rows
-    stay on the GEMV, 9 rows go to mgemm."""
+    """3..16 rows: linear_rms (norm prologue; fp8 too, bf16 activations), linear_residual and linear go to sgemv;
+    2 rows stay on the GEMV, 17 rows go to mgemm."""
     nat = ops.native()
     calls = []
     orig = nat.sgemv
@@ -115,11 +129,11 @@ def test_ops_route_small_batches_to_sgemv(monkeypatch):
     K, N = 2048, 512
     for fp8 in (False, True):
         w = _weights(N, K, fp8, 5)
-        for M in (2, 3, 8, 9):
+        for M in (2, 3, 8, 16, 17):
             x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
             ops.linear_rms(x, w, 1e-5)
             ops.linear(x, w)
             r = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
             ops.linear_residual(x, w, r)
     torch.cuda.synchronize()
-    assert sorted(set(calls)) == [3, 8] and len(calls) == 2 * 2 * 3
+    assert sorted(set(calls)) == [3, 8, 16] and len(calls) == 2 * 3 * 3

@@ -1,0 +1,125 @@
+// Load-pattern probe: HBM read rate of a 128 MiB bf16 matrix [8192 x 8192] streamed by 256 workgroups x 8 waves
+// (band of 32 rows per workgroup, each wave a 2 KiB k-slice of every row), where one 16-byte-per-lane load
+// instruction covers R rows x (1024 / R) contiguous bytes (R = 16: the matrix-core sgemv's A operand, R = 1: the
+// v_dot2 sgemv's), D loads per batch, and (MF) one dependent v_mfma_f32_16x16x32_bf16 per load, with the next
+// batch's loads issued before the current one is consumed (double buffer) when DB.  Prints GB/s.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+template <int R, int D, int MF, bool DB>
+__global__ void __launch_bounds__(512) stream(const char* __restrict__ W, unsigned* out, int K2, int band) {
+  const int lane = threadIdx.x & 63, kw = threadIdx.x >> 6;
+  const int lpr = 64 / R;
+  const int rin = lane / lpr, col = (lane % lpr) * 16;
+  const int seg = 1024 / R, per = 2048 / seg;
+  const char* base = W + (size_t)blockIdx.x * band * K2 + kw * 2048;
+  u32x4 acc = {0, 0, 0, 0};
+  f32x4 fa = {0.f, 0.f, 0.f, 0.f};
+  f32x4 fb[4] = {};
+  const u32x4 xb = {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
+  auto addr = [&](int q) {
+    const int rg = q / per, c = q % per;
+    return reinterpret_cast<const u32x4*>(base + (size_t)(rg * R + rin) * K2 + col + c * seg);
+  };
+  auto use = [&](const u32x4 (&v)[D]) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      if constexpr (MF == 1) {
+        fa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, v[u]), __builtin_bit_cast(bf16x8, xb),
+                                                      fa, 0, 0, 0);
+      } else if constexpr (MF >= 2) {   // MF = rows of x / 4: 4x4x4 16-block MFMAs, 2 k-quads per 16-byte chunk
+        const bf16x8 a8 = __builtin_bit_cast(bf16x8, v[u]);
+        const bf16x4 lo = {a8[0], a8[1], a8[2], a8[3]}, hi = {a8[4], a8[5], a8[6], a8[7]};
+        const bf16x8 b8 = __builtin_bit_cast(bf16x8, xb);
+        const bf16x4 xl = {b8[0], b8[1], b8[2], b8[3]};
+#pragma unroll
+        for (int g = 0; g < MF - 1; ++g) {
+          fb[g] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(lo, xl, fb[g], 0, 0, 0);
+          fb[g] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(hi, xl, fb[g], 0, 0, 0);
+        }
+      } else
+        acc ^= v[u];
+    }
+  };
+  const int nq = 2 * band;
+  if constexpr (DB) {
+    u32x4 va[D], vb[D];
+#pragma unroll
+    for (int u = 0; u < D; ++u) va[u] = __builtin_nontemporal_load(addr(u));
+    for (int q0 = 0; q0 < nq; q0 += 2 * D) {
+#pragma unroll
+      for (int u = 0; u < D; ++u) vb[u] = __builtin_nontemporal_load(addr(min(q0 + D + u, nq - 1)));
+      asm volatile("" ::: "memory");
+      asm volatile("" : "+v"(fa), "+v"(acc), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
+      use(va);
+#pragma unroll
+      for (int u = 0; u < D; ++u) va[u] = __builtin_nontemporal_load(addr(min(q0 + 2 * D + u, nq - 1)));
+      asm volatile("" ::: "memory");
+      asm volatile("" : "+v"(fa), "+v"(acc), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
+      use(vb);
+    }
+  } else {
+    for (int q0 = 0; q0 < nq; q0 += D) {
+      u32x4 v[D];
+#pragma unroll
+      for (int u = 0; u < D; ++u) v[u] = __builtin_nontemporal_load(addr(q0 + u));
+      use(v);
+    }
+  }
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u || fa.x == 1234.5f || fb[0].x + fb[1].y + fb[2].z + fb[3].w == 1234.5f) out[threadIdx.x] = acc.x;
+}
+
+template <int R, int D, int MF, bool DB>
+double gbs(const char* W, unsigned* out, int N, int K2, int band) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  float best = 1e9f;
+  for (int it = 0; it < 6; ++it) {
+    (void)hipEventRecord(a);
+    stream<R, D, MF, DB><<<N / band, 512>>>(W, out, K2, band);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms;
+    (void)hipEventElapsedTime(&ms, a, b);
+    if (it > 0 && ms < best) best = ms;
+  }
+  return (double)N * K2 / best / 1e6;
+}
+
+int main() {
+  const int N = 8192, K2 = 8192 * 2, band = 32;
+  char* W;
+  unsigned* out;
+  if (hipMalloc(&W, (size_t)N * K2) != hipSuccess || hipMalloc(&out, 4096) != hipSuccess) return 1;
+  (void)hipMemset(W, 0, (size_t)N * K2);
+  (void)hipDeviceSynchronize();
+  printf("single batch      D=8: R1 %.0f R4 %.0f R16 %.0f | D=16: R1 %.0f R4 %.0f R16 %.0f | D=32: R1 %.0f R4 %.0f R16 %.0f\n",
+         gbs<1, 8, 0, false>(W, out, N, K2, band), gbs<4, 8, 0, false>(W, out, N, K2, band),
+         gbs<16, 8, 0, false>(W, out, N, K2, band), gbs<1, 16, 0, false>(W, out, N, K2, band),
+         gbs<4, 16, 0, false>(W, out, N, K2, band), gbs<16, 16, 0, false>(W, out, N, K2, band),
+         gbs<1, 32, 0, false>(W, out, N, K2, band), gbs<4, 32, 0, false>(W, out, N, K2, band),
+         gbs<16, 32, 0, false>(W, out, N, K2, band));
+  printf("double buffer     D=8: R1 %.0f R4 %.0f R16 %.0f | D=16: R1 %.0f R4 %.0f R16 %.0f\n",
+         gbs<1, 8, 0, true>(W, out, N, K2, band), gbs<4, 8, 0, true>(W, out, N, K2, band),
+         gbs<16, 8, 0, true>(W, out, N, K2, band), gbs<1, 16, 0, true>(W, out, N, K2, band),
+         gbs<4, 16, 0, true>(W, out, N, K2, band), gbs<16, 16, 0, true>(W, out, N, K2, band));
+  printf("double buf + MFMA D=8: R1 %.0f R4 %.0f R16 %.0f | D=16: R1 %.0f R4 %.0f R16 %.0f\n",
+         gbs<1, 8, 1, true>(W, out, N, K2, band), gbs<4, 8, 1, true>(W, out, N, K2, band),
+         gbs<16, 8, 1, true>(W, out, N, K2, band), gbs<1, 16, 1, true>(W, out, N, K2, band),
+         gbs<4, 16, 1, true>(W, out, N, K2, band), gbs<16, 16, 1, true>(W, out, N, K2, band));
+  printf("db + 4x4x4, 8 rows  D=4: R4 %.0f | D=8: R4 %.0f | D=12: R4 %.0f\n", gbs<4, 4, 3, true>(W, out, N, K2, band),
+         gbs<4, 8, 3, true>(W, out, N, K2, band), gbs<4, 12, 3, true>(W, out, N, K2, band));
+  printf("db + 4x4x4, 16 rows D=4: R4 %.0f | D=8: R4 %.0f | D=12: R4 %.0f\n", gbs<4, 4, 5, true>(W, out, N, K2, band),
+         gbs<4, 8, 5, true>(W, out, N, K2, band), gbs<4, 12, 5, true>(W, out, N, K2, band));
+  printf("single + 4x4x4, 8 rows D=8: R4 %.0f | D=16: R4 %.0f\n", gbs<4, 8, 3, false>(W, out, N, K2, band),
+         gbs<4, 16, 3, false>(W, out, N, K2, band));
+  (void)hipFree(W);
+  (void)hipFree(out);
+  return 0;
+}

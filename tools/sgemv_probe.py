@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""sgemv.hip vs mgemm.hip at small decode batches (3..8 rows) on the Llama-3.3-70B projection shapes (TP = 1 and
+"""sgemv.hip vs mgemm.hip at small decode batches (4, 8, 16 rows) on the Llama-3.3-70B projection shapes (TP = 1 and
 TP = 8, bf16 and fp8 weights), interleaved rounds in one process, cold weights (a 512 MiB scrub between calls so the
 weights come from HBM as in a decode step).  Prints us per call and the weight-streaming rate.
 
@@ -46,7 +46,7 @@ for fp8 in (False, True):
         if fp8:
             w = ops.quantize_fp8(w)
         wbytes = rows * K * (1 if fp8 else 2)
-        for M in (4, 8):
+        for M in (4, 8, 16):
             x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
             r = torch.zeros(M, N, dtype=torch.bfloat16, device=dev) if res else None
             eps = 1e-5 if norm else None
