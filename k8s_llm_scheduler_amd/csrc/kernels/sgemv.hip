@@ -588,10 +588,12 @@ static bool sm_plan(int K, bool fp8, SmPlan& p) {
   p = {jw <= 1 ? 1 : (jw <= 2 ? 2 : (jw <= 4 ? 4 : 8)), jw, g};
   return true;
 }
-// rows from which the matrix-core form takes over from the register dot2 form (K8S_SGEMV_MFMA_MIN_M, default 5;
-// 17 turns it off: 9..16 rows then go back to mgemm)
+// rows from which the matrix-core form takes over from the register dot2 form (K8S_SGEMV_MFMA_MIN_M, default 3:
+// every sgemv row count -- at 4 rows it ties or beats the dot2 form, profiles/sgemv_mfma4_kernel_trace_r4.txt; 5
+// keeps 3..4 rows on dot2; 17 turns it off: 9..16 rows then go back to mgemm).  The dot2 form remains the path
+// for K that is not a whole number of 16-chunk steps.
 static int sm_min_m() {
-  static const int v = [] { const char* e = getenv("K8S_SGEMV_MFMA_MIN_M"); return e ? atoi(e) : 5; }();
+  static const int v = [] { const char* e = getenv("K8S_SGEMV_MFMA_MIN_M"); return e ? atoi(e) : 3; }();
   return v;
 }
 static int sm_cus() {

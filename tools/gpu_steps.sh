@@ -1,4 +1,4 @@
-# GPU steps on one MI355X, chosen by RUNS (space-separated): sgemv sgprobe sgprobe0 mfma0b8 b16 b4 b8 arr3 sg0b8 proffp8b64 selflaunch
+# GPU steps on one MI355X, chosen by RUNS (space-separated): sgemv sgprobe sgprobe0 mfma0b8 b4m3 b16 b4 b8 arr3 sg0b8 proffp8b64 selflaunch
 # tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b tune8b proftp8 fp8tp4 tunefp8 minmi.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
 # (any other rc) ends the script.  Logs land in gpurun_out/$OUT (default r4).
@@ -24,6 +24,8 @@ for spec in ${RUNS:-tests smoke bench}; do
            grep -v amdgpu.ids $O/sgemv_probe_nomfma.txt | grep M=8 ;;
     mfma0b8) K8S_SGEMV_MFMA_MIN_M=17 step 400 bench_b8_nomfma.json python -u bench.py --batch 8 --steps 4 --warmup 1
            grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*' $O/bench_b8_nomfma.json | tr '\n' ' '; echo " (batch 8, sgemv v_dot2 form)" ;;
+    b4m3) K8S_SGEMV_MFMA_MIN_M=3 step 400 bench_b4_mfma.json python -u bench.py --batch 4 --steps 4 --warmup 1
+           grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*' $O/bench_b4_mfma.json | tr '\n' ' '; echo " (batch 4, sgemv MFMA form)" ;;
     b16) step 400 bench_b16.json python -u bench.py --batch 16 --steps 4 --warmup 1
            grep -h '"metric"' $O/bench_b16.json | cut -c1-300; grep -ho '"decode_ms_per_step": [0-9.]*' $O/bench_b16.json ;;
     b4) step 400 bench_b4.json python -u bench.py --batch 4 --steps 4 --warmup 1

@@ -9,7 +9,7 @@ for M in ${MS:-8 16}; do
     tag=m${M}_f${form}
     M=$M K8S_SGEMV_MFMA_MIN_M=$form timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/$tag -o run -- python3 tools/probes/sm_trace.py > $O/$tag.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { echo "$tag rc=$rc"; tail -5 $O/$tag.log; exit $rc; }
-    echo "== M=$M form=$( [ $form -le 8 ] && echo mfma || echo dot2 )"
+    echo "== M=$M form=$( [ $form -le $M ] && echo mfma || echo dot2 )"
     python3 tools/probes/sm_trace_parse.py $(ls $O/$tag/*kernel_trace.csv $O/$tag/*/*kernel_trace.csv 2>/dev/null | head -1) $O/$tag.log
   done
 done
