@@ -106,6 +106,7 @@ class EngineSection:
     max_batch: int = 64
     max_model_len: int = 16384
     max_prefill_tokens: int = 8192     # chunked-prefill token budget per step
+    mixed_step_rows: int = 256         # rows (prompt tokens + riding decodes) of a mixed step; 0 = no cap
     cuda_graphs: bool = True
     prefix_caching: bool = True
     speculative_tokens: int = 0        # prompt-lookup speculative decoding: draft tokens per step (0 = off)

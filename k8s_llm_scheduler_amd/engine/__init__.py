@@ -87,7 +87,7 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
                  max_model_len: int = 16384, max_prefill_tokens: int = 8192, cuda_graphs: bool = True,
                  prefix_caching: bool = True, decode_chunk: int = 4, metrics=None, capture: bool = True, control=None,
                  weight_dtype: str = "bf16", capture_nucleus: bool = False, speculative_tokens: int = 0,
-                 watchdog_s: float = 60.0, on_unrecoverable: str = "stay"):
+                 watchdog_s: float = 60.0, on_unrecoverable: str = "stay", mixed_step_rows: int = 256):
     """Model + tokenizer + engine on this rank's GPU (or CPU when no GPU is present).
     ``weight_dtype``: "bf16" or "fp8" (row-scaled e4m3 projection weights).  ``capture_nucleus``:
     decode graphs with the top-p sampler passes too (serving with top_p < 1)."""
@@ -119,7 +119,7 @@ def build_engine(preset: str = "llama-3.3-70b", *, tp=None, device: Optional[str
                     max_prefill_tokens=max_prefill_tokens, cuda_graphs=cuda_graphs, prefix_caching=prefix_caching,
                     decode_chunk=decode_chunk, seed=seed, metrics=metrics, control=control,
                     capture_nucleus=capture_nucleus, speculative_tokens=speculative_tokens, watchdog_s=watchdog_s,
-                    on_unrecoverable=on_unrecoverable)
+                    on_unrecoverable=on_unrecoverable, mixed_step_rows=mixed_step_rows)
     if device.startswith("cuda"):
         warm_gemms(model)
     if capture and eng.use_graphs:
@@ -139,4 +139,5 @@ def engine_from_config(cfg, tp=None, metrics=None, control=None):
                         weight_dtype="fp8" if e.dtype in ("fp8", "fp8_e4m3") else "bf16",
                         capture_nucleus=cfg.llm.top_p < 1.0 and cfg.llm.temperature > 0,
                         speculative_tokens=e.speculative_tokens, decode_chunk=e.decode_chunk,
-                        watchdog_s=e.watchdog_s or float(cfg.llm.timeout), on_unrecoverable=e.on_unrecoverable)
+                        watchdog_s=e.watchdog_s or float(cfg.llm.timeout), on_unrecoverable=e.on_unrecoverable,
+                        mixed_step_rows=e.mixed_step_rows)

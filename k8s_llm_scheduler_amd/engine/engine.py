@@ -56,6 +56,7 @@ BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
 # either way -- the chunk is GEMM-bound, profiles/rocprof_prefill_tp8.txt).  The padding tokens
 # belong to no sequence (cu_q stops at the real length) and write their K/V into a scratch block.
 PREFILL_GRAPH_BUCKETS = (64, 128, 192, 256, 320, 384, 448, 512)
+MIXED_MIN_PROMPT_ROWS = 16   # a mixed step under the row cap still advances its prompts by at least this many tokens
 _P_SPLIT = 6   # packed prefill-graph inputs of the two micro-batch halves: cu_q0 (2), ctx0, cu_q1 (2), ctx1
 
 
@@ -203,7 +204,7 @@ class LLMEngine:
                  prefix_caching: bool = True, decode_chunk: int = 4, seed: int = 0, metrics=None,
                  control=None, capture_nucleus: bool = False, speculative_tokens: int = 0,
                  watchdog_s: float = 60.0, on_unrecoverable: str = "stay", device_stop: bool = True,
-                 mixed_steps: bool = True):
+                 mixed_steps: bool = True, mixed_step_rows: int = 256):
         self.model = model
         # Device-side stop detection: the decode graphs' sampler finishes rows itself (EOS,
         # closed JSON object, max_tokens) and raises a host-mapped flag; the host checks it after every replay
@@ -211,6 +212,12 @@ class LLMEngine:
         # running decode by one token in the same varlen forward, and new arrivals end a decode chunk early.
         self.device_stop = bool(device_stop)
         self.mixed_steps = bool(mixed_steps)
+        # rows of a mixed step's varlen forward (prompt tokens + one per running decode) are kept within this many
+        # (0: no cap), so an arrival's chunk plus the decode rows stays inside the GEMMs' 256-row plans: a 245-token
+        # prompt with 5 decodes riding along is 250 rows (41 ms of GEMMs at 70B TP=1), where 261 rows fell into the
+        # 384-row plans (62 ms, profiles/lastfwd_70b_tp1_arr3_r4.txt); the few prompt tokens over the cap go into
+        # the next step, itself a cheap mixed step
+        self.mixed_step_rows = max(0, int(mixed_step_rows))
         # Bounded device waits: every host wait for device results polls an event against
         # min(call deadline, step start + watchdog_s) instead of blocking in a synchronize, so a hung collective
         # surfaces as EngineStalled inside llm.timeout.  ``on_unrecoverable``: "exit" ends the process (exit code
@@ -931,6 +938,8 @@ class LLMEngine:
         if self._trace_steps:
             self.recovery_trace.append((time.monotonic(), f"prefill: {len(self.prefilling)} requests"))
         budget = self.max_prefill_tokens
+        if self.mixed_steps and self.running and self.mixed_step_rows:
+            budget = min(budget, max(MIXED_MIN_PROMPT_ROWS, self.mixed_step_rows - len(self.running)))
         chunk = []  # (req, start, end)
         for r in self.prefilling:
             if budget <= 0:

@@ -389,3 +389,35 @@ def test_decision_prefill_buckets_stay_on_captured_xgmi(tp):
     assert group._xgmi_ok(chunk, reduce=True)         # captured: xGMI
     assert 10 * tp * slot <= 320 << 20                # the whole peer region stays small next to 288 GB
     assert 64 * (128256 // 8) * 4 <= default_slot_bytes(8)   # TP=8 decode logits gather at batch 64 fits a slot
+
+
+def test_mixed_step_rows_stay_within_the_cap():
+    """engine.mixed_step_rows: a mixed step's rows (prompt tokens + one per running decode) stay within the cap; the
+    prompt tokens over it go into the next step, and the tokens equal the uncapped engine's."""
+    prompt_long = [9, 10, 11, 12] * 12             # 48 prompt tokens
+    params = [SamplingParams(max_tokens=n, temperature=0.0, ignore_eos=True) for n in (60, 60, 12)]
+
+    def run(cap):
+        eng = build_engine("tiny", device="cpu", max_batch=4, max_model_len=256, num_blocks=128, seed=1)
+        eng.mixed_step_rows = cap
+        rows = []
+        orig = eng.model.forward_prefill
+
+        def spy(ids, *a, **k):
+            rows.append(int(ids.shape[0]))
+            return orig(ids, *a, **k)
+
+        eng.model.forward_prefill = spy
+        reqs = [eng.add_request([5, 6, 7], params[0]), eng.add_request([5, 6, 8], params[1])]
+        eng.step()
+        eng.step()
+        reqs.append(eng.add_request(prompt_long, params[2]))
+        while eng.has_work():
+            eng.step()
+        return [r.output_ids for r in reqs], rows, eng.stats["mixed_steps"]
+
+    capped, rows_c, n_c = run(20)
+    free, rows_f, n_f = run(0)
+    assert capped == free
+    assert max(rows_c[1:]) <= 20 and n_c >= 3        # 48 prompt tokens in chunks of 18 beside 2 decodes
+    assert max(rows_f) == 48 + 2 and n_f == 1
