@@ -17,6 +17,7 @@
 //    logits, SwiGLU of the [gate; up] halves, or the residual add in place) are applied and stored.
 //  * K longer than one workgroup covers (KW x KPW) is split over G = gridDim.y workgroups: fp32 partial slabs and
 //    sgemv_finalize_kernel (fixed order over the slices + epilogue).
+#include <atomic>
 #include <cstdlib>
 
 #include "common.h"
@@ -309,11 +310,31 @@ __device__ __forceinline__ void sm_halve(float* v, int lane) {   // sg_halve tha
   }
 }
 
+template <int EPI, bool RES>
+__device__ __forceinline__ void sm_store(void* out, const bf16_t* res, size_t o, float a, float u) {
+  if constexpr (EPI == SG_F32) {
+    reinterpret_cast<float*>(out)[o] = a;
+  } else if constexpr (EPI == SG_SWIGLU) {
+    reinterpret_cast<bf16_t*>(out)[o] = f2bf(a / (1.f + __expf(-a)) * u);
+  } else {
+    if constexpr (RES) a += bf2f(res[o]);
+    reinterpret_cast<bf16_t*>(out)[o] = f2bf(a);
+  }
+}
+
+// Tickets of the in-kernel k-group reduction: zero at load, each range returned to zero by the last workgroup of
+// every launch that used it.  Launches draw ranges of SM_TICKET_RANGE in rotation, so kernels that overlap on
+// different streams do not share counters.
+constexpr int SM_TICKET_RANGE = 256, SM_TICKET_RANGES = 256;
+__device__ unsigned sm_tickets[SM_TICKET_RANGE * SM_TICKET_RANGES];
+
 template <int MT, int JT, int EPI, bool NORM, bool RES, bool FP8>
-__global__ void __launch_bounds__(512) smfma_kernel(void* __restrict__ out, float* __restrict__ part,
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MT == 8 ? 4 : 2)))
+smfma_kernel(void* __restrict__ out, float* __restrict__ part,
                                                      const bf16_t* __restrict__ x, const void* __restrict__ W,
                                                      const float* __restrict__ wscale, const bf16_t* res, int M,
-                                                     int N, int K, float eps, int band_rows, int jw) {
+                                                     int N, int K, float eps, int band_rows, int jw,
+                                                     unsigned* tickets) {
   constexpr int EPC = FP8 ? 16 : 8;                // k per 16-byte weight chunk
   constexpr int XG = MT / 4;                       // x groups of 4 rows (the B operand's 4 columns)
   constexpr int KQ = EPC / 4;                      // k-quads per chunk
@@ -510,22 +531,43 @@ __global__ void __launch_bounds__(512) smfma_kernel(void* __restrict__ out, floa
       a *= wscale[n];
       if (EPI == SG_SWIGLU) u *= wscale[N + n];
     }
-    if (G > 1) {
+    if (G > 1) {   // device-coherent stores (write-through past the XCD's L2): read back by another workgroup
       const int wrows = (EPI == SG_SWIGLU) ? 2 * N : N;
       float* slab = part + ((size_t)g * M + m) * wrows;
-      slab[n] = a;
-      if (EPI == SG_SWIGLU) slab[N + n] = u;
+      __hip_atomic_store(slab + n, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (EPI == SG_SWIGLU) __hip_atomic_store(slab + N + n, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       continue;
     }
-    if constexpr (EPI == SG_F32) {
-      reinterpret_cast<float*>(out)[(size_t)m * N + n] = a;
-    } else if constexpr (EPI == SG_SWIGLU) {
-      reinterpret_cast<bf16_t*>(out)[(size_t)m * N + n] = f2bf(a / (1.f + __expf(-a)) * u);
-    } else {
-      if constexpr (RES) a += bf2f(res[(size_t)m * N + n]);
-      reinterpret_cast<bf16_t*>(out)[(size_t)m * N + n] = f2bf(a);
-    }
+    sm_store<EPI, RES>(out, res, (size_t)m * N + n, a, u);
   }
+  if (G == 1 || tickets == nullptr) return;   // (no tickets: sgemv_finalize_kernel sums the slabs)
+
+  // ---- k-groups: the LAST workgroup of this band to finish sums the G slabs (fixed order, as the finalize kernel
+  // would) and stores the result -- no second launch.  No cache-wide fences: the slab stores above are device-coherent
+  // (write-through), every wave waits for its own stores to land before the workgroup counts its arrival with one
+  // device-scope add, and the last workgroup reads the slabs with device-coherent loads.
+  __shared__ int sm_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab stores have landed
+  __syncthreads();
+  if (tid == 0)
+    sm_last = __hip_atomic_fetch_add(&tickets[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              (unsigned)(G - 1);
+  __syncthreads();
+  if (!sm_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // (compiler ordering: the loads stay below the add)
+  const int wrows = (EPI == SG_SWIGLU) ? 2 * N : N;
+  for (int idx = tid; idx < band * M; idx += 512) {
+    const int m = idx / band, n = b0 + idx - m * band;
+    float a = 0.f, u = 0.f;
+    for (int k = 0; k < G; ++k) {
+      const float* slab = part + ((size_t)k * M + m) * wrows;
+      a += __hip_atomic_load(slab + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (EPI == SG_SWIGLU) u += __hip_atomic_load(slab + N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sm_store<EPI, RES>(out, res, (size_t)m * N + n, a, u);
+  }
+  if (tid == 0)   // ready for the next launch that draws this ticket range
+    __hip_atomic_store(&tickets[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int EPI, bool RES>
@@ -628,6 +670,49 @@ static void sg_finalize(void* out, float* part, const bf16_t* rr, int M, int N, 
   else sgemv_finalize_kernel<SG_BF16, false><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, G);
 }
 
+// Workgroups of the MFMA form per CU the band is sized for: what the kernel's registers allow (8-row x: <= 128
+// VGPRs, 2; 16-row: 1), capped by K8S_SGEMV_WG_PER_CU (default 1: at 2 the 70B QKV / gate/up / down ran 9 / 3 / 3 %
+// slower -- twice the workgroups re-read x -- and O 3 % faster; profiles/sgemv_mfma4_kernel_trace_r4.txt).
+static int sm_wg_cap() {
+  static const int v = [] { const char* e = getenv("K8S_SGEMV_WG_PER_CU"); return e ? max(1, atoi(e)) : 1; }();
+  return v;
+}
+static std::atomic<unsigned> g_sm_next_range{0};   // one rotation for every instantiation (launches on any stream)
+
+template <int MT, int JT, int EE, bool NN, bool RR, bool F8>
+static bool sm_launch(void* out, void* partial, const bf16_t* x, const void* W, const float* wscale, const bf16_t* res,
+                      int M, int N, int K, float eps, const SmPlan& sp, hipStream_t stream) {
+  static const int occ = [] {
+    int n = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&smfma_kernel<MT, JT, EE, NN, RR, F8>),
+                                                     512, 0) != hipSuccess)
+      n = 1;
+    return max(1, min(n, sm_wg_cap()));
+  }();
+  // ~occ workgroups per CU and k-group, at least 16 rows (x is re-read per workgroup), at most the LDS partials'
+  // quads (SwiGLU: gate + up quads, with the phantom rounding)
+  constexpr int qmax = 512 / MT;
+  const int bandmax = 4 * qmax / (EE == SG_SWIGLU ? 2 : 1);
+  const int per = max(1, sm_cus() * occ / sp.g);
+  int band = max(min(16, N), (N + per - 1) / per);
+  if (band > bandmax) {
+    int nb = (N + bandmax - 1) / bandmax;
+    nb = (nb + per - 1) / per * per;   // whole rounds of workgroups
+    band = (N + nb - 1) / nb;
+  }
+  const dim3 grid((N + band - 1) / band, sp.g);
+  float* part = sp.g > 1 ? (float*)partial : nullptr;
+  unsigned* tk = nullptr;   // k-groups: the in-kernel reduction's ticket range (rotating), if the bands fit one
+  if (sp.g > 1 && grid.x <= (unsigned)SM_TICKET_RANGE) {
+    unsigned* base = nullptr;
+    if (hipGetSymbolAddress((void**)&base, HIP_SYMBOL(sm_tickets)) == hipSuccess)
+      tk = base + (size_t)(g_sm_next_range.fetch_add(1) % SM_TICKET_RANGES) * SM_TICKET_RANGE;
+  }
+  smfma_kernel<MT, JT, EE, NN, RR, F8><<<grid, 512, 0, stream>>>(out, part, x, W, wscale, res, M, N, K, eps, band,
+                                                                 sp.jw, tk);
+  return tk != nullptr;
+}
+
 // out [M, N] (bf16, or fp32 for epi 1); x [M, K] bf16; W [N, K] (epi 2: [2N, K], gate rows then up rows) bf16, or
 // e4m3 bytes when wscale != null (fp32 per weight row); res [M, N] bf16 for the residual epilogue (may be out);
 // partial: k8s_sgemv_workspace floats.  norm: scale row m by 1/rms(x[m]) (the gamma folded into W).
@@ -647,22 +732,8 @@ extern "C" int k8s_sgemv(void* out, void* partial, const void* x, const void* W,
   if (sm_take(M, K, fp8, sp)) {
     if (norm && sp.g > 1) return -5;
     if (sp.g > 1 && partial == nullptr) return -3;
-    // ~one 512-thread workgroup per CU and k-group, at least 16 rows (x is re-read per workgroup), at most the LDS
-    // partials' quads (SwiGLU: gate + up quads, with the phantom rounding)
-    const int mt = M <= 8 ? 8 : 16, qmax = 512 / mt;
-    const int bandmax = 4 * qmax / (epi == SG_SWIGLU ? 2 : 1);
-    const int per = max(1, sm_cus() / sp.g);
-    int band = max(min(16, N), (N + per - 1) / per);
-    if (band > bandmax) {
-      int nb = (N + bandmax - 1) / bandmax;
-      nb = (nb + per - 1) / per * per;   // whole rounds of workgroups
-      band = (N + nb - 1) / nb;
-    }
-    const dim3 grid((N + band - 1) / band, sp.g);
-    float* part = sp.g > 1 ? (float*)partial : nullptr;
-#define SMK(MT, JT, EE, NN, RR, F8)                                                                   \
-  smfma_kernel<MT, JT, EE, NN, RR, F8><<<grid, 512, 0, stream>>>(out, part, xx, W, wscale, rr, M, N, K, \
-                                                                 eps, band, sp.jw)
+#define SMK(MT, JT, EE, NN, RR, F8) \
+  g_last = sm_launch<MT, JT, EE, NN, RR, F8>(out, partial, xx, W, wscale, rr, M, N, K, eps, sp, stream)
 #define SMK_COMBO(MT, JT, F8)                                                           \
   if (epi == SG_BF16 && norm) { SMK(MT, JT, SG_BF16, true, false, F8); }                \
   else if (epi == SG_BF16 && has_res) { SMK(MT, JT, SG_BF16, false, true, F8); }        \
@@ -680,11 +751,12 @@ extern "C" int k8s_sgemv(void* out, void* partial, const void* x, const void* W,
   else if (sp.jt == 2) { SMK_COMBO(MT, 2, false) }           \
   else if (sp.jt == 4) { SMK_COMBO(MT, 4, false) }           \
   else { SMK_COMBO(MT, 8, false) }
-    if (mt == 8) { SMK_JT(8) } else { SMK_JT(16) }
+    bool g_last = false;   // (true: the launch reduces its k-groups itself)
+    if (M <= 8) { SMK_JT(8) } else { SMK_JT(16) }
 #undef SMK_JT
 #undef SMK_COMBO
 #undef SMK
-    if (sp.g > 1) sg_finalize(out, part, rr, M, N, sp.g, epi, has_res, stream);
+    if (sp.g > 1 && !g_last) sg_finalize(out, (float*)partial, rr, M, N, sp.g, epi, has_res, stream);
     return (int)hipGetLastError();
   }
   if (M > 8) return -5;

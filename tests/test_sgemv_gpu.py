@@ -137,3 +137,28 @@ def test_ops_route_small_batches_to_sgemv(monkeypatch):
             ops.linear_residual(x, w, r)
     torch.cuda.synchronize()
     assert sorted(set(calls)) == [3, 8, 16] and len(calls) == 2 * 3 * 3
+
+
+def test_k_group_tickets_return_to_zero():
+    """K-group launches reduce their partial slabs in the kernel (the last workgroup of a band sums them, a ticket
+    per band): 600 launches cycle every ticket range twice and stay bitwise equal, also under graph replay."""
+    w = _weights(2 * 1024, 28672, True, 7)
+    x = (torch.rand(8, 28672, device=DEV) * 2 - 1).to(torch.bfloat16)
+    ref0 = ops._sgemv(x, w, ops.EPI_SWIGLU)
+    outs = [ops._sgemv(x, w, ops.EPI_SWIGLU) for _ in range(600)]
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, ref0) for o in outs)
+    exp = _oracle(x, w, ops.EPI_SWIGLU, False, None)
+    assert (ref0.float() - exp).abs().max().item() <= 1e-2 * exp.abs().max().item()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops._sgemv(x, w, ops.EPI_SWIGLU)
+        with torch.cuda.graph(g, stream=s):
+            y = ops._sgemv(x, w, ops.EPI_SWIGLU)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(5):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, ref0)
