@@ -978,7 +978,9 @@ class LLMEngine:
         elif dec:
             d = self._dev(dec, torch.long)
             ctx_d = self.s_ctx.index_select(0, d)
-            pos_d = ctx_d - 1
+            # (a row the device finished has context 0: clamped, it writes into its own first block, which its
+            # request still owns until the host reaps it, instead of indexing block -1)
+            pos_d = (ctx_d - 1).clamp_min(0)
             blk = self.s_bt.index_select(0, d).gather(1, (pos_d // bs).long().unsqueeze(1)).squeeze(1)
             n_p = len(ids)
             ids_t = torch.cat([t(ids), self.s_tokens.index_select(0, d)])
@@ -1374,8 +1376,12 @@ class LLMEngine:
             r.done.set()
         if r.slot >= 0:
             # fill kernels, never a host->device copy: this also runs on error paths while the stream is stalled
-            self.s_ctx[r.slot:r.slot + 1].fill_(0)
-            self.s_steps[r.slot:r.slot + 1].fill_(0)
+            try:
+                self.s_ctx[r.slot:r.slot + 1].fill_(0)
+                self.s_steps[r.slot:r.slot + 1].fill_(0)
+            except Exception as e:   # noqa: BLE001 -- a faulted device: the request still ends (and its caller
+                # returns); the engine goes not-ready and recovery resets every slot before serving again
+                self.health.update(ready=False, reason=f"device error: {e}")
             self.running.pop(r.slot, None)
             if r in self.prefilling:
                 self.prefilling.remove(r)
@@ -1421,6 +1427,12 @@ class LLMEngine:
         if self.prefilling or self.waiting:
             with trace("engine.prefill"):
                 self._prefill()
+            if self.mixed_steps and self.mixed_step_rows and self.running and self.prefilling:
+                # a prompt cut by the mixed-step row cap continues after ONE decode step instead of a whole decode
+                # chunk.  That step is needed: it syncs the rows the device finished (their context is zeroed on
+                # the device), which the next mixed step must not carry as decode rows
+                with trace("engine.decode"):
+                    return self._decode(max_steps=1)
         if self._share_deferred and not any(r.output_ids for r in self.running.values()):
             # requests are waiting for a prefix this step published: admit them before the
             # first decode, so the batch decodes in lock-step (no extra tail of decode steps)

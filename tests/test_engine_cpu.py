@@ -420,4 +420,5 @@ def test_mixed_step_rows_stay_within_the_cap():
     free, rows_f, n_f = run(0)
     assert capped == free
     assert max(rows_c[1:]) <= 20 and n_c >= 3        # 48 prompt tokens in chunks of 18 beside 2 decodes
+    assert rows_c[1:4] == [20, 20, 14]               # one decode step (not a chunk) between a prompt's pieces
     assert max(rows_f) == 48 + 2 and n_f == 1
