@@ -938,12 +938,15 @@ class LLMEngine:
         if self._trace_steps:
             self.recovery_trace.append((time.monotonic(), f"prefill: {len(self.prefilling)} requests"))
         budget = self.max_prefill_tokens
-        if self.mixed_steps and self.running and self.mixed_step_rows:
+        capped = bool(self.mixed_steps and self.running and self.mixed_step_rows)
+        if capped:
             budget = min(budget, max(MIXED_MIN_PROMPT_ROWS, self.mixed_step_rows - len(self.running)))
         chunk = []  # (req, start, end)
         for r in self.prefilling:
             if budget <= 0:
                 break
+            if capped and chunk and len(r.prompt_ids) - r.computed > budget:
+                break   # under the row cap a second prompt joins only whole (a split one costs an extra step)
             n = min(len(r.prompt_ids) - r.computed, budget)
             chunk.append((r, r.computed, r.computed + n))
             budget -= n
