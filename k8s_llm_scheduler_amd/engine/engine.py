@@ -25,6 +25,7 @@ Every TP rank runs the identical deterministic schedule; sampling is determinist
 
 from __future__ import annotations
 
+import gc
 import itertools
 import logging
 from array import array
@@ -623,11 +624,20 @@ class LLMEngine:
             # in the rehearsals stalled for the whole xGMI timeout that way)
             tp.barrier()
         keep, tp.capture_on_xgmi = tp.capture_on_xgmi, True   # RCCL stays out of the graphs (TPGroup._xgmi_ok)
+        # no cyclic garbage collection while graphs are captured: a collection inside a capture can finalize an
+        # unreachable object that owns device resources (another engine's graphs and their private memory pool),
+        # and freeing those is not a capturable call -- the capture fails and the graph destructor aborts the
+        # process (seen once in the GPU suite: an earlier test's engine collected during the next one's capture)
+        gc_on = gc.isenabled()
+        gc.collect()
+        gc.disable()
         try:
             with trace("engine.capture_graphs"):
                 self._capture_graphs(buckets, self.capture_nucleus if nucleus is None else nucleus)
         finally:
             tp.capture_on_xgmi = keep
+            if gc_on:
+                gc.enable()
 
     def _capture_graphs(self, buckets: Optional[Sequence[int]], nucleus: bool) -> None:
         assert not self.running and not self.prefilling, "capture needs an idle engine"
