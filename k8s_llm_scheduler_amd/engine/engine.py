@@ -219,6 +219,7 @@ class LLMEngine:
         # 384-row plans (62 ms, profiles/lastfwd_70b_tp1_arr3_r4.txt); the few prompt tokens over the cap go into
         # the next step, itself a cheap mixed step
         self.mixed_step_rows = max(0, int(mixed_step_rows))
+        self._prefill_capped = False
         # Bounded device waits: every host wait for device results polls an event against
         # min(call deadline, step start + watchdog_s) instead of blocking in a synchronize, so a hung collective
         # surfaces as EngineStalled inside llm.timeout.  ``on_unrecoverable``: "exit" ends the process (exit code
@@ -948,9 +949,15 @@ class LLMEngine:
         if self._trace_steps:
             self.recovery_trace.append((time.monotonic(), f"prefill: {len(self.prefilling)} requests"))
         budget = self.max_prefill_tokens
-        capped = bool(self.mixed_steps and self.running and self.mixed_step_rows)
-        if capped:
-            budget = min(budget, max(MIXED_MIN_PROMPT_ROWS, self.mixed_step_rows - len(self.running)))
+        capped = False
+        if self.mixed_steps and self.running and self.mixed_step_rows:
+            # the cap is for a serving step that would land just past the cap (an arrival or two beside the
+            # decodes); a throughput backlog (a batch of prompts, thousands of rows) keeps its big chunks
+            rows = min(sum(len(r.prompt_ids) - r.computed for r in self.prefilling), budget) + len(self.running)
+            if self.mixed_step_rows < rows <= 2 * self.mixed_step_rows:
+                capped = True
+                budget = min(budget, max(MIXED_MIN_PROMPT_ROWS, self.mixed_step_rows - len(self.running)))
+        self._prefill_capped = capped
         chunk = []  # (req, start, end)
         for r in self.prefilling:
             if budget <= 0:
@@ -1440,7 +1447,7 @@ class LLMEngine:
         if self.prefilling or self.waiting:
             with trace("engine.prefill"):
                 self._prefill()
-            if self.mixed_steps and self.mixed_step_rows and self.running and self.prefilling:
+            if self._prefill_capped and self.running and self.prefilling:
                 # a prompt cut by the mixed-step row cap continues after ONE decode step instead of a whole decode
                 # chunk.  That step is needed: it syncs the rows the device finished (their context is zeroed on
                 # the device), which the next mixed step must not carry as decode rows

@@ -392,8 +392,9 @@ def test_decision_prefill_buckets_stay_on_captured_xgmi(tp):
 
 
 def test_mixed_step_rows_stay_within_the_cap():
-    """engine.mixed_step_rows: a mixed step's rows (prompt tokens + one per running decode) stay within the cap; the
-    prompt tokens over it go into the next step, and the tokens equal the uncapped engine's."""
+    """engine.mixed_step_rows: a mixed step that would land just past the cap (up to twice it) keeps its rows (prompt
+    tokens + one per running decode) within it, the prompt tokens over it go into the next step; a larger backlog keeps
+    its big chunk; the tokens equal the uncapped engine's."""
     prompt_long = [9, 10, 11, 12] * 12             # 48 prompt tokens
     params = [SamplingParams(max_tokens=n, temperature=0.0, ignore_eos=True) for n in (60, 60, 12)]
 
@@ -416,9 +417,10 @@ def test_mixed_step_rows_stay_within_the_cap():
             eng.step()
         return [r.output_ids for r in reqs], rows, eng.stats["mixed_steps"]
 
-    capped, rows_c, n_c = run(20)
+    capped, rows_c, n_c = run(32)
     free, rows_f, n_f = run(0)
-    assert capped == free
-    assert max(rows_c[1:]) <= 20 and n_c >= 3        # 48 prompt tokens in chunks of 18 beside 2 decodes
-    assert rows_c[1:4] == [20, 20, 14]               # one decode step (not a chunk) between a prompt's pieces
+    backlog, rows_b, _ = run(16)                    # 50 rows > 2 x cap: a backlog keeps its big chunk
+    assert capped == free == backlog
+    assert rows_c[1:3] == [32, 20] and n_c >= 2      # 48 prompt tokens: 30 beside 2 decodes, then 18 (+2)
     assert max(rows_f) == 48 + 2 and n_f == 1
+    assert max(rows_b) == 48 + 2
