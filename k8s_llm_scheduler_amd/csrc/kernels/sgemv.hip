@@ -311,13 +311,13 @@ __device__ __forceinline__ void sm_halve(float* v, int lane) {   // sg_halve tha
 }
 
 template <int EPI, bool RES>
-__device__ __forceinline__ void sm_store(void* out, const bf16_t* res, size_t o, float a, float u) {
+__device__ __forceinline__ void sm_store(void* out, size_t o, float a, float u, float rv) {
   if constexpr (EPI == SG_F32) {
     reinterpret_cast<float*>(out)[o] = a;
   } else if constexpr (EPI == SG_SWIGLU) {
     reinterpret_cast<bf16_t*>(out)[o] = f2bf(a / (1.f + __expf(-a)) * u);
   } else {
-    if constexpr (RES) a += bf2f(res[o]);
+    if constexpr (RES) a += rv;
     reinterpret_cast<bf16_t*>(out)[o] = f2bf(a);
   }
 }
@@ -329,8 +329,7 @@ constexpr int SM_TICKET_RANGE = 256, SM_TICKET_RANGES = 256;
 __device__ unsigned sm_tickets[SM_TICKET_RANGE * SM_TICKET_RANGES];
 
 template <int MT, int JT, int EPI, bool NORM, bool RES, bool FP8>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MT == 8 ? 4 : 2)))
-smfma_kernel(void* __restrict__ out, float* __restrict__ part,
+__global__ void __launch_bounds__(512) smfma_kernel(void* __restrict__ out, float* __restrict__ part,
                                                      const bf16_t* __restrict__ x, const void* __restrict__ W,
                                                      const float* __restrict__ wscale, const bf16_t* res, int M,
                                                      int N, int K, float eps, int band_rows, int jw,
@@ -469,6 +468,20 @@ smfma_kernel(void* __restrict__ out, float* __restrict__ part,
     }
   }
 
+  // the first epilogue pass's residual and row scales are requested now, behind the first weight set (clamped, so no
+  // load sits under a branch): their latency hides under the weight stream instead of ending the kernel
+  float pre_res = 0.f, pre_sa = 1.f, pre_su = 1.f;
+  asm volatile("" ::: "memory");
+  {
+    const int idx = min(tid, band * M - 1);
+    const int m = idx / band, n = b0 + idx - m * band;
+    if constexpr (RES) pre_res = bf2f(res[(size_t)m * N + n]);
+    if constexpr (FP8) {
+      pre_sa = wscale[n];
+      if constexpr (EPI == SG_SWIGLU) pre_su = wscale[N + n];
+    }
+  }
+
   // quad blocks two at a time so the register set of every (block, set) pair is a compile-time choice; an odd
   // count runs a phantom block, and the last block prefetches the (out-of-range) block after it: no load sits
   // under a branch, so every wait stays a counted one
@@ -527,9 +540,10 @@ smfma_kernel(void* __restrict__ out, float* __restrict__ part,
       a *= inv;
       u *= inv;
     }
+    const bool first = idx == tid;
     if constexpr (FP8) {
-      a *= wscale[n];
-      if (EPI == SG_SWIGLU) u *= wscale[N + n];
+      a *= first ? pre_sa : wscale[n];
+      if (EPI == SG_SWIGLU) u *= first ? pre_su : wscale[N + n];
     }
     if (G > 1) {   // device-coherent stores (write-through past the XCD's L2): read back by another workgroup
       const int wrows = (EPI == SG_SWIGLU) ? 2 * N : N;
@@ -538,7 +552,8 @@ smfma_kernel(void* __restrict__ out, float* __restrict__ part,
       if (EPI == SG_SWIGLU) __hip_atomic_store(slab + N + n, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       continue;
     }
-    sm_store<EPI, RES>(out, res, (size_t)m * N + n, a, u);
+    const size_t o = (size_t)m * N + n;
+    sm_store<EPI, RES>(out, o, a, u, RES ? (first ? pre_res : bf2f(res[o])) : 0.f);
   }
   if (G == 1 || tickets == nullptr) return;   // (no tickets: sgemv_finalize_kernel sums the slabs)
 
@@ -564,7 +579,8 @@ smfma_kernel(void* __restrict__ out, float* __restrict__ part,
       a += __hip_atomic_load(slab + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (EPI == SG_SWIGLU) u += __hip_atomic_load(slab + N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    sm_store<EPI, RES>(out, res, (size_t)m * N + n, a, u);
+    const size_t o = (size_t)m * N + n;
+    sm_store<EPI, RES>(out, o, a, u, RES ? (idx == tid ? pre_res : bf2f(res[o])) : 0.f);
   }
   if (tid == 0)   // ready for the next launch that draws this ticket range
     __hip_atomic_store(&tickets[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -670,8 +686,8 @@ static void sg_finalize(void* out, float* part, const bf16_t* rr, int M, int N, 
   else sgemv_finalize_kernel<SG_BF16, false><<<blocks, 256, 0, stream>>>(out, part, rr, M, N, G);
 }
 
-// Workgroups of the MFMA form per CU the band is sized for: what the kernel's registers allow (8-row x: <= 128
-// VGPRs, 2; 16-row: 1), capped by K8S_SGEMV_WG_PER_CU (default 1: at 2 the 70B QKV / gate/up / down ran 9 / 3 / 3 %
+// Workgroups of the MFMA form per CU the band is sized for: what the kernel's registers allow (one for every form
+// since the epilogue prefetch took the 8-row kernels past 128 VGPRs), capped by K8S_SGEMV_WG_PER_CU (default 1: at 2 the 70B QKV / gate/up / down ran 9 / 3 / 3 %
 // slower -- twice the workgroups re-read x -- and O 3 % faster; profiles/sgemv_mfma4_kernel_trace_r4.txt).
 static int sm_wg_cap() {
   static const int v = [] { const char* e = getenv("K8S_SGEMV_WG_PER_CU"); return e ? max(1, atoi(e)) : 1; }();
