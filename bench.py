@@ -425,6 +425,11 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp, router=N
         "mean_decode_batch": round(eng.stats["decode_tokens"] / max(1, eng.stats["decode_steps"]), 2),
         "engine_prefill_s": round(eng.stats["prefill_time"], 2),
         "engine_decode_s": round(eng.stats["decode_time"], 2),
+        "engine_prefill_tokens": eng.stats["prefill_tokens"],
+        "engine_cached_tokens": eng.stats["cached_tokens"],
+        "engine_prefill_steps": eng.stats.get("prefill_steps", 0),
+        "engine_mixed_steps": eng.stats["mixed_steps"],
+        "engine_mixed_decode_rows": eng.stats["mixed_decode_rows"],
     }
     line = json.dumps(res)
     print(line, flush=True)

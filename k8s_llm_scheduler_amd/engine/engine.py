@@ -1038,6 +1038,7 @@ class LLMEngine:
             logits = self.model.forward_prefill(t(ids), t(pos), t(slots), t(cu), t(ctx), bt_d,
                                                 max(e - s for _, s, e in chunk), t(last), split=split)
         self.stats["prefill_tokens"] += len(ids)
+        self.stats["prefill_steps"] = self.stats.get("prefill_steps", 0) + 1
         if self._trace_steps:
             self.recovery_trace.append((time.monotonic(), "prefill: forward enqueued"))
         done = [(i, r) for i, (r, s, e) in enumerate(chunk) if e == len(r.prompt_ids)]
