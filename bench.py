@@ -214,6 +214,13 @@ def main() -> int:
         fallbacks += sum(d.fallback_needed for d in ds)
     barrier()
     elapsed = time.perf_counter() - t0
+    if os.environ.get("K8S_ENGINE_TRACE") == "1" and rank == 0:   # host timeline of the last prefill (diagnostics)
+        pf = [(t, m) for t, m in getattr(eng, "recovery_trace", []) if m.startswith("prefill")]
+        last = max((i for i, (_, m) in enumerate(pf) if m.startswith("prefill: ") and "requests" in m), default=None)
+        if last is not None:
+            t_0 = pf[last][0]
+            progress("last prefill host timeline: " + " | ".join(f"{m.split(': ', 1)[1]} +{(t - t_0) * 1e3:.1f} ms"
+                                                                   for t, m in pf[last + 1:last + 9]))
     if distributed:
         t = torch.tensor([elapsed], device="cuda" if on_gpu and tp.backend == "nccl" else "cpu",
                          dtype=torch.float64)
