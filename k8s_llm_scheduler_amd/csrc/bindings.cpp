@@ -418,7 +418,9 @@ PYBIND11_MODULE(_C, m) {
   using k8sllm::BlockAllocator;
   py::class_<BlockAllocator::Allocation>(m, "Allocation")
       .def_readonly("blocks", &BlockAllocator::Allocation::blocks)
-      .def_readonly("cached_tokens", &BlockAllocator::Allocation::cached_tokens);
+      .def_readonly("cached_tokens", &BlockAllocator::Allocation::cached_tokens)
+      .def_readonly("copy_src", &BlockAllocator::Allocation::copy_src)
+      .def_readonly("copy_tokens", &BlockAllocator::Allocation::copy_tokens);
   py::class_<BlockAllocator>(m, "BlockAllocator")
       .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("block_size"), py::arg("prefix_caching") = true)
       .def("allocate", &BlockAllocator::allocate)

@@ -11,6 +11,14 @@
 // the hashes of blocks whose KV has actually been written (a block is never shared before its KV
 // exists); release() drops references -- hashed blocks with no users stay cached (LRU) until
 // their space is needed.
+//
+// Sub-block prefix: a shared prefix rarely ends on a block boundary (the scheduler's system prompt
+// and chat header end 11 tokens into a block, and the pod-specific text follows in the same block).
+// Every published block is also indexed under its parent chain hash, so after the full-block hits
+// allocate() looks for a cached block with the same parent whose leading tokens match the next
+// tokens of the new prompt; the longest such run is reported (copy_src / copy_tokens) and counted
+// as cached: the caller copies those positions' K/V into the new sequence's own block before its
+// prefill (no sharing, so the block stays private and writable).
 #pragma once
 #include <cstdint>
 #include <list>
@@ -26,7 +34,9 @@ class BlockAllocator {
 
   struct Allocation {
     std::vector<int32_t> blocks;
-    int cached_tokens = 0;  // leading prompt tokens whose KV is already in shared blocks
+    int cached_tokens = 0;  // leading prompt tokens whose KV is already cached (shared blocks + copy_tokens)
+    int copy_src = -1;      // sub-block prefix: copy positions [0, copy_tokens) of this block's K/V ...
+    int copy_tokens = 0;    // ... into blocks[cached_tokens / block_size] before the prefill
   };
 
   // Reserve ceil(total_tokens / block_size) blocks for a sequence whose prompt is `tokens`.
@@ -50,7 +60,9 @@ class BlockAllocator {
  private:
   uint64_t chain_hash(uint64_t parent, const int32_t* toks, int n) const;
   int take_block();
-  int prefix_hits(const std::vector<int32_t>& tokens, std::vector<int>* blocks) const;
+  int prefix_hits(const std::vector<int32_t>& tokens, std::vector<int>* blocks, uint64_t* last = nullptr) const;
+  int sub_block_hit(const std::vector<int32_t>& tokens, int start, uint64_t parent, int* src) const;
+  void unindex(int block);
 
   int num_blocks_, block_size_;
   bool prefix_caching_;
@@ -61,6 +73,11 @@ class BlockAllocator {
   std::vector<std::list<int>::iterator> evict_pos_;
   std::vector<bool> in_evictable_;
   std::unordered_map<uint64_t, int> hash_to_block_;
+  // sub-block prefix index: parent chain hash -> the most recent published blocks under it (their tokens kept)
+  static constexpr int kChildren = 8;
+  std::unordered_map<uint64_t, std::vector<int>> children_;
+  std::vector<uint64_t> block_parent_;
+  std::vector<std::vector<int32_t>> block_tokens_;
   uint64_t hits_ = 0, queries_ = 0;
 };
 

@@ -939,9 +939,23 @@ class LLMEngine:
             a = self.allocator.allocate(r.prompt_ids, total)
             r.blocks = list(a.blocks)
             r.cached = r.computed = int(a.cached_tokens)
+            n_sub = int(getattr(a, "copy_tokens", 0))
+            if n_sub > 0:   # sub-block prefix hit: those positions' K/V come from a cached block (copied now, on
+                # the stream, before anything that could reuse the source block)
+                self._copy_kv_positions(int(a.copy_src), r.blocks[(r.cached - n_sub) // self.block_size], n_sub)
+                self.stats["sub_block_tokens"] = self.stats.get("sub_block_tokens", 0) + n_sub
             r.slot = self.free_slots.pop()
             self.prefilling.append(r)
             self.stats["cached_tokens"] += r.cached
+
+    def _copy_kv_positions(self, src_block: int, dst_block: int, n: int) -> None:
+        """K/V of positions [0, n) of ``src_block`` -> the same positions of ``dst_block``, every layer (the cache is
+        [layers, 2, slots, kv heads, D]; TP ranks copy their own heads)."""
+        kv = self.model.kv_cache
+        bs = self.block_size
+        src = self._dev(list(range(src_block * bs, src_block * bs + n)), torch.long)
+        dst = self._dev(list(range(dst_block * bs, dst_block * bs + n)), torch.long)
+        kv.index_copy_(2, dst, kv.index_select(2, src))
 
     def _prefill(self) -> None:
         if not self.prefilling:

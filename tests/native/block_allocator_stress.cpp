@@ -43,7 +43,11 @@ int main() {
         auto al = a.allocate(s.toks, total);
         CHECK(can);
         CHECK((int)al.blocks.size() == (total + bs - 1) / bs);
-        CHECK(al.cached_tokens % bs == 0 && al.cached_tokens <= (int)s.toks.size());
+        // full shared blocks, then at most block_size - 1 copied positions; the last prompt token is never cached
+        CHECK((al.cached_tokens - al.copy_tokens) % bs == 0 && al.cached_tokens < (int)s.toks.size());
+        CHECK(al.copy_tokens >= 0 && al.copy_tokens < bs);
+        CHECK(al.copy_tokens == 0 || (al.copy_src >= 0 && al.copy_src < nb));
+        for (int b : al.blocks) CHECK(al.copy_tokens == 0 || b != al.copy_src);
         for (int b : al.blocks) CHECK(b >= 0 && b < nb && a.refcount(b) >= 1);
         s.blocks = al.blocks;
         a.commit_prefix(s.blocks, s.toks, (int)s.toks.size());

@@ -183,6 +183,30 @@ def test_block_allocator_prefix_and_eviction():
         A.release([c.blocks[0], c.blocks[0]])
 
 
+def test_block_allocator_sub_block_prefix():
+    """Sub-block prefix hits: after the full-block hits, the longest run of leading tokens shared with a cached block
+    under the same parent chain is reported for copying (never the last prompt token); evicted blocks leave the
+    index."""
+    A = ops.native().BlockAllocator(8, 4, True)
+    t = list(range(10))                           # [0-3] [4-7] [8 9]
+    a = A.allocate(t, 12)
+    A.commit_prefix(a.blocks, t, 10)              # 2 full blocks published
+    u = [0, 1, 2, 3, 4, 5, 9, 9, 1]
+    b = A.allocate(u, 12)                         # block 0 shared, then tokens 4, 5 of block 1
+    assert (b.cached_tokens, b.copy_src, b.copy_tokens) == (6, a.blocks[1], 2)
+    assert b.blocks[0] == a.blocks[0] and b.blocks[1] != a.blocks[1]
+    c = A.allocate([0, 1, 2, 3, 4, 5], 8)         # the last prompt token (5) is recomputed
+    assert (c.cached_tokens, c.copy_tokens) == (5, 1)
+    d = A.allocate([7, 1, 2], 4)                  # nothing shared
+    assert (d.cached_tokens, d.copy_src, d.copy_tokens) == (0, -1, 0)
+    for x in (a, b, c, d):
+        A.release(x.blocks)
+    e = A.allocate(list(range(100, 132)), 32)     # takes every block: the cached ones are evicted
+    A.release(e.blocks)
+    f = A.allocate(u, 12)
+    assert (f.cached_tokens, f.copy_tokens) == (0, 0)
+
+
 def test_forced_decode_emits_script_and_stops_on_json(engine):
     ans = '{"selected_node": "kind-worker2", "confidence": 0.9, "reasoning": "r"}'
     ids = engine.tok.encode(ans)
@@ -424,3 +448,27 @@ def test_mixed_step_rows_stay_within_the_cap():
     assert rows_c[1:3] == [32, 20] and n_c >= 2      # 48 prompt tokens: 30 beside 2 decodes, then 18 (+2)
     assert max(rows_f) == 48 + 2 and n_f == 1
     assert max(rows_b) == 48 + 2
+
+
+def test_sub_block_prefix_hit_copies_kv_and_matches():
+    """A shared prefix that ends inside a block: after the full-block hits, the leading tokens of the next block come
+    from a cached block with the same parent chain (K/V copied into the new sequence's own block); the answers equal
+    an engine without prefix caching, and only the new tokens are prefilled."""
+    shared = [(i * 37) % 9000 + 100 for i in range(37)]          # 2 full blocks + 5 tokens of the third
+    pa = shared + list(range(11, 31))                             # its third block is full (published)
+    pb = shared + [21, 22, 23, 24, 25, 26, 27]
+    params = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+
+    def run(cache):
+        eng = build_engine("tiny", device="cpu", max_batch=2, max_model_len=256, num_blocks=64, seed=1,
+                           prefix_caching=cache)
+        a = eng.generate([pa], params)[0].token_ids
+        before = eng.stats["prefill_tokens"]
+        b = eng.generate([pb], params)[0].token_ids
+        return a, b, eng.stats["prefill_tokens"] - before, eng.stats.get("sub_block_tokens", 0)
+
+    a1, b1, pre1, sub1 = run(True)
+    a0, b0, pre0, sub0 = run(False)
+    assert (a1, b1) == (a0, b0)
+    assert sub1 == 5 and sub0 == 0
+    assert pre1 == len(pb) - 37 and pre0 == len(pb)
