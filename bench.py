@@ -139,7 +139,7 @@ def main() -> int:
                        weight_dtype=args.dtype, speculative_tokens=args.speculative, control=control)
     progress("engine built")
     if eng.use_graphs:
-        eng.capture_graphs([b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= slots] or [1],
+        eng.capture_graphs([b for b in (1, 2, 4, 6, 8, 16, 32, 48, 64) if b <= slots] or [1],
                            nucleus=args.top_p < 1)
     if on_gpu:
         torch.cuda.synchronize()

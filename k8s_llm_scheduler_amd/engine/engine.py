@@ -50,7 +50,7 @@ from ..utils.tracing import trace
 
 log = logging.getLogger(__name__)
 
-BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
+BUCKETS = (1, 2, 4, 6, 8, 16, 32, 48, 64, 96, 128, 192, 256)   # (6: serving at ~5 in flight runs 6 rows, not 8)
 # Single-sequence prompt chunks up to 512 tokens are padded to one of these lengths and replayed
 # from a captured graph, which removes the host launch gaps between the ~10 kernels per layer
 # (tools/prefill_probe.py, 256 tokens: TP=8 shapes 12.53 ms eager -> 12.28 ms replayed; TP=1 44.0 ms
