@@ -54,27 +54,49 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
   const size_t kvs = (size_t)nkv * D;
   const int start = p * PART;
   const int wbase = wid * TW;
-  // With 16-token blocks a 16-token tile is exactly one cache block, so the K rows of this
-  // wave depend only on 4 block-table entries -- not on the context length.  Partition 0 (live
-  // for every sequence) issues its K loads before anything else; the unused tail of a block
-  // table holds valid ids, so these speculative loads are always in bounds.
-  bf16x8 kf[NTILE][D / 32];
+  // With 16-token blocks a 16-token tile is exactly one cache block, so the rows of this wave depend only on 4
+  // block-table entries.  The context length and those entries are one round trip; then every live wave issues
+  // all its K loads (registers) and the V rows of its first 32-key step (LDS-DMA straight into its staging area,
+  // no registers) together -- waves past the context load nothing.  The unused tail of a block table holds valid
+  // ids, so K tiles past the context within a live wave stay in bounds.
+  // (vector buffer loads, all five values through one opaque statement: otherwise the compiler waits for a scalar
+  // load of the length, and branches, before it requests the block ids)
+  const auto rs_cl = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(context_lens), 0, 0x7fffffff, 0x00020000);
+  const auto rs_bt = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(bt), 0, 0x7fffffff, 0x00020000);
+  int ctx_v = (int)__builtin_amdgcn_raw_buffer_load_b32(rs_cl, b * 4, 0, 0);
   int tblk[NTILE];  // cache block of each 16-token tile of this wave (reused for V)
-  auto load_k = [&]() {
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t)
+    tblk[t] = (int)__builtin_amdgcn_raw_buffer_load_b32(rs_bt, min((start + wbase) / 16 + t, max_blocks - 1) * 4, 0, 0);
+  static_assert(NTILE == 4, "four block ids per wave");
+  asm volatile("" : "+v"(ctx_v), "+v"(tblk[0]), "+v"(tblk[1]), "+v"(tblk[2]), "+v"(tblk[3]));
+  const int ctx = __builtin_amdgcn_readfirstlane(ctx_v);
+  if (ctx <= 0 || start >= ctx) return;
+  const int n = min(PART, ctx - start);
+  const int wn = max(0, min(TW, n - wbase));  // live tokens of this wave (wave-uniform)
+  bf16x8 kf[NTILE][D / 32];
+  if (wn > 0) {
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
-      const int blk = bt[min((start + wbase) / 16 + t, max_blocks - 1)];
-      tblk[t] = blk;
-      const bf16_t* kp = k_cache + (size_t)(blk * 16 + li) * kvs + (size_t)kvh * D + g4 * 8;
+      const bf16_t* kp = k_cache + (size_t)(tblk[t] * 16 + li) * kvs + (size_t)kvh * D + g4 * 8;
 #pragma unroll
       for (int kk = 0; kk < D / 32; ++kk) kf[t][kk] = *reinterpret_cast<const bf16x8*>(kp + kk * 32);
     }
-  };
-  if (p == 0) load_k();
-  const int ctx = context_lens[b];
-  if (ctx <= 0 || start >= ctx) return;
-  if (p != 0) load_k();
-  const int n = min(PART, ctx - start);
+    // V of keys 0..31: instruction q fills staging bytes [1 KiB q, 1 KiB (q + 1)) = rows 4q..4q+3; lane L lands
+    // at row 4q + L/16, 16-byte slot L%16, which in the swizzled image holds column chunk (L%16) ^ vswz(row) -- so
+    // that is the chunk it fetches.  Rows past the wave's live keys re-read its last live row (their P is exactly
+    // 0; the bytes only have to be finite).
+    const int lr = min(wn, 32) - 1;
+    const int last_row = (lr < 16 ? tblk[0] : tblk[1]) * 16 + (lr & 15);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = 4 * q + g4;
+      const int srow = r < wn ? tblk[q >> 2] * 16 + (r & 15) : last_row;
+      const bf16_t* src = v_cache + (size_t)srow * kvs + (size_t)kvh * D + (li ^ vswz(r)) * 8;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(&vbuf[wid][0] + 1024 * q), 16,
+                                       0, 0);
+    }
+  }
   const int pos = ctx - 1;
   const bool owner = pos < start + n;
   const int nq = nkv * G;
@@ -125,7 +147,6 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
   for (int kk = 0; kk < D / 32; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(&qs[li][kk * 32 + g4 * 8]);
 
   // ---- S^T = K . Q^T over this wave's tokens; lane holds S[token 16t + 4*g4 + i][head li]
-  const int wn = max(0, min(TW, n - wbase));
   const float qscale = scale * LOG2E_F;
   f32x4 sacc[NTILE];
 #pragma unroll
@@ -139,18 +160,18 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
     for (int kk = 0; kk < D / 32; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][kk], qf[kk], acc, 0, 0, 0);
     sacc[t] = acc;
   }
-  // V rows of the first 32-key step: loads issued now (K registers are free), consumed after the
-  // softmax exchange; the second step's loads are issued once the first is staged in LDS
+  // V rows of the second 32-key step: register loads issued now (the K registers are free), in flight across
+  // the softmax exchange and the first step's P.V; staged into LDS once the first step's reads are done
   u32x4 vv[8];
-  auto load_v = [&](int st) {
+  const bool two = 32 < wn;  // wave-uniform
+  if (two) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int c = lane + 64 * q, r = c >> 4, ch = c & 15;
-      const int blk = (r < 16) ? tblk[2 * st] : tblk[2 * st + 1];  // r < 16 <=> q < 4 (lane-independent)
+      const int blk = (r < 16) ? tblk[2] : tblk[3];  // r < 16 <=> q < 4 (lane-independent)
       vv[q] = *reinterpret_cast<const u32x4*>(v_cache + (size_t)(blk * 16 + (r & 15)) * kvs + (size_t)kvh * D + ch * 8);
     }
-  };
-  if (wn > 0) load_v(0);
+  }
   // scale, mask, wave-local max per head
   float m = -INFINITY;
 #pragma unroll
@@ -190,23 +211,41 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
   for (int nn = 0; nn < D / 16; ++nn) o[nn] = f32x4{0.f, 0.f, 0.f, 0.f};
   char* vb = vbuf[wid];
   const int qd = li >> 2, pd = li & 3;
+  static_assert(NTILE == 4, "two 32-key steps per wave");
 #pragma unroll
   for (int st = 0; st < NTILE / 2; ++st) {
     if (32 * st < wn) {  // wave-uniform
-      // stage the 32 keys x 128 d loaded above (fresh token from LDS, keys past the wave zeroed)
+      if (st == 0) {
+        // the DMA image of keys 0..31 has landed (only the second step's register loads may still be in flight:
+        // loads complete in order); the new token's row -- and the padding rows after it, which re-read its
+        // stale cache slot -- take the fresh v
+        if (two) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int rp = pos - (start + wbase);
+        if (rp >= 0 && rp < 32) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int c = lane + 64 * q, r = c >> 4, ch = c & 15;
-        const int k = 32 * st + r;
-        if (start + wbase + k == pos) vv[q] = *reinterpret_cast<const u32x4*>(&vcur[ch * 8]);
-        if (k >= wn) vv[q] = u32x4{0u, 0u, 0u, 0u};
-      }
+          for (int q = 0; q < 8; ++q) {
+            const int c = lane + 64 * q, r = c >> 4, ch = c & 15;
+            if (r >= rp)
+              *reinterpret_cast<u32x4*>(vb + r * (D * 2) + 16 * (ch ^ vswz(r))) =
+                  *reinterpret_cast<const u32x4*>(&vcur[ch * 8]);
+          }
+        }
+      } else {
+        // stage the 32 keys x 128 d loaded above (fresh token from LDS, keys past the wave zeroed)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int c = lane + 64 * q, r = c >> 4, ch = c & 15;
-        *reinterpret_cast<u32x4*>(vb + r * (D * 2) + 16 * (ch ^ vswz(r))) = vv[q];
+        for (int q = 0; q < 8; ++q) {
+          const int c = lane + 64 * q, r = c >> 4, ch = c & 15;
+          const int k = 32 * st + r;
+          if (start + wbase + k == pos) vv[q] = *reinterpret_cast<const u32x4*>(&vcur[ch * 8]);
+          if (k >= wn) vv[q] = u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int c = lane + 64 * q, r = c >> 4, ch = c & 15;
+          *reinterpret_cast<u32x4*>(vb + r * (D * 2) + 16 * (ch ^ vswz(r))) = vv[q];
+        }
       }
-      if (st + 1 < NTILE / 2 && 32 * (st + 1) < wn) load_v(st + 1);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -97,10 +97,15 @@ __device__ __forceinline__ void split_body(
 
   // context length, the chunk's 4 block ids and the new token's q/k/v (lane p: dims p and p + 64
   // of every q head, of k and of v) are independent loads: one round trip
-  const int ctx = context_lens[b];
+  // (vector buffer loads, the five values through one opaque statement: otherwise the compiler waits for a scalar
+  // load of the length, and branches, before it requests the block ids -- two round trips instead of one)
+  int ctx_v = (int)__builtin_amdgcn_raw_buffer_load_b32(split_rsrc(context_lens), b * 4, 0, 0);
   int tblk[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) tblk[t] = bt[min(start / 16 + t, max_blocks - 1)];
+  for (int t = 0; t < 4; ++t)
+    tblk[t] = (int)__builtin_amdgcn_raw_buffer_load_b32(split_rsrc(bt), min(start / 16 + t, max_blocks - 1) * 4, 0, 0);
+  asm volatile("" : "+v"(ctx_v), "+v"(tblk[0]), "+v"(tblk[1]), "+v"(tblk[2]), "+v"(tblk[3]));
+  const int ctx = __builtin_amdgcn_readfirstlane(ctx_v);
   const int nq = nkv * G;
   const bf16_t* row = qkv + (size_t)b * (nq + 2 * nkv) * D;
   bf16_t xa[G], xb[G];
@@ -229,10 +234,15 @@ __device__ __forceinline__ void split_body(
   // ---- O = P . V over two 32-key steps.  The V image has landed (the K wait above drained the
   // DMA too); the owner chunk replaces the new token's row, which the cache did not hold yet.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (owner && lane < 16) {
+  if (owner) {   // the new token's row and the padding rows after it, which re-read its stale cache slot
     const int rp = pos - start;
-    *reinterpret_cast<u32x4*>(vbuf[rp >> 5] + (rp & 31) * (D * 2) + 16 * (li ^ swz(rp & 31))) =
-        *reinterpret_cast<const u32x4*>(&vcur[li * 8]);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = 4 * q + g4;
+      if (r >= rp)
+        *reinterpret_cast<u32x4*>(vbuf[r >> 5] + (r & 31) * (D * 2) + 16 * (li ^ swz(r & 31))) =
+            *reinterpret_cast<const u32x4*>(&vcur[li * 8]);
+    }
   }
   __syncthreads();
   f32x4 o[D / 16];

@@ -378,6 +378,36 @@ def test_decode_attention_fused(nq, nkv, ctxs, variant, monkeypatch):
         close(vc2, vr, 0, 0)
 
 
+@pytest.mark.parametrize("variant", ["one-wg-1024", "one-wg-512", "small-grid-split"])
+def test_decode_attention_stale_slots_do_not_leak(variant, monkeypatch):
+    """The new token's cache slot and the unused slots after it hold NaN before the call: the V rows the kernels
+    stage for padding keys (P = 0) must not carry them into the output (0 * NaN)."""
+    monkeypatch.setattr(ops, "SPLIT_MAX_PAIRS", 64 if variant == "small-grid-split" else 0)
+    monkeypatch.setattr(ops, "FUSED_PART_ENV", 512 if variant == "one-wg-512" else 1024)
+    nq, nkv, D, bs = 64, 8, 128, 16
+    ctxs = [1, 37, 600, 64, 65, 33]
+    B = len(ctxs)
+    maxb = (max(ctxs) + bs - 1) // bs + 1
+    nblocks = B * maxb + 3
+    kc, vc = _paged_cache(nkv, D, bs, nblocks)
+    bt = torch.randperm(nblocks, device=DEV)[: B * maxb].view(B, maxb).int()
+    btc = bt.cpu()
+    for b, c in enumerate(ctxs):
+        for t in range(c - 1, (c + bs - 1) // bs * bs):
+            slot = int(btc[b, t // bs]) * bs + t % bs
+            kc[slot] = float("nan")
+            vc[slot] = float("nan")
+    ctx = torch.tensor(ctxs, device=DEV, dtype=torch.int32)
+    qkv = rnd(B, (nq + 2 * nkv) * D)
+    cs = ref.rope_table(D, 4096, 500000.0, None).to(DEV)
+    kr, vr = kc.cpu().clone(), vc.cpu().clone()
+    got = ops.decode_attention_fused(qkv, cs, kc, vc, bt, ctx, 1 / math.sqrt(D), bs, 1024, nq, nkv, D)
+    want = ops.decode_attention_fused(qkv.cpu(), cs.cpu(), kr, vr, btc, ctx.cpu(), 1 / math.sqrt(D), bs, 1024, nq,
+                                      nkv, D)
+    assert torch.isfinite(got).all()
+    close(got, want, 2e-2)
+
+
 def test_fp8_decode_matches_torch_e4m3():
     """v_cvt_pk_f32_fp8 on gfx950 decodes OCP e4m3 (torch.float8_e4m3fn) for every finite byte."""
     codes = torch.tensor([c if c not in (0x7F, 0xFF) else 0 for c in range(256)], dtype=torch.uint8)

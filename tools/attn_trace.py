@@ -37,10 +37,14 @@ def main() -> int:
         [ctypes.c_void_p]
     dev, bf, D, bs = "cuda", torch.bfloat16, 128, 16
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
-    for (nq, nkv, tag) in ((8, 1, "TP=8"), (64, 8, "TP=1")):
-        for ctx in (64, 256, 564, 1024):
-            B, maxb = 1, 4096 // bs
-            pmax = math.ceil(ctx / 64)
+    # (nq, nkv, tag, batch, contexts, graph-class max context or None = the context itself)
+    cases = [(8, 1, "TP=8", 1, (64, 256, 564, 1024), None), (64, 8, "TP=1", 1, (64, 256, 564, 1024), None),
+             (64, 8, "TP=1 B=4", 4, (564,), 1024), (64, 8, "TP=1 B=8", 8, (564,), 1024),
+             (64, 8, "TP=1 B=8", 8, (564,), None)]
+    for (nq, nkv, tag, B, ctxs, maxctx) in cases:
+        for ctx in ctxs:
+            maxb = 4096 // bs
+            pmax = math.ceil((maxctx or ctx) / 64)
             kc = torch.randn(B * maxb * bs, nkv, D, device=dev).to(bf)
             vc = torch.randn_like(kc)
             bt = torch.arange(B * maxb, device=dev, dtype=torch.int32).view(B, maxb)
@@ -74,8 +78,12 @@ def main() -> int:
                 rel = torch.where(t > 0, (t - t0) * 0.01, torch.full_like(t, float("nan")))  # us
                 end = torch.nan_to_num(rel[:, 7], nan=-1).max().item()
                 starts = rel[:, 0]
-                print(f"{tag} ctx={ctx:5d} wgs={nwg:3d} {'cold' if cold else 'hot '}: total {end:5.2f} us; "
-                      f"entry spread {starts.max().item():4.2f} us")
+                live = ~torch.isnan(rel[:, 1])
+                ends = torch.nan_to_num(rel[:, 5], nan=-1)[live]
+                print(f"{tag} ctx={ctx:5d} pmax={pmax:2d} wgs={nwg:4d} {'cold' if cold else 'hot '}: total {end:5.2f} us; "
+                      f"entry spread {torch.nan_to_num(starts, nan=0).max().item():4.2f} us (live "
+                      f"{torch.nan_to_num(starts[live], nan=0).max().item():4.2f}); partial stored p50/max "
+                      f"{ends.median().item():4.2f}/{ends.max().item():4.2f} us")
                 # stage i ends at stamp i; the single-chunk output (7) follows 4, the merge runs 6 -> 8 -> 9 -> 7
                 prev = {1: 0, 2: 1, 3: 2, 4: 3, 5: 4, 6: 5, 7: 4, 8: 6, 9: 8, 10: 9}
                 end_of = {i: i for i in range(1, 10)}

@@ -1,5 +1,6 @@
 # GPU steps on one MI355X, chosen by RUNS (space-separated): sgemv sgprobe sgprobe0 mfma0b8 b4m3 b16 b4 b8 arr3 sg0b8 proffp8b64 selflaunch
-# tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b tune8b proftp8 fp8tp4 tunefp8 minmi.
+# tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b tune8b proftp8 fp8tp4 tunefp8 minmi
+# attn kbattn attntr.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
 # (any other rc) ends the script.  Logs land in gpurun_out/$OUT (default r4).
 set -o pipefail
@@ -16,6 +17,13 @@ step() {  # step <seconds> <log> <cmd...>
 }
 for spec in ${RUNS:-tests smoke bench}; do
   case $spec in
+    attn) step 300 attn_tests.log python -u -m pytest tests/test_kernels_gpu.py -x -q -k "decode_attention" --timeout 120 --timeout-method thread
+          tail -3 $O/attn_tests.log ;;
+    kbattn) for m in 4 8 16 64; do step 200 kb_attn_m$m.txt python -u tools/kbench.py --tp 1 --M $m
+              grep -h "decode_attn" $O/kb_attn_m$m.txt | sed "s/^/M=$m /"; done
+            step 200 kb_attn_tp8_m64.txt python -u tools/kbench.py --tp 8 --M 64
+            grep -h "decode_attn" $O/kb_attn_tp8_m64.txt | sed "s/^/tp8 M=64 /" ;;
+    attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
     sgemv) step 300 sgemv_tests.log python -u -m pytest tests/test_sgemv_gpu.py -x -q --timeout 200 --timeout-method thread
            tail -3 $O/sgemv_tests.log ;;
     sgprobe) step 300 sgemv_probe.txt python -u tools/sgemv_probe.py 5
