@@ -473,6 +473,10 @@ def _mg_load_table() -> dict:
 
             with open(MG_TABLE_PATH) as f:
                 plans = json.load(f).get("plans", {})
+            # K8S_MGEMM_OVERRIDE="M,N,K,epi,fp8=cfg:grid;...": replace table rows (in-situ plan A/B runs)
+            for item in filter(None, os.environ.get("K8S_MGEMM_OVERRIDE", "").split(";")):
+                key, val = item.split("=")
+                plans[key.strip()] = [int(t) for t in val.split(":")] + [0.0, 0.0]
             for k, v in plans.items():
                 mb, n, kk, epi, fp8 = (int(t) for t in k.split(","))
                 mg_us, lib_us = (float(v[2]), float(v[3])) if len(v) >= 4 else (0.0, 0.0)

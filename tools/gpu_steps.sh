@@ -23,6 +23,14 @@ for spec in ${RUNS:-tests smoke bench}; do
               grep -h "decode_attn" $O/kb_attn_m$m.txt | sed "s/^/M=$m /"; done
             step 200 kb_attn_tp8_m64.txt python -u tools/kbench.py --tp 8 --M 64
             grep -h "decode_attn" $O/kb_attn_tp8_m64.txt | sed "s/^/tp8 M=64 /" ;;
+    kbattn512) for m in 8 16 64; do K8S_ATTN_FUSED_PART=512 step 200 kb_attn512_m$m.txt python -u tools/kbench.py --tp 1 --M $m
+                 grep -h "decode_attn\[one-wg\]" $O/kb_attn512_m$m.txt | sed "s/^/part512 M=$m /"; done
+               K8S_ATTN_FUSED_PART=512 step 200 kb_attn512_tp8_m64.txt python -u tools/kbench.py --tp 8 --M 64
+               grep -h "decode_attn\[one-wg\]" $O/kb_attn512_tp8_m64.txt | sed "s/^/part512 tp8 M=64 /" ;;
+    mgab) i=0; for ov in "" ${MGOV:-}; do i=$((i+1)); K8S_MGEMM_OVERRIDE="$ov" step 400 bench_b64_ov$i.json python -u bench.py --batch 64 --steps 2 --warmup 1
+            echo "override [$ov]: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_b64_ov$i.json | tr '\n' ' ')"; done ;;
+    mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only qkv o_proj --verbose
+              tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
     sgemv) step 300 sgemv_tests.log python -u -m pytest tests/test_sgemv_gpu.py -x -q --timeout 200 --timeout-method thread
            tail -3 $O/sgemv_tests.log ;;
