@@ -24,6 +24,17 @@ def test_mgemm_table_lookup_stays_inside_the_tuned_range():
     assert ops._mg_table_row(4 * top + 1, n, k, epi, True) is None
 
 
+def test_mgemm_override_replaces_a_table_row(monkeypatch):
+    monkeypatch.setenv("K8S_MGEMM_OVERRIDE", "64,10240,8192,0,0=11:1;64,8192,8192,0,0=12:2")
+    monkeypatch.setattr(ops, "_MG_TABLE", None)
+    try:
+        assert ops._mg_table_row(64, 10240, 8192, ops.EPI_BF16, False)[1:3] == (11, 1)
+        assert ops._mg_table_row(64, 8192, 8192, ops.EPI_BF16, False)[1:3] == (12, 2)
+    finally:
+        monkeypatch.delenv("K8S_MGEMM_OVERRIDE")
+        ops._MG_TABLE = None   # the next lookup reloads the bundled table
+
+
 LLAMA_TP1 = [(10240, 8192, ops.EPI_BF16), (8192, 8192, ops.EPI_BF16), (28672, 8192, ops.EPI_SWIGLU),
              (8192, 28672, ops.EPI_BF16)]
 
