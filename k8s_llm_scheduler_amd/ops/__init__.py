@@ -735,6 +735,14 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
     return pgemm(x2, w, epi, cfg=cfg, splits=sp, group_m=gm, res=res, rms_eps=rms_eps, out=out, act=act)
 
 
+# bf16 rows in (SGEMV_MAX_M, RMS_PROLOGUE_MAX_UNFUSED] take a separate RMSNorm + plain GEMM instead of mgemm's RMS
+# prologue (K8S_RMS_UNFUSED_MAX_M, default 64; 0 = always the prologue).  Batched decode on mgemm measured faster
+# that way: batch 64 decode 31.41 -> 30.78-30.82 ms/step, batch 32 28.28 -> 28.10; a 245-row prefill with the split
+# up to 256 rows was unchanged (46.86 vs 46.74 ms), so the prologue keeps everything past 64 rows
+# (profiles/bench_r4_rms_prologue_ab.txt).
+RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "64"))
+
+
 def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Tensor:
     """epi(rmsnorm(r) @ w.T) for M > GEMV_MAX_M rows with the norm gamma folded into ``w`` (LlamaModel folds it at
     load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
@@ -755,7 +763,7 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
         if epi == EPI_SWIGLU:
             return ref.linear_swiglu(xa, w).to(BF16)
         return ref.linear(xa, w, F32 if epi == EPI_F32 else BF16)
-    if _gpu(r) and M > GEMV_MAX_M:
+    if _gpu(r) and M > GEMV_MAX_M and (M <= SGEMV_MAX_M or M > RMS_PROLOGUE_MAX_UNFUSED or _is_fp8(w)):
         y = _gemm(r.contiguous(), w, epi, rms_eps=eps)
         if y is not None:
             return y

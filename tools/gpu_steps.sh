@@ -29,6 +29,12 @@ for spec in ${RUNS:-tests smoke bench}; do
                grep -h "decode_attn\[one-wg\]" $O/kb_attn512_tp8_m64.txt | sed "s/^/part512 tp8 M=64 /" ;;
     mgab) i=0; for ov in "" ${MGOV:-}; do i=$((i+1)); K8S_MGEMM_OVERRIDE="$ov" step 400 bench_b64_ov$i.json python -u bench.py --batch 64 --steps 2 --warmup 1
             echo "override [$ov]: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_b64_ov$i.json | tr '\n' ' ')"; done ;;
+    rmsab) for i in 1 2; do for um in 0 64; do K8S_RMS_UNFUSED_MAX_M=$um step 400 bench_b64_rms$um.json python -u bench.py --batch 64 --steps 2 --warmup 1
+             echo "unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*' $O/bench_b64_rms$um.json | tr '\n' ' ')"; done; done ;;
+    rmsab2) for um in 0 64; do K8S_RMS_UNFUSED_MAX_M=$um step 400 bench_b32_rms$um.json python -u bench.py --batch 32 --steps 2 --warmup 1
+             echo "b32 unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*' $O/bench_b32_rms$um.json | tr '\n' ' ')"; done
+            for um in 0 256; do K8S_RMS_UNFUSED_MAX_M=$um step 400 bench_def_rms$um.json python -u bench.py --steps 6 --warmup 2
+             echo "default unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_def_rms$um.json | tr '\n' ' ')"; done ;;
     mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only qkv o_proj --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
