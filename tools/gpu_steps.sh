@@ -35,7 +35,9 @@ for spec in ${RUNS:-tests smoke bench}; do
              echo "b32 unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*' $O/bench_b32_rms$um.json | tr '\n' ' ')"; done
             for um in 0 256; do K8S_RMS_UNFUSED_MAX_M=$um step 400 bench_def_rms$um.json python -u bench.py --steps 6 --warmup 2
              echo "default unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_def_rms$um.json | tr '\n' ' ')"; done ;;
-    mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only qkv o_proj --verbose
+    wgab) for i in 1 2; do for wg in 1 2; do K8S_SGEMV_WG_PER_CU=$wg step 400 bench_b8_wg$wg.json python -u bench.py --batch 8 --steps 4 --warmup 1
+             echo "b8 wg/cu=$wg: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*' $O/bench_b8_wg$wg.json | tr '\n' ' ')"; done; done ;;
+    mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only ${MGONLY:-qkv o_proj} --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
     sgemv) step 300 sgemv_tests.log python -u -m pytest tests/test_sgemv_gpu.py -x -q --timeout 200 --timeout-method thread
