@@ -2,7 +2,10 @@
 // attention over the paged cache in ONE kernel that reads the QKV projection output directly.
 //
 // Structure (one workgroup = 16 waves x 64 tokens = PART = 1024 context tokens of one (sequence,
-// kv head); each wave issues all its K loads, then all its V loads, before consuming any):
+// kv head)): the context length and the wave's 4 block ids are one round trip; then every wave
+// holding live tokens issues all its K loads (registers) and the V rows of its first 32 keys
+// (LDS-DMA into its staging area) before consuming any; the second 32 keys' V rows are register
+// loads issued after the scores, in flight across the softmax exchange and the first P.V step:
 //  * MFMA v_mfma_f32_16x16x32_bf16 in the "swapped" orientation S^T = K . Q^T: the 16 rows are
 //    16 context tokens, the 16 columns the query heads of the GQA group (G <= 16, padded with
 //    zero heads), so each K row is read once for all heads, with 16 rows x 64 B per load
