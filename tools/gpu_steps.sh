@@ -1,6 +1,6 @@
 # GPU steps on one MI355X, chosen by RUNS (space-separated): sgemv sgprobe sgprobe0 mfma0b8 b4m3 b16 b4 b8 arr3 sg0b8 proffp8b64 selflaunch
 # tests ktests recov mg smoke bench fp8 fp8loop ab n256 n256w4 gmm prio tp2 tp8 pf8 loopprobe prof proffp8 fp8head loopbf wide merge swl b8b b64 tp8b64 tp8plain ab8b tune8b proftp8 fp8tp4 tunefp8 minmi
-# attn kbattn attntr.
+# attn kbattn attntr chain.
 # Each GPU step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault
 # (any other rc) ends the script.  Logs land in gpurun_out/$OUT (default r4).
 set -o pipefail
@@ -37,6 +37,10 @@ for spec in ${RUNS:-tests smoke bench}; do
              echo "default unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_def_rms$um.json | tr '\n' ' ')"; done ;;
     wgab) for i in 1 2; do for wg in 1 2; do K8S_SGEMV_WG_PER_CU=$wg step 400 bench_b8_wg$wg.json python -u bench.py --batch 8 --steps 4 --warmup 1
              echo "b8 wg/cu=$wg: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*' $O/bench_b8_wg$wg.json | tr '\n' ' ')"; done; done ;;
+    chain) step 120 chain_probe.txt python -u tools/probes/chain_probe.py
+           cat $O/chain_probe.txt
+           step 120 chain_probe_pre2.txt python -u tools/probes/chain_probe.py chain_pre2.so
+           cat $O/chain_probe_pre2.txt ;;
     mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only ${MGONLY:-qkv o_proj} --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
