@@ -41,6 +41,7 @@ long long k8s_sgemv_workspace(int M, int N, int K, int epi);
 int k8s_gemv_set_loop(int wg_per_cu);
 int k8s_gemv_set_wide(int on);
 int k8s_pgemm_set_prio(int mode);
+int k8s_pgemm_set_row_slabs(int on);
 int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out,
                  int K, int epi, const void* res_in, void* res_out, const void* nw, float eps, hipStream_t s);
 int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s);
@@ -163,6 +164,7 @@ PYBIND11_MODULE(_C, m) {
     }
   }, py::arg("event"), py::arg("timeout_s"));
   m.def("pgemm_set_prio", [](int mode) { return k8s_pgemm_set_prio(mode); });
+  m.def("pgemm_set_row_slabs", [](int on) { return k8s_pgemm_set_row_slabs(on); });
   m.def("gemv_set_wide", [](int on) { return k8s_gemv_set_wide(on); });
   m.def("gemv_set_loop", [](int wg) { return k8s_gemv_set_loop(wg); });
   m.def("gemv_plan", [](int M, int N, int K, int epi, int mode) {

@@ -30,9 +30,10 @@
 //    conflict-free.
 //  * block -> tile: XCD-aware bijective remap, then group_m m-tiles per n-column group (the x rows and the
 //    weight rows of concurrently running tiles share their XCD's L2); k-slices of one tile are adjacent.
-//  * split-K (small tile counts, e.g. TP = 8 or 256-row prefill chunks): every slice publishes an fp32 slab in
-//    fragment order (agent release + arrival ticket); the last arriving slice sums ALL slabs in slice order
-//    (deterministic) and runs the epilogue.  The ticket is reset by the reducer.
+//  * split-K (small tile counts, e.g. TP = 8 or 256-row prefill chunks): every slice stores its raw fp32 sums as a
+//    row-major slab and k8s_pgemm_reduce (pgemm4.hip) sums the slabs in slice order (deterministic) and runs the
+//    epilogue over every CU.  The alternative in-launch form (K8S_PGEMM_ROWSLAB=0) publishes fragment-order slabs
+//    (agent release + arrival ticket) and the last arriving slice reduces them; the ticket is reset by the reducer.
 //  * RMS prologue (bf16): the un-normalised residual stream is the x operand; the x fragments every wave
 //    already holds give the row sums of squares (v_dot2_f32_bf16, waves 0-3 for QB0, 4-7 for QB1), and the
 //    epilogue scales by 1 / rms (the norm gamma is folded into W at load time).
@@ -117,6 +118,8 @@ struct PgArgs {
   int prio;              // wave priority: 0 = s_setprio 1 around every MFMA section, 1 = waves 4-7 at 1 for the
                          // whole loop (MI355X_MICROARCH.md "static priority for the younger half"), 2 = none
   float eps;
+  int row_slabs;         // split-K: 1 = every slice stores a row-major slab ([splits][M][wrows], then the RMS row
+                         // sums [splits][M]) and k8s_pgemm_reduce (all CUs) combines them -- no last-arriver tail
 };
 
 template <int FP, int FQ, int EPI, bool FP8, bool RMS>
@@ -364,6 +367,40 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     __syncthreads();
   }
 
+  // ---- split-K, row-major slabs: this slice's raw sums go where the reduce kernel reads them; done
+  if (a.splits > 1 && a.row_slabs) {
+    const long long wrows = EPI == PG_SWIGLU ? 2LL * a.N_out : (long long)a.N_out;
+    float* sl = a.ws + (size_t)slice * a.M * wrows;
+#pragma unroll
+    for (int bq = 0; bq < NB; ++bq) {
+      const int bh = bq / FQ, fq = bq % FQ;
+      const int m = mt * BQ + wc * (BQ / 4) + bh * (BQ / 8) + fq * 16 + li;
+      if (m >= a.M) continue;
+      float* row = sl + (size_t)m * wrows;
+      if constexpr (EPI == PG_SWIGLU) {
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) {
+          const int f0 = nt * (BP / 2) + wr * (BP / 4) + fp * 16 + 4 * g;
+          if (f0 >= a.N_out) continue;
+          *reinterpret_cast<f32x4*>(row + f0) = acc[fp][bq];
+          *reinterpret_cast<f32x4*>(row + a.N_out + f0) = acc[FP + fp][bq];
+        }
+      } else {
+#pragma unroll
+        for (int ap = 0; ap < NA; ++ap) {
+          const int ah = ap / FP, fp = ap % FP;
+          const int n0 = nt * BP + wr * (BP / 2) + ah * (BP / 4) + fp * 16 + 4 * g;
+          if (n0 < a.N_out) *reinterpret_cast<f32x4*>(row + n0) = acc[ap][bq];
+        }
+      }
+    }
+    if constexpr (RMS) {   // one n-tile per m-tile publishes the slice's row sums of squares
+      if (nt == 0 && tid < BQ && mt * BQ + tid < a.M)
+        a.ws[(size_t)a.splits * a.M * wrows + (size_t)slice * a.M + mt * BQ + tid] = rss[tid];
+    }
+    return;
+  }
+
   // ---- split-K: publish this slice; the last arriving slice of the tile reduces every slab in order
   if (a.splits > 1) {
     float* base = a.ws + (size_t)tile * a.splits * SLAB;
@@ -552,6 +589,22 @@ extern "C" int k8s_pgemm_set_prio(int mode) {
   return old;
 }
 
+// Split-K combine: 1 (default) = row-major slabs + k8s_pgemm_reduce over every CU (one launch more, no cache-wide
+// fence, no single-CU tail); 0 = the last arriving slice of each tile sums the tile's slabs (fragment order) in the
+// same launch, after agent-scope release / acquire fences (an L2 write-back per arriving workgroup and an L2
+// invalidate per reducer).  Bit-identical results (same slice order, same epilogue arithmetic).  Measured on the
+// default bench (245-row chunks, the down projection at 8 splits): prefill 53.8-53.9 -> 46.9 ms per decision on one
+// box, 46.8 either way on others (profiles/bench_r4_pgemm_rowslab_ab.txt).  K8S_PGEMM_ROWSLAB at load,
+// k8s_pgemm_set_row_slabs for A/B probes.
+static int g_pg_row_slabs = [] { const char* e = getenv("K8S_PGEMM_ROWSLAB"); return e ? atoi(e) : 1; }();
+extern "C" int k8s_pgemm_set_row_slabs(int on) {
+  const int old = g_pg_row_slabs;
+  if (on >= 0) g_pg_row_slabs = on ? 1 : 0;
+  return old;
+}
+extern "C" int k8s_pgemm_reduce(void* out, const void* res, const float* slab, int splits, int M, int N_out, int K,
+                                int epi, int rms, float eps, const float* xs, const float* wsc, hipStream_t s);
+
 extern "C" int k8s_pgemm_num_configs() { return kPgNumCfgs; }
 
 extern "C" int k8s_pgemm_config(int cfg, int* bp, int* bq, int* lds_bytes) {
@@ -615,5 +668,9 @@ extern "C" int k8s_pgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.nwg = nwg;
   a.prio = g_pg_prio;
   a.eps = eps;
-  return fp8 ? pg_cfg<true>(a, cfg, epi, 0, stream) : pg_cfg<false>(a, cfg, epi, rms, stream);
+  a.row_slabs = splits > 1 && g_pg_row_slabs;
+  const int rc = fp8 ? pg_cfg<true>(a, cfg, epi, 0, stream) : pg_cfg<false>(a, cfg, epi, rms, stream);
+  if (rc != 0 || !a.row_slabs) return rc;
+  return k8s_pgemm_reduce(out, res, ws, splits, M, N_out, K, epi, rms, eps, fp8 ? xs : nullptr, fp8 ? wsc : nullptr,
+                          stream);
 }

@@ -106,6 +106,37 @@ def test_rms_prologue_and_residual_epilogue(epi):
                     assert err <= 2e-2 * want.abs().max().item(), f"res cfg {cfg} splits {splits} M {M}: {err}"
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("epi", [ops.EPI_BF16, ops.EPI_F32, ops.EPI_SWIGLU])
+def test_row_slab_reduce_is_bit_identical_to_last_arriver(epi, fp8):
+    """Split-K combine by the separate reduce kernel (row-major slabs) against the in-launch last-arriver
+    reduction: same slice order, same epilogue arithmetic -> the same bits (RMS prologue, residual, fp8 scales)."""
+    torch.manual_seed(2)
+    K, N, eps = 2048, 200, 1e-5
+    rows = 2 * N if epi == ops.EPI_SWIGLU else N
+    w = _weights(rows, K, fp8, 7)
+    old = ops.native().pgemm_set_row_slabs(0)
+    try:
+        for cfg, (bp, bq, _lds) in enumerate(ops.pgemm_configs()):
+            for M in (13, bq + 7):
+                x = ((torch.rand(M, K, device=DEV) * 2 - 1) * 3).to(torch.bfloat16)
+                res = ((torch.rand(M, N, device=DEV) * 2 - 1) * 8).to(torch.bfloat16) \
+                    if epi == ops.EPI_BF16 else None
+                rms = None if fp8 else eps
+                for splits in (2, 5):
+                    got = []
+                    for mode in (0, 1):
+                        ops.native().pgemm_set_row_slabs(mode)
+                        r = None if res is None else res.clone()
+                        got.append(ops.pgemm(x, w, epi, cfg=cfg, splits=splits, rms_eps=rms, res=r))
+                    torch.cuda.synchronize()
+                    assert torch.equal(got[0], got[1]), f"cfg {cfg} M {M} splits {splits}"
+                    if rms is None and res is None:
+                        _check(got[1], x, w, epi, what=f"row slabs cfg {cfg} M {M} splits {splits}")
+    finally:
+        ops.native().pgemm_set_row_slabs(old)
+
+
 def test_split_k_tickets_reset_and_graph_replay():
     K, N, M = 4096, 512, 300
     w = _weights(N, K, False, 3)
