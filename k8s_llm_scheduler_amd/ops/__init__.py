@@ -735,12 +735,14 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
     return pgemm(x2, w, epi, cfg=cfg, splits=sp, group_m=gm, res=res, rms_eps=rms_eps, out=out, act=act)
 
 
-# bf16 rows in (SGEMV_MAX_M, RMS_PROLOGUE_MAX_UNFUSED] take a separate RMSNorm + plain GEMM instead of mgemm's RMS
-# prologue (K8S_RMS_UNFUSED_MAX_M, default 64; 0 = always the prologue).  Batched decode on mgemm measured faster
-# that way: batch 64 decode 31.41 -> 30.78-30.82 ms/step, batch 32 28.28 -> 28.10; a 245-row prefill with the split
-# up to 256 rows was unchanged (46.86 vs 46.74 ms), so the prologue keeps everything past 64 rows
-# (profiles/bench_r4_rms_prologue_ab.txt).
+# bf16 rows in (SGEMV_MAX_M, RMS_PROLOGUE_MAX_UNFUSED] with at least RMS_UNFUSED_MIN_N output features take a
+# separate RMSNorm + plain GEMM instead of mgemm's RMS prologue (K8S_RMS_UNFUSED_MAX_M, default 64; 0 = always the
+# prologue).  Measured (profiles/bench_r4_rms_prologue_ab.txt): the TP = 1 projections (QKV 10240, gate/up 28672
+# features) are faster that way -- batch 64 decode 31.54-31.63 -> 31.02-31.04 ms/step, batch 32 28.28 -> 28.10 --
+# while one TP = 8 rank's (1280 / 3584 features) is slower (batch 64 7.56-7.62 -> 8.23-8.26 ms/step: the norm launch
+# costs more than those small GEMMs' prologue); a 245-row prefill was unchanged, so the prologue keeps > 64 rows.
 RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "64"))
+RMS_UNFUSED_MIN_N = int(os.environ.get("K8S_RMS_UNFUSED_MIN_N", "8192"))
 
 
 def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Tensor:
@@ -763,7 +765,9 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
         if epi == EPI_SWIGLU:
             return ref.linear_swiglu(xa, w).to(BF16)
         return ref.linear(xa, w, F32 if epi == EPI_F32 else BF16)
-    if _gpu(r) and M > GEMV_MAX_M and (M <= SGEMV_MAX_M or M > RMS_PROLOGUE_MAX_UNFUSED or _is_fp8(w)):
+    n_out = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    if _gpu(r) and M > GEMV_MAX_M and (M <= SGEMV_MAX_M or M > RMS_PROLOGUE_MAX_UNFUSED or _is_fp8(w)
+                                       or n_out < RMS_UNFUSED_MIN_N):
         y = _gemm(r.contiguous(), w, epi, rms_eps=eps)
         if y is not None:
             return y

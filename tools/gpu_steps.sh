@@ -41,6 +41,26 @@ for spec in ${RUNS:-tests smoke bench}; do
            cat $O/chain_probe.txt
            step 120 chain_probe_pre2.txt python -u tools/probes/chain_probe.py chain_pre2.so
            cat $O/chain_probe_pre2.txt ;;
+    rowslab) step 300 pgemm_tests.log python -u -m pytest tests/test_pgemm_gpu.py -x -q --timeout 200 --timeout-method thread
+             tail -3 $O/pgemm_tests.log
+             for i in 1 2; do for rs in 0 1; do K8S_PGEMM_ROWSLAB=$rs step 400 bench_def_rs$rs.json python -u bench.py --steps 6 --warmup 2
+               echo "default rowslab=$rs: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_def_rs$rs.json | tr '\n' ' ')"; done; done ;;
+    gemmtests) step 400 gemm_tests.log python -u -m pytest tests/test_pgemm_gpu.py tests/test_mgemm_gpu.py tests/test_kernels_gpu.py -x -q --timeout 200 --timeout-method thread
+               tail -3 $O/gemm_tests.log ;;
+    mgemm_ab) for i in 1 2; do step 400 bench_b64_$i.json python -u bench.py --batch 64 --steps 2 --warmup 1
+                echo "b64 run $i: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_b64_$i.json | tr '\n' ' ')"
+                step 400 bench_tp8b64_$i.json python -u bench.py --simulate-tp 8 --batch 64 --steps 3 --warmup 1
+                echo "tp8sim b64 run $i: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_tp8b64_$i.json | tr '\n' ' ')"; done ;;
+    rsab2) for rs in 1 0 1 0; do K8S_PGEMM_ROWSLAB=$rs step 400 bench_tp8b64_rs$rs.json python -u bench.py --simulate-tp 8 --batch 64 --steps 3 --warmup 1
+             echo "tp8sim b64 rowslab=$rs: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_tp8b64_rs$rs.json | tr '\n' ' ')"
+             K8S_PGEMM_ROWSLAB=$rs step 400 bench_b64_rs$rs.json python -u bench.py --batch 64 --steps 2 --warmup 1
+             echo "b64 rowslab=$rs: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_b64_rs$rs.json | tr '\n' ' ')"
+             K8S_PGEMM_ROWSLAB=$rs step 400 bench_tp8_rs$rs.json python -u bench.py --simulate-tp 8 --steps 6 --warmup 2
+             echo "tp8sim rowslab=$rs: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_tp8_rs$rs.json | tr '\n' ' ')"; done ;;
+    rmsab3) for um in 0 64 0 64; do K8S_RMS_UNFUSED_MAX_M=$um step 400 bench_tp8b64_um$um.json python -u bench.py --simulate-tp 8 --batch 64 --steps 3 --warmup 1
+             echo "tp8sim b64 unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_tp8b64_um$um.json | tr '\n' ' ')"
+             K8S_RMS_UNFUSED_MAX_M=$um step 400 bench_b64_um$um.json python -u bench.py --batch 64 --steps 2 --warmup 1
+             echo "b64 unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_b64_um$um.json | tr '\n' ' ')"; done ;;
     mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only ${MGONLY:-qkv o_proj} --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
