@@ -61,6 +61,14 @@ for spec in ${RUNS:-tests smoke bench}; do
              echo "tp8sim b64 unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_tp8b64_um$um.json | tr '\n' ' ')"
              K8S_RMS_UNFUSED_MAX_M=$um step 400 bench_b64_um$um.json python -u bench.py --batch 64 --steps 2 --warmup 1
              echo "b64 unfused<=$um: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_step": [0-9.]*' $O/bench_b64_um$um.json | tr '\n' ' ')"; done ;;
+    ptune256) step 900 ptune256.txt python -u tools/pgemm_tune.py --tp 1 --m 256 --write --json-out $O/ptune256.json
+              cp k8s_llm_scheduler_amd/engine/assets/pgemm_gfx950.json $O/pgemm_gfx950_tuned.json
+              tail -12 $O/ptune256.txt
+              step 400 bench_default_tuned.json python -u bench.py --steps 6 --warmup 2
+              echo "default with the re-tuned 256-row plans: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_default_tuned.json | tr '\n' ' ')" ;;
+    ptunewide) step 1100 ptunewide.txt python -u tools/pgemm_tune.py --tp 1 8 4 --m 192 256 320 384 512 768 1024 2048 8192 --write --json-out $O/ptunewide.json
+               cp k8s_llm_scheduler_amd/engine/assets/pgemm_gfx950.json $O/pgemm_gfx950_wide.json
+               grep "pgemm >= library" $O/ptunewide.txt ;;
     mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only ${MGONLY:-qkv o_proj} --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
