@@ -69,6 +69,11 @@ for spec in ${RUNS:-tests smoke bench}; do
     ptunewide) step 1100 ptunewide.txt python -u tools/pgemm_tune.py --tp 1 8 4 --m 192 256 320 384 512 768 1024 2048 8192 --write --json-out $O/ptunewide.json
                cp k8s_llm_scheduler_amd/engine/assets/pgemm_gfx950.json $O/pgemm_gfx950_wide.json
                grep "pgemm >= library" $O/ptunewide.txt ;;
+    ptunefp8) step 1100 ptunefp8.txt python -u tools/pgemm_tune.py --fp8 --tp 1 4 --m 192 256 320 384 512 --write --json-out $O/ptunefp8.json
+              cp k8s_llm_scheduler_amd/engine/assets/pgemm_gfx950.json $O/pgemm_gfx950_fp8.json
+              grep "pgemm >= library" $O/ptunefp8.txt
+              step 400 bench_fp8_tuned.json python -u bench.py --dtype fp8 --steps 6 --warmup 2
+              echo "fp8 with the re-tuned plans: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_fp8_tuned.json | tr '\n' ' ')" ;;
     mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only ${MGONLY:-qkv o_proj} --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
