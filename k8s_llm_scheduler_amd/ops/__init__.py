@@ -642,8 +642,8 @@ def pgemm4(x: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, cfg: int = 0, 
 # bucket at or above it; past the largest tuned bucket, the largest one's (big tiles, no split-K: it only gets
 # better with more rows).
 _PG_TABLE: Optional[dict] = None
-PG_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "assets",
-                             "pgemm_gfx950.json")
+PG_TABLE_PATH = os.environ.get("K8S_PGEMM_TABLE_PATH") or os.path.join(   # (override: in-situ table A/B runs)
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "assets", "pgemm_gfx950.json")
 PG_MIN_M = 129      # below: mgemm's streaming tiles (batched decode, short prefill chunks)
 
 
