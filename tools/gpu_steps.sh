@@ -74,7 +74,9 @@ for spec in ${RUNS:-tests smoke bench}; do
               grep "pgemm >= library" $O/ptunefp8.txt
               step 400 bench_fp8_tuned.json python -u bench.py --dtype fp8 --steps 6 --warmup 2
               echo "fp8 with the re-tuned plans: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_fp8_tuned.json | tr '\n' ' ')" ;;
-    n256ab) for v in cur rs0 prev cur; do
+    n256ab) # prev: a table file placed at tmp_ab/pgemm_prev.json before the call (e.g. git show <rev>:<table>)
+            for v in cur rs0 prev cur; do
+              [ $v = prev ] && [ ! -f tmp_ab/pgemm_prev.json ] && continue
               case $v in cur) E="";; rs0) E="K8S_PGEMM_ROWSLAB=0";; prev) E="K8S_PGEMM_TABLE_PATH=$GRAFT_REPO_ROOT/tmp_ab/pgemm_prev.json";; esac
               env $E timeout -k 10 400 python -u bench.py --nodes 256 --max-model-len 32768 --steps 3 --warmup 1 > $O/n256_$v.json 2>&1 || { tail -5 $O/n256_$v.json; exit 1; }
               echo "n256 $v: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/n256_$v.json | tr '\n' ' ')"; done ;;
