@@ -80,7 +80,8 @@ def main() -> int:
                 starts = rel[:, 0]
                 live = ~torch.isnan(rel[:, 1])
                 ends = torch.nan_to_num(rel[:, 5], nan=-1)[live]
-                print(f"{tag} ctx={ctx:5d} pmax={pmax:2d} wgs={nwg:4d} {'cold' if cold else 'hot '}: total {end:5.2f} us; "
+                temp = 'cold' if cold else 'hot '
+                print(f"{tag} ctx={ctx:5d} pmax={pmax:2d} wgs={nwg:4d} {temp}: total {end:5.2f} us; "
                       f"entry spread {torch.nan_to_num(starts, nan=0).max().item():4.2f} us (live "
                       f"{torch.nan_to_num(starts[live], nan=0).max().item():4.2f}); partial stored p50/max "
                       f"{ends.median().item():4.2f}/{ends.max().item():4.2f} us")
