@@ -32,6 +32,10 @@ namespace {
 constexpr float SPLIT_LOG2E = 1.4426950408889634f;
 constexpr int SPLIT_CH = 64;  // context tokens per workgroup (one wave)
 constexpr int SC1 = 16;       // buffer-op cache policy: sc1 (L1 bypass, coherent at the L2)
+#ifndef SPLIT_QB_LANES
+#define SPLIT_QB_LANES 36       // merge: chunk accumulators per round trip x loads per chunk (G = 8: 9 chunks, the
+                                // bench's 465-528-token contexts in one round trip; 208 VGPRs, 2 waves / SIMD kept)
+#endif
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_split_t;
 
 // Timeline probe (tools/attn_trace.py builds this file with -DK8S_ATTN_TRACE into its own library):
@@ -342,7 +346,7 @@ __device__ __forceinline__ void split_body(
   constexpr int LPH = 64 / G, DPL = D / LPH;  // lanes per head, d per lane (DPL = 2G)
   constexpr int VW = (DPL % 4 == 0) ? 4 : 2;  // floats per load
   constexpr int NV = DPL / VW;                // loads per chunk
-  constexpr int QB = (32 / NV) > 0 ? 32 / NV : 1;
+  constexpr int QB = (SPLIT_QB_LANES / NV) > 0 ? SPLIT_QB_LANES / NV : 1;
   const int h = lane / LPH, d0 = (lane % LPH) * DPL;
   float buf[QB][DPL];
   auto load_batch = [&](int q0) {

@@ -29,7 +29,7 @@ STAGES = ("ctx+bt", "q+rope", "K+softmax", "V+PV", "store", "atomic", "out", "me
 
 
 def main() -> int:
-    lib = ctypes.CDLL(str(ROOT / "tools" / "probes" / "attn_trace.so"))
+    lib = ctypes.CDLL(str(ROOT / "tools" / "probes" / (sys.argv[1] if len(sys.argv) > 1 else "attn_trace.so")))
     lib.k8s_attn_trace_set.argtypes = [ctypes.c_void_p]
     lib.k8s_decode_split_workspace.restype = ctypes.c_longlong
     lib.k8s_decode_split_workspace.argtypes = [ctypes.c_int] * 4

@@ -83,6 +83,8 @@ for spec in ${RUNS:-tests smoke bench}; do
     mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only ${MGONLY:-qkv o_proj} --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
+    attnqb) for v in 32 "" 32 ""; do step 200 attn_trace_qb$v.txt python -u tools/attn_trace.py attn_trace$v.so
+              echo "== merge batch ${v:-36} lanes"; grep -A1 "TP=8 ctx=  564\|TP=1 ctx=  564 pmax= 9" $O/attn_trace_qb$v.txt | grep -v "^--"; done ;;
     sgemv) step 300 sgemv_tests.log python -u -m pytest tests/test_sgemv_gpu.py -x -q --timeout 200 --timeout-method thread
            tail -3 $O/sgemv_tests.log ;;
     sgprobe) step 300 sgemv_probe.txt python -u tools/sgemv_probe.py 5
