@@ -66,18 +66,27 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_kernel(
   // 16-byte column chunk idx%16) of K and V into registers while the current tile is computed,
   // then stores them swizzled into LDS.  Keys past the context: K clamped (their scores are
   // masked), V zero (P is 0 there, V must be finite).
+  // The block ids of a tile are requested one tile before its K/V (nbt): otherwise every prefetch is two dependent
+  // round trips (block id, then K/V) against one tile of math, and long contexts pay that chain once per tile.
   u32x4 kn[CPT], vn[CPT];
-  auto fetch = [&](int t) {
+  int nbt[CPT];
+  auto load_bt = [&](int t) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) nbt[c] = bt[min(t * KT + (tid + NT * c) / (D / 8), ctx - 1) / block_size];
+  };
+  auto fetch = [&](int t) {   // tile t's K/V with the ids in nbt, then tile t + 1's ids
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int idx = tid + NT * c;
       const int key = t * KT + idx / (D / 8), ch = idx % (D / 8);
       const int kc = min(key, ctx - 1);
-      const size_t off = (size_t)(bt[kc / block_size] * block_size + kc % block_size) * kv_stride + kvh * D + ch * 8;
+      const size_t off = (size_t)(nbt[c] * block_size + kc % block_size) * kv_stride + kvh * D + ch * 8;
       kn[c] = *reinterpret_cast<const u32x4*>(k_cache + off);
       vn[c] = key < ctx ? *reinterpret_cast<const u32x4*>(v_cache + off) : u32x4{0u, 0u, 0u, 0u};
     }
+    load_bt(t + 1);   // (keys past the context clamp to the last one: always a valid id)
   };
+  load_bt(0);
   fetch(0);
 
   // my (query, head) row (B operand columns / softmax rows)

@@ -80,6 +80,10 @@ for spec in ${RUNS:-tests smoke bench}; do
               case $v in cur) E="";; rs0) E="K8S_PGEMM_ROWSLAB=0";; prev) E="K8S_PGEMM_TABLE_PATH=$GRAFT_REPO_ROOT/tmp_ab/pgemm_prev.json";; esac
               env $E timeout -k 10 400 python -u bench.py --nodes 256 --max-model-len 32768 --steps 3 --warmup 1 > $O/n256_$v.json 2>&1 || { tail -5 $O/n256_$v.json; exit 1; }
               echo "n256 $v: $(grep -ho '"value": [0-9.]*\|"decode_ms_per_step": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/n256_$v.json | tr '\n' ' ')"; done ;;
+    pfattn) step 300 pfattn_tests.log python -u -m pytest tests/test_kernels_gpu.py -x -q -k "prefill" --timeout 120 --timeout-method thread
+            tail -2 $O/pfattn_tests.log
+            bash tools/gpu_prof.sh tp1_default_pf "" > $O/prof_pf.log 2>&1 || { tail -20 $O/prof_pf.log; exit 1; }
+            grep -A12 "last prefill" gpurun_out/lastfwd_tp1_default_pf.txt ;;
     mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only ${MGONLY:-qkv o_proj} --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
