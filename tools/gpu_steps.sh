@@ -84,6 +84,10 @@ for spec in ${RUNS:-tests smoke bench}; do
             tail -2 $O/pfattn_tests.log
             bash tools/gpu_prof.sh tp1_default_pf "" > $O/prof_pf.log 2>&1 || { tail -20 $O/prof_pf.log; exit 1; }
             grep -A12 "last prefill" gpurun_out/lastfwd_tp1_default_pf.txt ;;
+    redab) step 300 pgemm_tests.log python -u -m pytest tests/test_pgemm_gpu.py -x -q --timeout 200 --timeout-method thread
+           tail -2 $O/pgemm_tests.log
+           bash tools/gpu_prof.sh tp1_default_red "" > $O/prof_red.log 2>&1 || { tail -20 $O/prof_red.log; exit 1; }
+           grep -A12 "last prefill" gpurun_out/lastfwd_tp1_default_red.txt ;;
     mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only ${MGONLY:-qkv o_proj} --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
