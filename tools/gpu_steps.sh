@@ -88,6 +88,10 @@ for spec in ${RUNS:-tests smoke bench}; do
            tail -2 $O/pgemm_tests.log
            bash tools/gpu_prof.sh tp1_default_red "" > $O/prof_red.log 2>&1 || { tail -20 $O/prof_red.log; exit 1; }
            grep -A12 "last prefill" gpurun_out/lastfwd_tp1_default_red.txt ;;
+    awab) for aw in 0 8 0 8; do K8S_PREFILL_ATTN_WAVES=$aw step 400 bench_def_aw$aw.json python -u bench.py --steps 6 --warmup 2
+            echo "default attn waves=$aw: $(grep -ho '"value": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_def_aw$aw.json | tr '\n' ' ')"; done
+          for aw in 0 4; do K8S_PREFILL_ATTN_WAVES=$aw step 400 bench_n256_aw$aw.json python -u bench.py --nodes 256 --max-model-len 32768 --steps 3 --warmup 1
+            echo "n256 attn waves=$aw: $(grep -ho '"value": [0-9.]*\|"prefill_ms_per_decision": [0-9.]*' $O/bench_n256_aw$aw.json | tr '\n' ' ')"; done ;;
     mgtune64) step 300 mgtune64.txt python -u tools/mgemm_tune.py --tp 1 --m 64 --only ${MGONLY:-qkv o_proj} --verbose
               tail -40 $O/mgtune64.txt ;;
     attntr) step 200 attn_trace.txt python -u tools/attn_trace.py ;;
