@@ -175,7 +175,11 @@ def main() -> int:
             items.append((pe.construct_scheduling_prompt(pod, nodes), pod, list(nodes)))
         return items
 
-    prompt_tokens = len(eng.render_chat(svc.system_message, make_items()[0][0]))
+    # size check on a sample drawn from a COPY of the generator: the timed steps see exactly the snapshots they would
+    # without it (the reported prompt sizes below are those of the timed decisions themselves)
+    state = rng.getstate()
+    prompt_tokens = max(len(eng.render_chat(svc.system_message, p)) for p, _, _ in make_items())
+    rng.setstate(state)
     if prompt_tokens + args.gen_tokens > args.max_model_len:
         # the engine would reject every request and the bench would time the fallback path instead
         raise SystemExit(f"prompt ({prompt_tokens} tokens) + --gen-tokens {args.gen_tokens} exceeds --max-model-len "
@@ -204,6 +208,7 @@ def main() -> int:
     eng.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in eng.stats.items()})
     tp.rccl_calls = 0
     lat = []
+    log_mark = len(eng.finished_log)
     barrier()
     t0 = time.perf_counter()
     fallbacks = 0
@@ -214,6 +219,17 @@ def main() -> int:
         fallbacks += sum(d.fallback_needed for d in ds)
     barrier()
     elapsed = time.perf_counter() - t0
+    # the workload the timed region ran, per engine request (retries included): prompt tokens, tokens prefilled
+    # (prompt minus the prefix-cache hit) and tokens generated
+    timed = list(eng.finished_log)[log_mark:]
+
+    def dist_of(vals):
+        return {"mean": round(statistics.mean(vals), 1), "min": min(vals), "max": max(vals)} if vals else None
+
+    workload = {"engine_requests": len(timed),
+                "prompt_tokens": dist_of([e[4] for e in timed]),
+                "prefilled_tokens": dist_of([e[4] - e[5] for e in timed]),
+                "generated_tokens": dist_of([e[3] for e in timed])}
     if os.environ.get("K8S_ENGINE_TRACE") == "1" and rank == 0:   # host timeline of the last prefill (diagnostics)
         pf = [(t, m) for t, m in getattr(eng, "recovery_trace", []) if m.startswith("prefill")]
         last = max((i for i, (_, m) in enumerate(pf) if m.startswith("prefill: ") and "requests" in m), default=None)
@@ -247,8 +263,8 @@ def main() -> int:
         "config": {
             "model": f"{args.preset} (Llama-3.3-70B-Instruct architecture)" if "70b" in args.preset else args.preset,
             "global_batch": args.batch * dp,
-            "seq_len": prompt_tokens + args.gen_tokens,
-            "prompt_tokens": prompt_tokens,
+            "seq_len": round(workload["prompt_tokens"]["mean"] + args.gen_tokens) if timed else None,
+            "prompt_tokens": workload["prompt_tokens"]["mean"] if timed else None,
             "gen_tokens": args.gen_tokens,
             "cluster_nodes": args.nodes,
             "parallelism": (f"dp{dp}-" if dp > 1 else "") + f"tp{tp.world}" + ("-SIMULATED-no-comm" if tp.simulate else ""),
@@ -265,6 +281,7 @@ def main() -> int:
         "prefill_ms_per_decision": round(1000 * st["prefill_time"] / max(1, args.steps * args.batch), 2),
         "prefill_tokens_per_decision": round(st["prefill_tokens"] / max(1, args.steps * args.batch), 1),
         "prefill_graph_replays": st.get("prefill_graph_replays", 0),
+        "timed_workload": workload,
         "rccl_calls_timed": tp.rccl_calls,
         "prefill_overlap_chunks": st.get("prefill_overlap_chunks", 0),
         "speculative": {"tokens": args.speculative, "steps": st.get("spec_steps", 0),
@@ -393,8 +410,8 @@ def run_arrivals(args, eng, svc, prompt_tokens: int, init_s: float, tp, router=N
                 "decision_call": p50([p["ret"] - p["call"] for d, p, _ in ph]),
                 "decision_to_bind": p50([b - p["ret"] for d, p, b in ph])}
     fl = list(eng.finished_log)[args.warmup:]
-    ttft = sorted(f - a for a, f, _, _ in fl) or [0.0]
-    e2e = sorted(e - a for a, _, e, _ in fl) or [0.0]
+    ttft = sorted(e[1] - e[0] for e in fl) or [0.0]
+    e2e = sorted(e[2] - e[0] for e in fl) or [0.0]
     res = {
         "metric": "scheduling_decisions_per_sec",
         "value": round(len(lat) / span, 4),

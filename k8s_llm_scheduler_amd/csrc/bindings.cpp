@@ -37,7 +37,7 @@ int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, c
 void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* ks_out, int* splits_out);
 int k8s_sgemv(void* out, void* partial, const void* x, const void* W, const float* wscale, const void* res, int M,
               int N, int K, int epi, int norm, float eps, hipStream_t s);
-long long k8s_sgemv_workspace(int M, int N, int K, int epi);
+long long k8s_sgemv_workspace(int M, int N, int K, int epi, int fp8);
 int k8s_gemv_set_loop(int wg_per_cu);
 int k8s_gemv_set_wide(int on);
 int k8s_pgemm_set_prio(int mode);
@@ -206,7 +206,7 @@ PYBIND11_MODULE(_C, m) {
     if (rc != -5) check(rc, "sgemv");
     return rc;
   });
-  m.def("sgemv_workspace", [](int M, int N, int K, int epi) { return k8s_sgemv_workspace(M, N, K, epi); });
+  m.def("sgemv_workspace", [](int M, int N, int K, int epi, int fp8) { return k8s_sgemv_workspace(M, N, K, epi, fp8); });
   m.def("gemv_rms", [](uintptr_t out, uintptr_t partial, uintptr_t x, uintptr_t W, uintptr_t wscale, int M, int N,
                        int K, int epi, uintptr_t res_in, uintptr_t res_out, float eps, int64_t s) {
     check(k8s_gemv_rms(P(out), P(partial), P(x), P(W), P<float>(wscale), M, N, K, epi, P(res_in), P(res_out), eps, S(s)),

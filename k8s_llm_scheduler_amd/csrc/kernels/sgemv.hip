@@ -667,12 +667,10 @@ static int sm_cus() {
 static bool sm_take(int M, int K, bool fp8, SmPlan& p) { return M >= sm_min_m() && M <= 16 && sm_plan(K, fp8, p); }
 
 // Workspace floats for the partial slabs (0 when the plan has one k-group).
-extern "C" long long k8s_sgemv_workspace(int M, int N, int K, int epi) {
+// The same plan k8s_sgemv takes for these operands (fp8: e4m3 weights), so the slabs always fit.
+extern "C" long long k8s_sgemv_workspace(int M, int N, int K, int epi, int fp8) {
   SmPlan sp;
-  int g = sg_plan(K).g;
-  // (the fp8 flag is not known here: size for the larger of the two plans)
-  if (sm_take(M, K, false, sp)) g = sp.g;
-  if (sm_take(M, K, true, sp)) g = max(g, sp.g);
+  const int g = sm_take(M, K, fp8 != 0, sp) ? sp.g : sg_plan(K).g;
   if (g <= 1) return 0;
   return (long long)g * M * (epi == SG_SWIGLU ? 2 : 1) * N;
 }

@@ -1012,14 +1012,15 @@ class LLMEngine:
         elif dec:
             d = self._dev(dec, torch.long)
             ctx_d = self.s_ctx.index_select(0, d)
-            # (a row the device finished has context 0: clamped, it writes into its own first block, which its
-            # request still owns until the host reaps it, instead of indexing block -1)
+            # (a row the device finished has context 0: its position is clamped to 0 for the block lookup, and its
+            # leftover token's K/V goes nowhere (slot -1, skipped by the KV write) -- position 0 of its first block
+            # is usually a shared, published prefix block that other sequences and later prefix hits read)
             pos_d = (ctx_d - 1).clamp_min(0)
             blk = self.s_bt.index_select(0, d).gather(1, (pos_d // bs).long().unsqueeze(1)).squeeze(1)
             n_p = len(ids)
             ids_t = torch.cat([t(ids), self.s_tokens.index_select(0, d)])
             pos_t = torch.cat([t(pos), pos_d])
-            slot_t = torch.cat([t(slots), blk * bs + pos_d % bs])
+            slot_t = torch.cat([t(slots), torch.where(ctx_d > 0, blk * bs + pos_d % bs, torch.full_like(blk, -1))])
             cu_all = cu + [cu[-1] + k + 1 for k in range(len(dec))]
             ctx_t = torch.cat([t(ctx), ctx_d])
             bt_t = torch.cat([self._dev(bt), self.s_bt.index_select(0, d)])
@@ -1403,7 +1404,8 @@ class LLMEngine:
         r.finish_reason = reason
         r.finish_time = time.perf_counter()
         # (arrival, first token, finish, tokens) of the last requests: queueing vs service time
-        self.finished_log.append((r.arrival, r.first_token_time or r.finish_time, r.finish_time, len(r.output_ids)))
+        self.finished_log.append((r.arrival, r.first_token_time or r.finish_time, r.finish_time, len(r.output_ids),
+                                 len(r.prompt_ids), int(getattr(r, "cached", 0) or 0)))
         if r.done is not None:
             # background-loop request: its caller holds the object, so drop it from the table here (the
             # caller never waits for the engine lock, which the loop holds for a whole step)

@@ -284,7 +284,7 @@ def _sgemv(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rm
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     if out is None:
         out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x2.device)
-    ws = native().sgemv_workspace(M, N, K, epi)
+    ws = native().sgemv_workspace(M, N, K, epi, int(fp8))
     part = torch.empty(ws, dtype=F32, device=x2.device) if ws > 0 else None
     rc = native().sgemv(out.data_ptr(), part.data_ptr() if part is not None else 0, _chk(x2, BF16, "x"),
                         w.q.data_ptr() if fp8 else _chk(w, BF16, "w"), w.scale.data_ptr() if fp8 else 0,

@@ -229,7 +229,7 @@ class TPGroup:
             # one decision for the whole replica: a rank whose own communicator looks healthy (it never saw the
             # stall) must still take part in the rebuild the others need, or the collectives below do not match
             control.barrier(timeout_s)
-            rebuild = control.any_rank(rebuild)
+            rebuild = control.any_rank(rebuild, timeout_s)
         if rebuild:
             from .. import ops
 
@@ -399,13 +399,28 @@ class ControlChannel:
         dist.recv(buf, src=self.src, group=self.group, tag=3)
         return int(buf[0])
 
-    def any_rank(self, flag: bool) -> bool:
-        """True on every rank of the replica iff ``flag`` is true on any of them (every rank must call this)."""
+    _votes = 0
+
+    def any_rank(self, flag: bool, timeout_s: Optional[float] = None) -> bool:
+        """True on every rank of the replica iff ``flag`` is true on any of them (every rank must call this).
+        ``timeout_s``: a bounded vote through the process group's TCP store (each rank sets its key, then waits
+        for every rank's key at most that long and raises :class:`CollectiveError` otherwise) -- a rank that dies
+        between the recovery barrier and this vote cannot park the others for the group's default timeout."""
         if self.world <= 1:
             return bool(flag)
-        flags = [None] * self.world
-        dist.all_gather_object(flags, bool(flag), group=self.group)
-        return any(flags)
+        st = self.store() if timeout_s is not None else None
+        if st is None:
+            flags = [None] * self.world
+            dist.all_gather_object(flags, bool(flag), group=self.group)
+            return any(flags)
+        self._votes += 1
+        keys = [f"k8s_vote/{self.replica}/{self._votes}/{r}" for r in range(self.world)]
+        st.set(keys[self.rank], "1" if flag else "0")
+        try:
+            st.wait(keys, datetime.timedelta(seconds=timeout_s))
+        except Exception as e:  # noqa: BLE001 -- store timeout / store gone
+            raise CollectiveError(f"recovery vote timed out after {timeout_s:.0f}s on rank {self.rank}: {e}") from e
+        return any(st.get(k) == b"1" for k in keys)
 
     def broadcast_object(self, obj):
         box = [obj]

@@ -36,6 +36,11 @@ from .comm import TPGroup
 log = logging.getLogger(__name__)
 
 _STOP = "__stop__"
+_PING, _PONG = "__ping__", "__pong__"
+# Gloo link timeout: a stalled but live peer fails the link within this many seconds instead of parking the receive
+# threads for days (K8S_REPLICA_LINK_TIMEOUT_S; the engine watchdog's scale).  Idle links stay up through keepalives
+# sent every quarter of it (rank 0 pings, the remote leader answers).
+LINK_TIMEOUT_S = float(__import__("os").environ.get("K8S_REPLICA_LINK_TIMEOUT_S", "300"))
 
 
 class ReplicaLink:
@@ -43,8 +48,9 @@ class ReplicaLink:
     exactly one thread per side (so the collectives stay in the same order on both ranks).  Requests and replies
     carry ids: any number can be outstanding, replies arrive in completion order."""
 
-    def __init__(self, replica: int, leader: int, down, up):
+    def __init__(self, replica: int, leader: int, down, up, timeout_s: float = LINK_TIMEOUT_S):
         self.replica = replica
+        self.timeout_s = timeout_s
         self.leader = leader        # global rank of the remote replica's TP rank 0
         self.down = down            # rank 0 -> leader (requests, stop)
         self.up = up                # leader -> rank 0 (replies, stop acknowledgement)
@@ -55,6 +61,9 @@ class ReplicaLink:
         self._rx: Optional[threading.Thread] = None
         self.inflight = 0           # requests sent and not answered yet (router load)
         self.dead: Optional[str] = None   # set when the link failed: every later submit fails at once
+        self._last_send = time.monotonic()
+        self._ka: Optional[threading.Thread] = None
+        self._closing = threading.Event()
 
     @staticmethod
     def _bcast(obj, src: int, group):
@@ -74,6 +83,8 @@ class ReplicaLink:
                     msg = self._bcast(None, self.leader, self.up)
                     if msg == _STOP:
                         break
+                    if msg == _PONG:
+                        continue
                     with self._plock:
                         fut = self._pending.pop(msg["id"], None)
                     if fut is None:
@@ -90,6 +101,29 @@ class ReplicaLink:
         self._rx = threading.Thread(target=run, name=f"replica{self.replica}-rx", daemon=True)
         self._rx.start()
 
+        def keepalive():
+            every = max(0.05, self.timeout_s / 4)
+            while not self._closing.wait(every / 4):
+                if self.dead:
+                    return
+                if time.monotonic() - self._last_send < every:
+                    continue
+                try:
+                    self._send(_PING)
+                except Exception as e:  # noqa: BLE001
+                    self._close(f"replica {self.replica} link failed on keepalive: {type(e).__name__}: {e}")
+                    return
+
+        self._ka = threading.Thread(target=keepalive, name=f"replica{self.replica}-keepalive", daemon=True)
+        self._ka.start()
+
+    def _send(self, obj) -> None:
+        with self._send_lock:
+            if self._closing.is_set() and obj is not _STOP:
+                return
+            self._bcast(obj, 0, self.down)
+            self._last_send = time.monotonic()
+
     def _close(self, why: str) -> None:
         """Nothing more will be answered on this link: fail every pending future and every later submit."""
         with self._plock:
@@ -105,6 +139,7 @@ class ReplicaLink:
         self._start_rx()
         fut: Future = Future()
         rid = next(self._ids)
+        fut.rid = rid   # type: ignore[attr-defined]  (cancel() takes it)
         n = len(requests)
         with self._plock:
             if self.dead:
@@ -119,23 +154,23 @@ class ReplicaLink:
 
         fut.add_done_callback(done)
         try:
-            with self._send_lock:
-                self._bcast({"id": rid, "requests": list(requests)}, 0, self.down)
+            self._send({"id": rid, "requests": list(requests)})
         except Exception as e:  # noqa: BLE001
             self._close(f"replica {self.replica} link failed on send: {type(e).__name__}: {e}")
         return fut
 
-    def request(self, payload):
-        """Blocking form (one share, returns the leader's reply dict)."""
-        try:
-            return {"texts": self.submit(payload["requests"]).result()}
-        except RuntimeError as e:
-            return {"error": str(e)}
+    def cancel(self, fut: Future, why: str) -> None:
+        """Give up on a share (its caller's deadline passed): it leaves the pending table and the router's load
+        figure at once; a late reply is dropped."""
+        with self._plock:
+            self._pending.pop(getattr(fut, "rid", None), None)
+        if not fut.done():
+            fut.set_exception(TimeoutError(why))
 
     def stop(self) -> None:
         self._start_rx()
-        with self._send_lock:
-            self._bcast(_STOP, 0, self.down)
+        self._closing.set()
+        self._send(_STOP)
         self._rx.join(timeout=120)
 
     # ---- leader side
@@ -147,19 +182,21 @@ class ReplicaLink:
             self._bcast(payload, self.leader, self.up)
 
 
-def make_replica_links(tp: TPGroup) -> List[ReplicaLink]:
+def make_replica_links(tp: TPGroup, timeout_s: float = LINK_TIMEOUT_S) -> List[ReplicaLink]:
     """Collective over the world (every rank must call it).  Rank 0 gets one link per remote
-    replica, a remote leader gets its own link, every other rank an empty list."""
+    replica, a remote leader gets its own link, every other rank an empty list.  Every link operation is bounded
+    by ``timeout_s`` (idle links are kept alive by keepalives)."""
     links: List[ReplicaLink] = []
     if tp.replicas <= 1 or tp.simulate:
         return links
     me = tp.global_rank
+    tmo = datetime.timedelta(seconds=timeout_s)
     for r in range(1, tp.replicas):
         leader = r * tp.world
-        down = dist.new_group(ranks=[0, leader], backend="gloo", timeout=datetime.timedelta(days=7))
-        up = dist.new_group(ranks=[0, leader], backend="gloo", timeout=datetime.timedelta(days=7))
+        down = dist.new_group(ranks=[0, leader], backend="gloo", timeout=tmo)
+        up = dist.new_group(ranks=[0, leader], backend="gloo", timeout=tmo)
         if me in (0, leader):
-            links.append(ReplicaLink(r, leader, down, up))
+            links.append(ReplicaLink(r, leader, down, up, timeout_s))
     return links
 
 
@@ -211,6 +248,10 @@ class ReplicaRouterBackend:
         shares: List[List[int]] = [[] for _ in range(self.replicas)]
         for j, i in enumerate(where):
             shares[i].append(j)
+        # a remote share is waited for no longer than the call's deadline (plus a grace period for the reply),
+        # counted from the start of the call, not from the end of the local share
+        limits = [float(r.deadline_s) for r in requests if getattr(r, "deadline_s", None)]
+        end = time.monotonic() + min(limits) + self.reply_grace_s if limits else None
         futs = {i: self.links[i - 1].submit([requests[j] for j in shares[i]])
                 for i in range(1, self.replicas) if shares[i]}
         out: List[str] = [""] * len(requests)
@@ -224,16 +265,15 @@ class ReplicaRouterBackend:
         finally:
             with self._lock:
                 self._local_inflight -= len(shares[0])
-        # a remote share is waited for no longer than the call's deadline (plus a grace period for the reply)
-        limits = [float(r.deadline_s) for r in requests if getattr(r, "deadline_s", None)]
-        end = time.monotonic() + min(limits) + self.reply_grace_s if limits else None
         for i, fut in futs.items():
             try:
                 left = None if end is None else max(0.0, end - time.monotonic())
                 for j, text in zip(shares[i], fut.result(timeout=left)):
                     out[j] = text
             except FutureTimeout:
-                err = err or TimeoutError(f"replica {i} did not answer within the call deadline")
+                why = f"replica {i} did not answer within the call deadline"
+                self.links[i - 1].cancel(fut, why)
+                err = err or TimeoutError(why)
             except BaseException as e:  # noqa: BLE001
                 err = err or e
         if err is not None:
@@ -267,6 +307,9 @@ def serve_replica(backend, link: ReplicaLink, engine=None, workers: int = 64) ->
             msg = link.receive()
             if msg == _STOP:
                 break
+            if msg == _PING:
+                link.reply(_PONG)
+                continue
             pool.submit(handle, msg)
         pool.shutdown(wait=True)
         link.reply(_STOP)

@@ -32,6 +32,24 @@ def test_bench_json_line_contract():
     assert abs(d["vs_baseline"] - d["value"] / 0.3) < 0.01 * d["vs_baseline"] + 1e-3
 
 
+def test_bench_reports_the_timed_workload():
+    """with --nodes > 3 every timed step draws a fresh cluster, so the reported prompt / prefill
+    sizes must be those of the timed decisions (mean, min, max over the engine requests of the timed region), not one
+    pre-timing sample; the prefilled tokens must add up to the engine's own prefill counter."""
+    p = _run("--preset", "tiny", "--nodes", "6", "--steps", "3", "--warmup", "1", "--gen-tokens", "4",
+             "--max-model-len", "4096")
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    w = d["timed_workload"]
+    assert w["engine_requests"] == 3
+    pt, pf, gen = w["prompt_tokens"], w["prefilled_tokens"], w["generated_tokens"]
+    assert pt["min"] <= pt["mean"] <= pt["max"] and pt["min"] < pt["max"]      # fresh random clusters per step
+    assert d["config"]["prompt_tokens"] == pt["mean"]
+    assert 0 < pf["min"] and pf["max"] <= pt["max"]
+    assert abs(pf["mean"] - d["prefill_tokens_per_decision"]) < 1e-6 * pf["mean"] + 0.11
+    assert gen == {"mean": 4, "min": 4, "max": 4}
+
+
 def test_bench_arrival_mode():
     p = _run("--preset", "tiny", "--arrival-rate", "20", "--steps", "6", "--warmup", "1", "--batch", "4",
              "--gen-tokens", "8")

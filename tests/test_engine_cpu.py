@@ -388,6 +388,30 @@ def test_mixed_prefill_decode_steps_match_split_path():
     assert mixed == split and all(len(t) == 20 for t in mixed)
 
 
+def test_mixed_step_leaves_a_device_finished_rows_prefix_block_alone():
+    """a decode row the device has already finished (context 0, not yet reaped by the host) can ride
+    a mixed step.  Its leftover token's K/V must go nowhere: position 0 of its first block is the shared, published
+    prefix block (BOS / attention sink) that other sequences and later prefix hits read."""
+    eng = build_engine("tiny", device="cpu", max_batch=4, max_model_len=256, num_blocks=128, seed=1)
+    eng.mixed_steps = True
+    shared = [(i * 13) % 500 + 20 for i in range(40)]        # 2 full (published) blocks + 8 tokens
+    p = SamplingParams(max_tokens=30, temperature=0.0, ignore_eos=True)
+    a = eng.add_request(shared + [7, 8], p)
+    eng.step()
+    eng.step()
+    assert a.slot is not None and a in eng.running.values()
+    kv = eng.model.kv_cache
+    slot0 = a.blocks[0] * eng.block_size
+    before = kv[:, :, slot0].clone()
+    eng.s_ctx[a.slot:a.slot + 1].fill_(0)                    # the device finished row a (stop detected on device)
+    eng.add_request(shared + [9, 10, 11], p)                 # arrives: the next step is a mixed step with row a
+    n0 = eng.stats["mixed_steps"]
+    eng._admit()
+    eng._prefill()
+    assert eng.stats["mixed_steps"] == n0 + 1
+    assert torch.equal(kv[:, :, slot0], before)
+
+
 @pytest.mark.parametrize("tp", [2, 4, 8])
 def test_decision_prefill_buckets_stay_on_captured_xgmi(tp):
     """with the default slot size every decision-sized prefill bucket (<= 512 tokens, 8 MiB

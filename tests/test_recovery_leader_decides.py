@@ -103,3 +103,35 @@ def test_follower_finishes_a_rejected_request_and_keeps_serving():
     res = run_ranks(_reject_rank, 2, timeout_s=180)
     assert res[0]["big"] == "rejected" and res[0]["ok"] == "length" and res[0]["n"] == 4, res
     assert res[1]["ready"], res
+
+
+def _vote_rank(rank, world):
+    import time
+
+    import torch.distributed as dist
+
+    from k8s_llm_scheduler_amd.parallel import init_from_env, make_control_channel
+    from k8s_llm_scheduler_amd.parallel.comm import CollectiveError
+
+    tp = init_from_env("cpu", backend="gloo")
+    control = make_control_channel(tp)
+    both = control.any_rank(rank == 1, timeout_s=30)        # every rank votes: the flag of any rank wins
+    out = dict(both=both, raised=False, took=0.0)
+    if rank == 0:                                            # rank 1 "died" after the barrier: it never votes
+        t0 = time.monotonic()
+        try:
+            control.any_rank(False, timeout_s=2)
+        except CollectiveError:
+            out["raised"] = True
+        out["took"] = time.monotonic() - t0
+    dist.barrier()
+    dist.destroy_process_group()
+    return out
+
+
+def test_recovery_vote_is_bounded():
+    """the RCCL-rebuild vote after the monitored barrier is bounded by the recovery timeout (a store
+    vote), so a rank that dies between the two cannot park the others for the group's default timeout."""
+    res = run_ranks(_vote_rank, 2, timeout_s=120)
+    assert res[0]["both"] and res[1]["both"]
+    assert res[0]["raised"] and res[0]["took"] < 10

@@ -174,3 +174,55 @@ def test_link_failure_fails_pending_and_later_requests():
     except TimeoutError:
         pass
     assert _t.monotonic() - t0 < 5
+    # the timed-out share left the link's pending table and the router's load figure
+    assert router.links[0].inflight == 0 and not router.links[0]._pending
+
+
+def test_idle_link_sends_keepalives_and_leader_answers_them():
+    """links are bounded by a gloo timeout (K8S_REPLICA_LINK_TIMEOUT_S) instead of 7 days, so an
+    idle link must keep both directions busy: rank 0 pings every quarter of the timeout, the remote leader pongs, and
+    rank 0's receive thread drops the pongs."""
+    import threading
+    import time as _t
+
+    from k8s_llm_scheduler_amd.parallel import replicas as R
+
+    sent, up = [], []
+    pong = threading.Event()
+
+    class _Link(R.ReplicaLink):
+        def _bcast(self, obj, src, group):
+            if group == "up":
+                if src == 0:                       # (not used: rank 0 never sends on up)
+                    return obj
+                pong.wait(5)
+                pong.clear()
+                return R._PONG
+            sent.append(obj)
+            return obj
+
+    link = _Link(1, 4, "down", "up", timeout_s=0.2)
+    link._start_rx()
+    _t.sleep(0.5)
+    assert R._PING in sent and not link.dead
+    pong.set()
+    _t.sleep(0.05)
+    assert not link.dead and link.inflight == 0
+
+    # leader side: a ping is answered on the up link and never reaches the engine
+    class _Leader(R.ReplicaLink):
+        msgs = [R._PING, R._STOP]
+
+        def receive(self):
+            return self.msgs.pop(0)
+
+        def reply(self, payload):
+            up.append(payload)
+
+    class _Backend:
+        def complete(self, reqs):
+            raise AssertionError("a keepalive reached the engine")
+
+    R.serve_replica(_Backend(), _Leader(1, 4, "down", "up"), engine=None, workers=1)
+    assert up == [R._PONG, R._STOP]
+    link._closing.set()
