@@ -58,6 +58,13 @@ int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const v
                                float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax, int part,
                                hipStream_t s);
 long long k8s_decode_split_workspace(int B, int nq, int nkv, int pmax);
+int k8s_decode_persist_plan(int M, int H, int nq, int nkv, int I, int pmax, int* gl, int* grid);
+int k8s_decode_persist(const void* layers, int L, const void* x0, void* xout, int M, int H, int nq, int nkv, int I,
+                       float eps, float scale, const float* cos_sin, const int* block_tables, const int* context_lens,
+                       int max_blocks, int pmax, void* gran, void* part, uint32_t* counters, uint32_t* sync,
+                       void* trace, long long timeout_ticks, hipStream_t s);
+int k8s_decode_persist_layer_bytes();
+int k8s_decode_persist_trace_points();
 int k8s_decode_attention_split_oproj(void* attn, void* part, uint32_t* counters, const void* qkv, const float* cos_sin,
                                      void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
                                      float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks,
@@ -218,6 +225,23 @@ PYBIND11_MODULE(_C, m) {
     check(k8s_decode_attention_fused(P(out), P(pacc), P(pml), P(qkv), P<float>(cos_sin), P(kc), P(vc), P<int>(bt),
                                      P<int>(ctx), scale, B, nq, nkv, D, bs, max_blocks, pmax, part, S(s)),
           "decode_attention_fused");
+  });
+  // layer-persistent decode (decode_persist.hip): plan -> (rc, granules per (layer, row), grid); rc < 0: not taken
+  m.def("decode_persist_plan", [](int M, int H, int nq, int nkv, int I, int pmax) {
+    int gl = 0, grid = 0;
+    const int rc = k8s_decode_persist_plan(M, H, nq, nkv, I, pmax, &gl, &grid);
+    return py::make_tuple(rc, gl, grid);
+  });
+  m.def("decode_persist_layer_bytes", []() { return k8s_decode_persist_layer_bytes(); });
+  m.def("decode_persist_trace_points", []() { return k8s_decode_persist_trace_points(); });
+  m.def("decode_persist", [](uintptr_t layers, int L, uintptr_t x0, uintptr_t xout, int M, int H, int nq, int nkv,
+                             int I, float eps, float scale, uintptr_t cos_sin, uintptr_t bt, uintptr_t ctx,
+                             int max_blocks, int pmax, uintptr_t gran, uintptr_t part, uintptr_t counters,
+                             uintptr_t sync, uintptr_t trace, long long timeout_ticks, int64_t s) {
+    check(k8s_decode_persist(P(layers), L, P(x0), P(xout), M, H, nq, nkv, I, eps, scale, P<float>(cos_sin),
+                             P<int>(bt), P<int>(ctx), max_blocks, pmax, P(gran), P(part), P<uint32_t>(counters),
+                             P<uint32_t>(sync), P(trace), timeout_ticks, S(s)),
+          "decode_persist");
   });
   m.def("decode_split_workspace", [](int B, int nq, int nkv, int pmax) {
     return k8s_decode_split_workspace(B, nq, nkv, pmax);

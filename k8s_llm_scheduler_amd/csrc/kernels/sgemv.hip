@@ -273,11 +273,11 @@ __global__ void __launch_bounds__(256) sgemv_kernel(void* __restrict__ out, floa
 // (fp8: 72 with the conversions): VALU-bound at ~5 TB/s (fp8 ~3 TB/s), and it cannot hold 16 rows of x.  Here the
 // products run on v_mfma_f32_4x4x4bf16_1k -- 16 independent 4x4x4 blocks, lane 4b + i holding row i of block b
 // (A: weights, items = 4 k; B: x, column j = lane & 3; D: item i of lane 4b + j = D[i][j]; checked on the chip by
-// tools/probes/mfma4_layout.hip) -- so the VALU is free and the kernel is a pure weight stream again:
+// tools/experiments/mfma4_layout.hip) -- so the VALU is free and the kernel is a pure weight stream again:
 //  * one 16-byte-per-lane load covers 4 weight rows x 256 contiguous bytes (lane l: row l & 3, chunk l >> 2): the
 //    16 blocks are 16 consecutive chunks of the same 4 rows, each chunk two (bf16) or four (fp8) k-quads.  That
 //    access shape streams at ~6.2 TB/s where the 16x16x32 MFMA's A operand (16 rows x 64 B per load) manages ~5.0
-//    (tools/probes/ldpat.hip, profiles/sgemv_load_patterns_r4.txt);
+//    (tools/experiments/ldpat.hip, profiles/sgemv_load_patterns_r4.txt);
 //  * x lives in registers for the whole launch (B operand: x row 4 xg + (l & 3), the same chunks), MT / 4 groups
 //    of 4 rows; fp8 weights become bf16 k-quads with v_cvt_scalef32_pk_bf16_fp8 (x stays bf16, the row scale
 //    lands in the epilogue);

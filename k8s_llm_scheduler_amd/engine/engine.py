@@ -1230,10 +1230,12 @@ class LLMEngine:
             ev_t[1].record()
         tp = self.model.tp
         tp.snapshot_health()             # rides on the bounded wait below
+        self.model.snapshot_decode_health()
         if tr is not None:
             tr.append((time.monotonic(), "decode: fetch"))
         hist, nsteps = self._fetch(self.s_hist[:B], self.s_steps[:B], what="decode")
         tp.check_health()                # a failed collective raises into the decision service
+        self.model.check_decode_health()
         self.stats["decode_time"] += (ev_t[0].elapsed_time(ev_t[1]) / 1e3) if ev_t is not None \
             else time.perf_counter() - t0
         finished = []

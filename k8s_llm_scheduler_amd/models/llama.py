@@ -434,6 +434,8 @@ class LlamaModel:
         """One decode step for B sequences (one token each, positions from context_lens)."""
         B = tokens.shape[0]
         if self.device.type == "cuda" and B <= ops.GEMV_MAX_M and self.fused_decode:
+            if self.persist_decode_ok(B, max_context):
+                return self._forward_decode_persist(tokens, context_lens, block_tables, max_context)
             return self._forward_decode_fused(tokens, context_lens, block_tables, max_context)
         kv = self.kv_cache
         fused_attn = self.device.type == "cuda" and self.fused_decode   # batched decode (B > 8)
@@ -455,6 +457,47 @@ class LlamaModel:
 
 
     fused_decode = True
+
+    # ------------------------------------------------------------------ layer-persistent decode (ops/persist.py)
+    _persist = None
+    persist_decode = None        # None: follow K8S_DECODE_PERSIST; True / False: force (tests, A/B)
+
+    def persist_decode_ok(self, B: int, max_context: int) -> bool:
+        """Every decoder layer of the step in ONE launch (decode_persist.hip): TP = 1 or one simulated TP rank, bf16
+        weights, gammas folded, <= 2 sequences, contexts <= 4096, shapes the kernel plans."""
+        from ..ops import persist
+
+        on = persist.enabled() if self.persist_decode is None else self.persist_decode
+        if not on or self.device.type != "cuda" or not self.norm_folded or self.weight_dtype != "bf16":
+            return False
+        if not (self.tp.world == 1 or self.tp.simulate):
+            return False
+        if self._persist is None:
+            self._persist = persist.PersistentDecode(self)
+        return self._persist.supports(B, max_context)
+
+    def _forward_decode_persist(self, tokens: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
+                                max_context: int) -> torch.Tensor:
+        h = ops.embedding(tokens, self.embed)
+        x = self._persist.run(h, context_lens, block_tables, max_context)
+        logits = ops.linear_norm(x, self.lm_head, None, self.cfg.rms_eps, None, None, epi=ops.EPI_F32)
+        return self.tp.all_gather_shards(logits)
+
+    def snapshot_decode_health(self) -> None:
+        """Enqueue a copy of the persistent decode kernel's error word (read by check_decode_health after the
+        caller's own stream synchronisation)."""
+        if self._persist is not None:
+            self._persist.snapshot_error()
+
+    def check_decode_health(self) -> None:
+        """Raise CollectiveError if an in-kernel wait of the persistent decode timed out (its outputs are not
+        trustworthy); the kernel state is reset for the next step."""
+        if self._persist is not None:
+            e = self._persist.take_error()
+            if e:
+                from ..parallel.comm import CollectiveError
+
+                raise CollectiveError(f"persistent decode kernel: in-kernel wait timed out (error bits {e:#x})")
 
     # ------------------------------------------------------------------ decode weight prefetch (opt-in experiment)
     # K8S_DECODE_PREFETCH_MB = M > 0: after each layer's QKV GEMV a side stream reads the first M MB of that layer's

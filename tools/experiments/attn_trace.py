@@ -9,7 +9,7 @@ point is where the chain spends its microseconds.
 
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -DK8S_ATTN_TRACE \\
         -I k8s_llm_scheduler_amd/csrc/kernels k8s_llm_scheduler_amd/csrc/kernels/attn_decode_split.hip \\
-        -o tools/probes/attn_trace.so
+        -o tools/experiments/attn_trace.so
     python tools/attn_trace.py
 """
 
@@ -29,7 +29,7 @@ STAGES = ("ctx+bt", "q+rope", "K+softmax", "V+PV", "store", "atomic", "out", "me
 
 
 def main() -> int:
-    lib = ctypes.CDLL(str(ROOT / "tools" / "probes" / (sys.argv[1] if len(sys.argv) > 1 else "attn_trace.so")))
+    lib = ctypes.CDLL(str(ROOT / "tools" / "experiments" / (sys.argv[1] if len(sys.argv) > 1 else "attn_trace.so")))
     lib.k8s_attn_trace_set.argtypes = [ctypes.c_void_p]
     lib.k8s_decode_split_workspace.restype = ctypes.c_longlong
     lib.k8s_decode_split_workspace.argtypes = [ctypes.c_int] * 4

@@ -15,7 +15,7 @@
 // last arrival of the last phase re-arms the counter.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -I k8s_llm_scheduler_amd/csrc/kernels \
-//       tools/probes/chain.hip -o tools/probes/chain.so
+//       tools/experiments/chain.hip -o tools/experiments/chain.so
 #include "common.h"
 
 using namespace k8sllm;

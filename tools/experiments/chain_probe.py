@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Persistent GEMV chain vs separate launches (tools/probes/chain.hip): the measured cost of a kernel boundary in the
+"""Persistent GEMV chain vs separate launches (tools/experiments/chain.hip): the measured cost of a kernel boundary in the
 decode layer, the quantity behind VERDICT r3 item 2 (one launch per decode layer).
 
 Runs 8 layers x 4 projections (QKV, O, gate/up, down shapes of one TP rank of Llama-3.3-70B, distinct weights per
@@ -11,8 +11,8 @@ previous projection's output, both ways:
 and checks that both give identical outputs and that no barrier wait timed out.
 
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -I k8s_llm_scheduler_amd/csrc/kernels \\
-        tools/probes/chain.hip -o tools/probes/chain.so
-    python tools/probes/chain_probe.py [chain_pre2.so]   (built with -DCH_PRE2=1: two rows per wave in flight
+        tools/experiments/chain.hip -o tools/experiments/chain.so
+    python tools/experiments/chain_probe.py [chain_pre2.so]   (built with -DCH_PRE2=1: two rows per wave in flight
                                                           across each barrier instead of one)
 """
 
@@ -32,7 +32,7 @@ def shapes(tp: int):
 
 
 def main() -> int:
-    lib = ctypes.CDLL(str(ROOT / "tools" / "probes" / (sys.argv[1] if len(sys.argv) > 1 else "chain.so")))
+    lib = ctypes.CDLL(str(ROOT / "tools" / "experiments" / (sys.argv[1] if len(sys.argv) > 1 else "chain.so")))
     lib.chain_run.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3
     ncu = lib.chain_cus()
     dev = "cuda"
