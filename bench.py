@@ -93,6 +93,11 @@ def main() -> int:
         print(f"[bench rank {os.environ.get('RANK', '0')} +{time.perf_counter() - t_start:.1f}s] {msg}",
               file=sys.stderr, flush=True)
 
+    from k8s_llm_scheduler_amd.utils import stages
+
+    # every start-up stage is timed and bounded: one that outlives its bound exits with code 3 naming the stage
+    # (a rank parked in a collective cannot be interrupted otherwise; utils/stages.py, K8S_STAGE_TIMEOUT_*)
+    stages.install(int(os.environ.get("RANK", "0")))
     import torch
     import torch.distributed as dist
 
@@ -132,17 +137,19 @@ def main() -> int:
     per_seq = max(2048, args.max_model_len) + args.gen_tokens + bs   # KV blocks reserved per decision
     # serving (--arrival-rate): the engine's decode batch must hold the pods in flight, not --batch (pods per step)
     slots = max(1, args.batch, 16 if args.arrival_rate > 0 else 1)
-    eng = build_engine(args.preset, tp=tp, max_batch=slots, block_size=bs,
-                       num_blocks=max(slots, 2) * (per_seq // bs + 2) + 64,
-                       max_model_len=args.max_model_len, cuda_graphs=not args.no_graphs,
-                       prefix_caching=not args.no_prefix_cache, capture=False, decode_chunk=8,
-                       weight_dtype=args.dtype, speculative_tokens=args.speculative, control=control)
+    with stages.stage("engine_build"):
+        eng = build_engine(args.preset, tp=tp, max_batch=slots, block_size=bs,
+                           num_blocks=max(slots, 2) * (per_seq // bs + 2) + 64,
+                           max_model_len=args.max_model_len, cuda_graphs=not args.no_graphs,
+                           prefix_caching=not args.no_prefix_cache, capture=False, decode_chunk=8,
+                           weight_dtype=args.dtype, speculative_tokens=args.speculative, control=control)
     progress("engine built")
-    if eng.use_graphs:
-        eng.capture_graphs([b for b in (1, 2, 4, 6, 8, 16, 32, 48, 64) if b <= slots] or [1],
-                           nucleus=args.top_p < 1)
-    if on_gpu:
-        torch.cuda.synchronize()
+    with stages.stage("graph_capture"):
+        if eng.use_graphs:
+            eng.capture_graphs([b for b in (1, 2, 4, 6, 8, 16, 32, 48, 64) if b <= slots] or [1],
+                               nucleus=args.top_p < 1)
+        if on_gpu:
+            torch.cuda.synchronize()
     init_s = time.perf_counter() - t_init
     progress(f"graphs captured, init {init_s:.1f}s")
 
@@ -202,9 +209,24 @@ def main() -> int:
         if on_gpu:
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        svc.decide_many(make_items())
+    with stages.stage("warmup"):
+        for _ in range(args.warmup):
+            svc.decide_many(make_items())
+        if on_gpu:
+            torch.cuda.synchronize()
     progress("warmup done")
+    # per-stage start-up times of every rank (rank 0's and, per stage, the slowest rank's)
+    init_stages = {"rank0": stages.timings()}
+    if distributed:
+        every = [None] * dist.get_world_size()
+        dist.all_gather_object(every, stages.timings())
+        init_stages["rank0"] = every[0]
+        slowest = {}
+        for r, t in enumerate(every):
+            for k, v in t.items():
+                if k not in slowest or v > slowest[k][0]:
+                    slowest[k] = (v, r)
+        init_stages["slowest"] = {k: {"s": v, "rank": r} for k, (v, r) in slowest.items()}
     eng.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in eng.stats.items()})
     tp.rccl_calls = 0
     lat = []
@@ -290,6 +312,8 @@ def main() -> int:
         "init_s": round(init_s, 1),
         "physical_gpus": torch.cuda.device_count() if on_gpu else 0,
         "tp_comm": tp.comm_info,
+        "init_stages": init_stages,
+        "allreduce_transports": dict(sorted(tp.ar_log.items())),
         "baseline_note": "BASELINE.md publishes no numbers; vs_baseline uses the implied 0.3 decisions/s of test_e2e.py",
     }
     if rank == 0:

@@ -64,6 +64,10 @@ int k8s_decode_persist(const void* layers, int L, const void* x0, void* xout, in
                        int max_blocks, int pmax, void* gran, void* part, uint32_t* counters, uint32_t* sync,
                        void* trace, long long timeout_ticks, hipStream_t s);
 int k8s_decode_persist_layer_bytes();
+int k8s_xgemm_plan(int M, int N, int K, int epi, int rms, int* nslab, int* gps, long long* ws_floats,
+                   long long* rss_floats);
+int k8s_xgemm(void* out, void* ws, void* rss, const void* x, const void* W, const void* res, int M, int N, int K,
+              int epi, int rms, float eps, hipStream_t s);
 int k8s_decode_persist_trace_points();
 int k8s_decode_attention_split_oproj(void* attn, void* part, uint32_t* counters, const void* qkv, const float* cos_sin,
                                      void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
@@ -233,6 +237,17 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(rc, gl, grid);
   });
   m.def("decode_persist_layer_bytes", []() { return k8s_decode_persist_layer_bytes(); });
+  // activation-resident GEMM for 17-64 decode rows (xgemm.hip): plan -> (rc, slabs, groups, ws floats, rss floats)
+  m.def("xgemm_plan", [](int M, int N, int K, int epi, int rms) {
+    int ns = 0, g = 0;
+    long long wf = 0, rf = 0;
+    const int rc = k8s_xgemm_plan(M, N, K, epi, rms, &ns, &g, &wf, &rf);
+    return py::make_tuple(rc, ns, g, wf, rf);
+  });
+  m.def("xgemm", [](uintptr_t out, uintptr_t ws, uintptr_t rss, uintptr_t x, uintptr_t W, uintptr_t res, int M, int N,
+                    int K, int epi, int rms, float eps, int64_t s) {
+    check(k8s_xgemm(P(out), P(ws), P(rss), P(x), P(W), P(res), M, N, K, epi, rms, eps, S(s)), "xgemm");
+  });
   m.def("decode_persist_trace_points", []() { return k8s_decode_persist_trace_points(); });
   m.def("decode_persist", [](uintptr_t layers, int L, uintptr_t x0, uintptr_t xout, int M, int H, int nq, int nkv,
                              int I, float eps, float scale, uintptr_t cos_sin, uintptr_t bt, uintptr_t ctx,

@@ -396,6 +396,7 @@ class LlamaModel:
         all-reduces overlap the other half's GEMMs (``_layers_folded_overlap``)."""
         T = ids.shape[0]
         kv = self.kv_cache
+        self.tp.phase = "prefill"
 
         def attn(l: int, qkv: torch.Tensor) -> torch.Tensor:
             q = ops.rope_kv_write(qkv, self.cos_sin, kv[l, 0], kv[l, 1], self.nq, self.nkv, self.D,
@@ -433,6 +434,7 @@ class LlamaModel:
                        max_context: int) -> torch.Tensor:
         """One decode step for B sequences (one token each, positions from context_lens)."""
         B = tokens.shape[0]
+        self.tp.phase = "decode"
         if self.device.type == "cuda" and B <= ops.GEMV_MAX_M and self.fused_decode:
             if self.persist_decode_ok(B, max_context):
                 return self._forward_decode_persist(tokens, context_lens, block_tables, max_context)

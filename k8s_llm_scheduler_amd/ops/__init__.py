@@ -713,6 +713,34 @@ def gemm_route(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[str, Option
     return plan[0], plan[1:]
 
 
+# bf16 GEMMs of (SGEMV_MAX_M, XGEMM_MAX_M] rows (batched decode) run the activation-resident xgemm.hip (x held in
+# registers per K slab, the weights alone through a deep LDS ring) where it plans the shape (K8S_XGEMM=0: mgemm).
+XGEMM_MAX_M = 64
+XGEMM_ON = os.environ.get("K8S_XGEMM", "0") == "1"   # opt-in until it beats mgemm (docs/PERF.md)
+
+
+def xgemm(x: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, res: Optional[torch.Tensor] = None,
+          rms_eps: Optional[float] = None, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """epi(x[M, K] @ w.T) for 1..64 rows with bf16 weights on xgemm.hip (``rms_eps``: scaled by 1/rms of each x row,
+    the norm gamma folded into ``w``; ``res``: + res, bf16 epilogue, ``out`` may be ``res``).  None where the kernel
+    does not plan the shape."""
+    M, K = x.shape
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    rms = 1 if rms_eps is not None else 0
+    rc, ns, g, wf, rf = native().xgemm_plan(M, N, K, epi, rms)
+    if rc != 0:
+        return None
+    if out is None:
+        out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
+    ws = torch.empty(wf, dtype=F32, device=x.device)
+    rs = torch.empty(rf, dtype=F32, device=x.device) if rf > 0 else None
+    native().xgemm(out.data_ptr(), ws.data_ptr(), rs.data_ptr() if rs is not None else 0, _chk(x, BF16, "x"),
+                   _chk(w, BF16, "w"), _chk(res, BF16, "res") if res is not None else 0, M, N, K, epi, rms,
+                   float(rms_eps or 0.0), -1)
+    del ws, rs
+    return out
+
+
 def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
           out: Optional[torch.Tensor] = None, act=None) -> Optional[torch.Tensor]:
     """Routed hand-written GEMM of M > GEMV_MAX_M rows (None: the library route).  ``act``: the fp8 activations
@@ -725,6 +753,11 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
             return y
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     kern, plan = gemm_route(M, N, K, epi, fp8)
+    if (XGEMM_ON and not fp8 and act is None and M <= XGEMM_MAX_M and kern != "library"
+            and GEMM_BACKEND not in ("mgemm", "pgemm")):
+        y = xgemm(x2, w, epi, res=res, rms_eps=rms_eps, out=out)
+        if y is not None:
+            return y
     if kern == "library" or (fp8 and rms_eps is not None):
         return None   # (fp8: the activations are quantized after the norm, so the caller normalises first)
     if kern == "mgemm":
@@ -766,8 +799,10 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
             return ref.linear_swiglu(xa, w).to(BF16)
         return ref.linear(xa, w, F32 if epi == EPI_F32 else BF16)
     n_out = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    xg = (XGEMM_ON and not _is_fp8(w) and M <= XGEMM_MAX_M and GEMM_BACKEND == "auto"
+          and native().xgemm_plan(M, n_out, K, epi, 1)[0] == 0) if _gpu(r) else False
     if _gpu(r) and M > GEMV_MAX_M and (M <= SGEMV_MAX_M or M > RMS_PROLOGUE_MAX_UNFUSED or _is_fp8(w)
-                                       or n_out < RMS_UNFUSED_MIN_N):
+                                       or n_out < RMS_UNFUSED_MIN_N or xg):
         y = _gemm(r.contiguous(), w, epi, rms_eps=eps)
         if y is not None:
             return y

@@ -31,6 +31,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..utils.stages import stage
+
 
 _DT = {torch.bfloat16: 0, torch.float32: 1, torch.float16: 2, torch.int32: 3}
 log = logging.getLogger(__name__)
@@ -63,6 +65,14 @@ class TPGroup:
     # transport difference, and RCCL stays out of captured graphs (engine._prefill_bucket_capturable)
     capture_on_xgmi: bool = False
     rccl_calls: int = 0             # RCCL collectives issued from the host (a graph replay issues none)
+    # transport of every all-reduce issued from the host, "<phase>:<transport>:<bytes>" -> calls (a captured graph's
+    # all-reduces count once, at capture); ``phase`` is set by the model ("decode" / "prefill")
+    phase: str = "eager"
+    ar_log: dict = field(default_factory=dict)
+
+    def _log_ar(self, transport: str, nbytes: int) -> None:
+        k = f"{self.phase}:{transport}:{nbytes}"
+        self.ar_log[k] = self.ar_log.get(k, 0) + 1
 
     def _xgmi_ok(self, t: torch.Tensor, reduce: bool = False) -> bool:
         n = t.numel() * t.element_size()
@@ -81,7 +91,9 @@ class TPGroup:
         """In-place sum over the TP group; with ``residual`` the result is sum + residual (the xGMI
         kernels fuse the residual add, SURVEY K14 + K2; other transports add it afterwards)."""
         if self.world > 1 and not self.simulate:
+            nbytes = t.numel() * t.element_size()
             if t.dtype == torch.bfloat16 and t.is_contiguous() and self._xgmi_ok(t, reduce=True):
+                self._log_ar("xgmi", nbytes)
                 rp = 0
                 if residual is not None:
                     if residual.dtype != t.dtype or residual.shape != t.shape or not residual.is_contiguous():
@@ -90,9 +102,11 @@ class TPGroup:
                 self.xgmi.all_reduce_bf16(t.data_ptr(), t.data_ptr(), t.numel() * 2, -1, rp)
                 return t
             elif self.rccl is not None and t.is_cuda:
+                self._log_ar("rccl", nbytes)
                 self.rccl_calls += 1
                 self.rccl.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], 0, -1)
             elif self.backend == "gloo" and t.dtype == torch.bfloat16:
+                self._log_ar("gloo", nbytes)
                 f = t.float()
                 dist.all_reduce(f, group=self.group)
                 t.copy_(f)
@@ -115,6 +129,7 @@ class TPGroup:
                 and x.dim() == 2 and x.shape[0] <= ops.GEMV_MAX_M and (residual is None or residual.is_contiguous())):
             y = ops.gemv_allreduce(self.xgmi, x, w, residual)
             if y is not None:
+                self._log_ar("fused_gemv_ar", y.numel() * y.element_size())
                 return y
         y = ops.linear(x, w)
         return self.all_reduce_(y, residual=residual)
@@ -482,8 +497,9 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backe
             torch.cuda.set_device(local)
             if backend == "nccl":
                 kw["device_id"] = torch.device("cuda", local)
-        dist.init_process_group(backend, rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        with stage("process_group"):
+            dist.init_process_group(backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
     replica = rank // tp_size
     group = dist.group.WORLD
     if replicas > 1:   # collective: every rank creates every replica's group, in order
@@ -497,7 +513,8 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backe
         return tp   # pure data parallelism: no collectives inside the model
     if device_type == "cuda":
         if backend == "nccl" and comm in ("auto", "rccl"):
-            tp.rccl = make_rccl_comm(tp)
+            with stage("rccl_init"):
+                tp.rccl = make_rccl_comm(tp)
         if comm in ("auto", "xgmi"):
             tp.xgmi = make_xgmi_comm(tp)
         tune = os.environ.get("K8S_COMM_AUTOTUNE", "1")
@@ -505,7 +522,8 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600, backe
         # keep the built-in thresholds there unless forced
         own_gpu = torch.cuda.device_count() >= tp_size
         if tp.xgmi is not None and (tune == "force" or (tune == "1" and own_gpu)):
-            autotune_comm(tp)   # thresholds between the xGMI protocols (and RCCL, when present)
+            with stage("comm_autotune"):
+                autotune_comm(tp)   # thresholds between the xGMI protocols (and RCCL, when present)
         tp.comm_info["selected"] = "xgmi+rccl" if tp.xgmi is not None and tp.rccl is not None else \
             ("xgmi" if tp.xgmi is not None else ("rccl" if tp.rccl is not None else backend))
     return tp
@@ -573,25 +591,35 @@ def make_xgmi_comm(tp: TPGroup, slot_bytes: Optional[int] = None, blocks: Option
     info = [None] * tp.world
     dist.all_gather_object(info, (socket.gethostname(), dev, handle, err), group=tp.group)
     ok = all(h == info[0][0] and hd and not er for h, _, hd, er in info)
-    if ok:
-        try:
-            for _, d, _, _ in info:
-                if d != dev and not torch.cuda.can_device_access_peer(dev, d):
-                    raise RuntimeError(f"GPU {dev} cannot access GPU {d}")
-            comm.open([x[2] for x in info])
-        except Exception as e:  # noqa: BLE001
-            ok, err = False, str(e)
-    if not _agree(tp, ok):
+    with stage("xgmi_open"):
+        if ok:
+            try:
+                for _, d, _, _ in info:
+                    if d != dev and not torch.cuda.can_device_access_peer(dev, d):
+                        raise RuntimeError(f"GPU {dev} cannot access GPU {d}")
+                comm.open([x[2] for x in info])
+            except Exception as e:  # noqa: BLE001
+                ok, err = False, str(e)
+        ok = _agree(tp, ok)
+    if not ok:
         reasons = sorted({x[3] for x in info if x[3]} | ({err} if err else set()))
-        log.warning(f" xGMI peer-memory collectives disabled: {'; '.join(reasons) or 'a peer could not map memory'}")
+        why = '; '.join(reasons) or 'a peer could not map memory'
+        tp.comm_info["xgmi"] = f"disabled: {why}"
+        log.warning(f" xGMI peer-memory collectives disabled: {why}")
         return None
-    ok = _xgmi_selftest(tp, comm, dev)
-    if not _agree(tp, ok):
+    with stage("xgmi_selftest"):
+        ok = _agree(tp, _xgmi_selftest(tp, comm, dev))
+    if not ok:
+        tp.comm_info["xgmi"] = "disabled: self-test failed"
         log.warning(" xGMI peer-memory collectives disabled: self-test failed")
         return None
+    tp.comm_info["xgmi"] = "self-test passed"
     # the GEMV with the all-reduce in its epilogue (decode O / down projections): bit-exact against GEMV + the LL
     # all-reduce on this node's links, or the decode falls back to the separate kernels (same bits, one launch more)
-    if not _agree(tp, _fused_ar_selftest(tp, comm, dev)):
+    with stage("fused_ar_selftest"):
+        fused_ok = _agree(tp, _fused_ar_selftest(tp, comm, dev))
+    tp.comm_info["fused_gemv_ar_selftest"] = "passed" if fused_ok else "failed"
+    if not fused_ok:
         log.warning(" fused GEMV all-reduce disabled: self-test failed (decode uses GEMV + xGMI all-reduce)")
         tp.fused_ar = False
     return comm
