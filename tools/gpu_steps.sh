@@ -8,6 +8,8 @@
 #   prof        rocprofv3 kernel stats + last-forward timeline of the default bench (tools/gpu_prof.sh)
 #   proftp8     the same for --simulate-tp 8 (PERSIST=0/1)
 #   kbench      tools/kbench.py per-kernel microbench at TP=1 and TP=8 shapes
+#   nodes256    bench.py --nodes 256 (22k-token prompts), 10 timed steps
+#   gen200      bench.py --gen-tokens 200 (the reference's max_tokens) at TP=1 and --simulate-tp 8
 #   persist     the layer-persistent decode: its GPU tests, then --simulate-tp 8 and Llama-3-8B A/B (off vs on)
 # Each step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault (any other
 # rc) ends the script.  Logs land in gpurun_out/$OUT (default run).
@@ -38,6 +40,12 @@ for spec in ${RUNS:-tests smoke bench}; do
     prof)    step 700 prof_default.log bash tools/gpu_prof.sh default ""; cat "$O/prof_default.log" | head -25 ;;
     proftp8) K8S_DECODE_PERSIST=${PERSIST:-0} step 700 prof_tp8sim.log bash tools/gpu_prof.sh tp8sim_p${PERSIST:-0} "--simulate-tp 8"
              head -25 "$O/prof_tp8sim.log" ;;
+    nodes256) step 900 bench_nodes256.json python -u bench.py --nodes 256 --max-model-len 32768 --steps ${STEPS:-10} --warmup 1
+             tail -1 "$O/bench_nodes256.json" ;;
+    gen200)  step 600 bench_gen200.json python -u bench.py --gen-tokens 200 --steps ${STEPS:-10} --warmup 2
+             tail -1 "$O/bench_gen200.json"
+             step 400 bench_tp8sim_gen200.json python -u bench.py --gen-tokens 200 --simulate-tp 8 --steps ${STEPS:-10} --warmup 2
+             tail -1 "$O/bench_tp8sim_gen200.json" ;;
     kbench)  step 300 kbench_tp1.txt python -u tools/kbench.py --tp 1; step 300 kbench_tp8.txt python -u tools/kbench.py --tp 8 ;;
     persist) step 600 persist_tests.log $PT tests/test_persist_gpu.py; tail -3 "$O/persist_tests.log"
              for p in 0 1; do
