@@ -91,6 +91,7 @@ int k8s_prefetch(const void* p, long long bytes, int blocks, void* sink, hipStre
 int k8s_hash_init(void* out, int rows, int cols, long long gcols, long long row0, long long col0, uint32_t seed,
                   uint32_t tensor_id, float scale, float shift, hipStream_t s);
 int k8s_mgemm_num_configs();
+int k8s_mgemm_lds_bytes(int cfg, int mode);
 int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* lds_bytes, int* swiglu, int* rb);
 int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, long long* tiles, int* cmax,
                         long long* ws_elems);
@@ -328,6 +329,7 @@ PYBIND11_MODULE(_C, m) {
     }
     return out;
   });
+  m.def("mgemm_lds_bytes", [](int cfg, int mode) { return k8s_mgemm_lds_bytes(cfg, mode); });
   m.def("mgemm_plan_info", [](int M, int N, int K, int epi, int fp8, int cfg, int nwg) {
     long long tiles = 0, ws = 0;
     int cmax = 0;

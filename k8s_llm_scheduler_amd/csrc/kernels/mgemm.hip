@@ -24,6 +24,12 @@
 //    second kernel; the ticket is reset by the reducer).
 //  * fp8: activations are quantized per token (fp8.hip), weights per row; the epilogue applies
 //    sx[m] * sw[n].  Non-scaled fp8 MFMA runs at the bf16 rate but halves the staged bytes.
+//  * fp8 weights x bf16 activations (W8, host mode fp8 = 2; the batched-decode regime): no activation
+//    quantization at all -- x is staged as bf16 (twice the row bytes of the weight k-step), every lane turns
+//    its 8 e4m3 weights of a k32 step into bf16 with v_cvt_scalef32_pk_bf16_fp8 (exact) and the MFMA is the
+//    bf16 one, the same rate as the non-scaled fp8 MFMA.  The weight bytes streamed are the fp8 ones; the RMS
+//    prologue works as for bf16 (the un-normalised residual is the x operand), so the fp8 QKV / gate-up / O /
+//    down projections of a 17-128-row decode step launch no quantize kernel.
 #include "common.h"
 
 namespace k8sllm {
@@ -65,9 +71,10 @@ struct MgArgs {
   unsigned* cnt;         // [tiles] arrival tickets, zero between launches
   const uint8_t* x;      // [M][K] bf16 or e4m3
   const uint8_t* W;      // [rows][K] bf16 or e4m3
-  const float* xs;       // fp8: [M] per-token activation scales
+  const float* xs;       // fp8 activations: [M] per-token activation scales
   const float* wsc;      // fp8: [rows] per-row weight scales
-  long long kbytes;      // bytes per row of x / W
+  long long kbytes;      // bytes per row of W (and of x, except W8: x rows are bf16, xkbytes)
+  long long xkbytes;     // bytes per row of x
   long long total;       // tiles * T work items (one item = one tile x one 128-byte k-step)
   int M, N_out, half_rows;
   int m_tiles, T;        // T: 128-byte k-steps over the whole K
@@ -87,7 +94,7 @@ __device__ __forceinline__ int mg_swz_rb(int r) {
   return RB == 64 ? ((r >> 2) & 3) : RB == 128 ? ((r >> 1) & 7) : (r & 15);
 }
 
-template <int BM, int BN, int WM, int WN, int WK, int RB, int S, int EPI, bool FP8>
+template <int BM, int BN, int WM, int WN, int WK, int RB, int S, int EPI, bool FP8, bool W8 = false>
 __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   constexpr int NW = WM * WN * WK;
   constexpr int FM = BM / (WM * 16), FN = BN / (WN * 16);
@@ -96,12 +103,14 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert(S >= 2 && S <= 8, "ring depth");
   static_assert(WN == 1 || WN == 2 || WN == 4, "the RMS prologue splits a fragment's 4 dot2 over WN waves");
   static_assert(RB == 64 || RB == 128 || RB == 256 || RB == 512, "row bytes per k-step");
-  constexpr int CPR = RB / 16;                       // 16-byte chunks per staged row
-  constexpr int KS = FP8 ? RB / 32 : RB / 64;        // k32 MFMA steps per k-step (RB = 64: one)
+  static_assert(!(FP8 && W8), "W8: fp8 weights with bf16 activations");
+  constexpr int XRB = W8 ? 2 * RB : RB;              // x row bytes per k-step (W8: RB bf16 values)
+  constexpr int CPR = RB / 16, XCPR = XRB / 16;      // 16-byte chunks per staged W / x row
+  constexpr int KS = (FP8 || W8) ? RB / 32 : RB / 64;   // k32 MFMA steps per k-step (RB = 64: one)
   static_assert(KS % WK == 0, "k32 steps split evenly over WK waves");
-  constexpr int WREG = BN * RB, STAGE_B = (BM + BN) * RB;
-  static_assert((BN * CPR) % NW == 0 && (BM * CPR) % NW == 0, "chunks per wave");
-  constexpr int WCH = BN * CPR / NW, XCH = BM * CPR / NW;  // 16-byte chunks per wave per stage
+  constexpr int WREG = BN * RB, STAGE_B = BN * RB + BM * XRB;
+  static_assert((BN * CPR) % NW == 0 && (BM * XCPR) % NW == 0, "chunks per wave");
+  constexpr int WCH = BN * CPR / NW, XCH = BM * XCPR / NW;  // 16-byte chunks per wave per stage
   constexpr int WI = (WCH + 63) / 64, XI = (XCH + 63) / 64, LPS = WI + XI;
   static_assert((S - 2) * LPS <= 63, "vmcnt range");
   static_assert(WK == 1 || (WK - 1) * FN * FM * 64 * 16 * WM * WN <= S * STAGE_B, "LDS reduction space");
@@ -148,7 +157,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     // per-lane DMA sources as 32-bit offsets from the operand bases (swizzle on the source,
     // lane-linear LDS destination); the host checks that every operand spans < 4 GiB
     const uint8_t* wseg = a.W + (long long)kb * RB;
-    const uint8_t* xseg = a.x + (long long)kb * RB;
+    const uint8_t* xseg = a.x + (long long)kb * XRB;
     uint32_t woff[WI], xoff[XI];
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
@@ -166,14 +175,14 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int p = wid * XCH + min(i * 64 + lane, XCH - 1);
-      const int r = p / CPR, c = (p % CPR) ^ mg_swz_rb<RB>(p / CPR);
-      xoff[i] = (uint32_t)min(mt * BM + r, a.M - 1) * (uint32_t)a.kbytes + (uint32_t)(c * 16);
+      const int r = p / XCPR, c = (p % XCPR) ^ mg_swz_rb<XRB>(p / XCPR);
+      xoff[i] = (uint32_t)min(mt * BM + r, a.M - 1) * (uint32_t)a.xkbytes + (uint32_t)(c * 16);
     }
 
     auto issue = [&](int t, int stage) {
       char* sb = lds + stage * STAGE_B;
       const uint8_t* wb = wseg + (long long)t * RB;
-      const uint8_t* xb = xseg + (long long)t * RB;
+      const uint8_t* xb = xseg + (long long)t * XRB;
 #pragma unroll
       for (int i = 0; i < WI; ++i) {
         if (WCH % 64 == 0 || i * 64 + lane < WCH)
@@ -199,6 +208,15 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
 #pragma unroll
     for (int j = 0; j < FM; ++j) ss[j] = 0.f;
     const bool do_rms = !FP8 && a.rms != 0;
+    // 8 e4m3 weights -> the bf16x8 A operand (exact; the row scale is applied in the epilogue)
+    auto w8_frag = [](long q) {
+      const uint32_t lo = (uint32_t)q, hi = (uint32_t)((unsigned long)q >> 32);
+      const bf16x2 p0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, false);
+      const bf16x2 p1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, true);
+      const bf16x2 p2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, false);
+      const bf16x2 p3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, true);
+      return bf16x8{p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
+    };
 
     auto compute = [&](int stage) {
       const char* wb = lds + stage * STAGE_B;
@@ -209,13 +227,21 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
         if constexpr (!FP8) {
           const int c = kk * 4 + g;
           bf16x8 af[FN], bfr[FM];
+          if constexpr (W8) {   // lane: 8 e4m3 of k = 32 kk + 8 g .. +8 (8 bytes of chunk 2 kk + g / 2)
+            const int cw = kk * 2 + (g >> 1), hb = (g & 1) * 8;
 #pragma unroll
-          for (int f = 0; f < FN; ++f)
-            af[f] = *reinterpret_cast<const bf16x8*>(wb + arow[f] * RB + ((c ^ mg_swz_rb<RB>(arow[f])) << 4));
+            for (int f = 0; f < FN; ++f)
+              af[f] = w8_frag(
+                  *reinterpret_cast<const long*>(wb + arow[f] * RB + ((cw ^ mg_swz_rb<RB>(arow[f])) << 4) + hb));
+          } else {
+#pragma unroll
+            for (int f = 0; f < FN; ++f)
+              af[f] = *reinterpret_cast<const bf16x8*>(wb + arow[f] * RB + ((c ^ mg_swz_rb<RB>(arow[f])) << 4));
+          }
 #pragma unroll
           for (int j = 0; j < FM; ++j) {
             const int r = brow0 + j * 16;
-            bfr[j] = *reinterpret_cast<const bf16x8*>(xb + r * RB + ((c ^ mg_swz_rb<RB>(r)) << 4));
+            bfr[j] = *reinterpret_cast<const bf16x8*>(xb + r * XRB + ((c ^ mg_swz_rb<XRB>(r)) << 4));
           }
 #pragma unroll
           for (int f = 0; f < FN; ++f)
@@ -383,7 +409,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
       const int m = mt * BM + wm * (BM / WM) + j * 16 + li;
       if (m >= a.M) continue;
       float sx = FP8 ? a.xs[m] : 1.f;
-      if (do_rms) sx = rsqrtf(rss[wm * (BM / WM) + j * 16 + li] / (float)(a.kbytes >> 1) + a.eps);
+      if (do_rms) sx = rsqrtf(rss[wm * (BM / WM) + j * 16 + li] / (float)(a.xkbytes >> 1) + a.eps);
       if constexpr (EPI == MG_SWIGLU) {
 #pragma unroll
         for (int f = 0; f < FN / 2; ++f) {
@@ -393,7 +419,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float gt = acc[f][j][i] * sx, up = acc[f + FN / 2][j][i] * sx;
-            if (FP8) { gt *= a.wsc[n0 + i]; up *= a.wsc[a.half_rows + n0 + i]; }
+            if (FP8 || W8) { gt *= a.wsc[n0 + i]; up *= a.wsc[a.half_rows + n0 + i]; }
             v[i] = mg_silu(gt) * up;
           }
           u32x2 o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
@@ -406,7 +432,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
           if (n0 >= a.N_out) continue;
           float v[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = acc[f][j][i] * sx * (FP8 ? a.wsc[n0 + i] : 1.f);
+          for (int i = 0; i < 4; ++i) v[i] = acc[f][j][i] * sx * ((FP8 || W8) ? a.wsc[n0 + i] : 1.f);
           if constexpr (EPI == MG_F32) {
             *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + (long long)m * a.N_out + n0) =
                 f32x4{v[0], v[1], v[2], v[3]};
@@ -470,37 +496,50 @@ constexpr MgCfg kMgCfgs[] = {
     {256, 128, 2, 2, 1, 64, 5},   // 25
     {128, 256, 2, 4, 1, 64, 6},   // 26  8 waves
     {256, 128, 2, 4, 1, 64, 5},   // 27  8 waves
+    // --- 64-row weight-streaming tiles whose W8 image (x staged as bf16) fits: 4-deep rings of 128-byte k-steps
+    {64, 32, 2, 1, 2, 128, 4},    // 28
+    {64, 64, 2, 2, 1, 128, 4},    // 29
+    {64, 128, 1, 4, 1, 128, 4},   // 30
+    {64, 64, 2, 2, 2, 128, 4},    // 31  8 waves, k-shared
 };
 constexpr int kMgNumCfgs = sizeof(kMgCfgs) / sizeof(kMgCfgs[0]);
 
-template <int C, int EPI, bool FP8>
+// LDS bytes of config c in mode (0 bf16, 1 fp8 x and W, 2 W8: fp8 W, bf16 x)
+constexpr int mg_lds_bytes(const MgCfg c, int mode) {
+  return c.s * (c.bn * c.rb + c.bm * c.rb * (mode == 2 ? 2 : 1)) + 16 + c.wk * c.wn * c.bm * 4;
+}
+// W8 is built for the weight-streaming configurations (batched decode) only
+constexpr bool mg_w8_cfg(int c) { return c <= 14 || c >= 28; }
+
+template <int C, int EPI, bool FP8, bool W8>
 int mg_launch(const MgArgs& a, int grid, hipStream_t s) {
-  constexpr bool ok = EPI != MG_SWIGLU || (kMgCfgs[C].bn / (kMgCfgs[C].wn * 16)) % 2 == 0;
+  constexpr bool ok = (EPI != MG_SWIGLU || (kMgCfgs[C].bn / (kMgCfgs[C].wn * 16)) % 2 == 0) &&
+                      (!W8 || (mg_w8_cfg(C) && mg_lds_bytes(kMgCfgs[C], 2) <= 160 * 1024));
   if constexpr (!ok) {
     return -2;
   } else {
     hipLaunchKernelGGL((mgemm_kernel<kMgCfgs[C].bm, kMgCfgs[C].bn, kMgCfgs[C].wm, kMgCfgs[C].wn, kMgCfgs[C].wk,
-                                      kMgCfgs[C].rb, kMgCfgs[C].s, EPI, FP8>),
+                                      kMgCfgs[C].rb, kMgCfgs[C].s, EPI, FP8, W8>),
                        dim3(grid), dim3(64 * kMgCfgs[C].wm * kMgCfgs[C].wn * kMgCfgs[C].wk), 0, s, a);
     return (int)hipGetLastError();
   }
 }
 
-template <int C, bool FP8>
+template <int C, bool FP8, bool W8>
 int mg_epi(const MgArgs& a, int grid, int epi, hipStream_t s) {
   switch (epi) {
-    case MG_BF16: return mg_launch<C, MG_BF16, FP8>(a, grid, s);
-    case MG_F32: return mg_launch<C, MG_F32, FP8>(a, grid, s);
-    case MG_SWIGLU: return mg_launch<C, MG_SWIGLU, FP8>(a, grid, s);
+    case MG_BF16: return mg_launch<C, MG_BF16, FP8, W8>(a, grid, s);
+    case MG_F32: return mg_launch<C, MG_F32, FP8, W8>(a, grid, s);
+    case MG_SWIGLU: return mg_launch<C, MG_SWIGLU, FP8, W8>(a, grid, s);
   }
   return -2;
 }
 
-template <bool FP8, int C = 0>
+template <bool FP8, bool W8, int C = 0>
 int mg_cfg(const MgArgs& a, int grid, int cfg, int epi, hipStream_t s) {
   if constexpr (C < kMgNumCfgs) {
-    if (cfg == C) return mg_epi<C, FP8>(a, grid, epi, s);
-    return mg_cfg<FP8, C + 1>(a, grid, cfg, epi, s);
+    if (cfg == C) return mg_epi<C, FP8, W8>(a, grid, epi, s);
+    return mg_cfg<FP8, W8, C + 1>(a, grid, cfg, epi, s);
   } else {
     return -4;
   }
@@ -509,6 +548,14 @@ int mg_cfg(const MgArgs& a, int grid, int cfg, int epi, hipStream_t s) {
 }  // namespace
 
 extern "C" int k8s_mgemm_num_configs() { return kMgNumCfgs; }
+
+// LDS bytes of a config in a mode (0 bf16, 1 fp8, 2 W8); -1: the config is not built for that mode.
+extern "C" int k8s_mgemm_lds_bytes(int cfg, int mode) {
+  if (cfg < 0 || cfg >= kMgNumCfgs || mode < 0 || mode > 2) return -1;
+  const int b = mg_lds_bytes(kMgCfgs[cfg], mode);
+  if (mode == 2 && (!mg_w8_cfg(cfg) || b > 160 * 1024)) return -1;
+  return b;
+}
 
 // (bm, bn) of a config: the Python planner sizes grids from them.
 extern "C" int k8s_mgemm_config(int cfg, int* bm, int* bn, int* threads, int* lds_bytes, int* swiglu, int* rb) {
@@ -557,23 +604,28 @@ extern "C" int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, in
 }
 
 // out[M, N_out] = epi(x[M, K] . W^T) with `nwg` workgroups streaming equal shares of the
-// (tile, k-step) items.  fp8: x / W are e4m3 bytes with per-row scales xs / wsc.
+// (tile, k-step) items.  fp8 = 1: x / W are e4m3 bytes with per-row scales xs / wsc; fp8 = 2 (W8): W is e4m3
+// with row scales wsc, x is bf16 (no activation scales; the RMS prologue is allowed).
 // SwiGLU: W holds 2 * N_out rows ([gate; up]); out has N_out columns.
 extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs,
                          const float* wsc, int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax,
                          const void* res, int rms, float eps, hipStream_t stream) {
   if (cfg < 0 || cfg >= kMgNumCfgs || M <= 0 || N_out <= 0 || K <= 0 || nwg <= 0 || cmax < 1) return -1;
   if (N_out % 4 != 0) return -1;
-  const long long kbytes = (long long)K * (fp8 ? 1 : 2);
+  if (fp8 < 0 || fp8 > 2) return -1;
+  const bool w8 = fp8 == 2;
+  const long long kbytes = (long long)K * (fp8 ? 1 : 2), xkbytes = (long long)K * (fp8 == 1 ? 1 : 2);
   if (kbytes % kMgCfgs[cfg].rb != 0) return -1;
+  if (w8 && k8s_mgemm_lds_bytes(cfg, 2) < 0) return -4;
   const MgGeom g = mg_geom(M, N_out, K, epi, fp8, cfg);
   if (nwg > g.total) return -1;
   if (cmax > 1 && (ws == nullptr || tickets == nullptr)) return -3;
   const long long wrows = epi == MG_SWIGLU ? 2LL * N_out : (long long)N_out;
-  if (wrows * kbytes >= (1LL << 32) || (long long)M * kbytes >= (1LL << 32)) return -5;  // 32-bit DMA offsets
-  if (fp8 && (xs == nullptr || wsc == nullptr)) return -3;
+  if (wrows * kbytes >= (1LL << 32) || (long long)M * xkbytes >= (1LL << 32)) return -5;  // 32-bit DMA offsets
+  if (fp8 == 1 && (xs == nullptr || wsc == nullptr)) return -3;
+  if (w8 && wsc == nullptr) return -3;
   if (res != nullptr && epi != MG_BF16) return -6;   // residual epilogue: bf16 output only
-  if (rms && fp8) return -6;                         // fp8: activations are quantized before the GEMM
+  if (rms && fp8 == 1) return -6;                    // fp8 activations are quantized before the GEMM
   MgArgs a;
   a.res = static_cast<const bf16_t*>(res);
   a.rms = rms;
@@ -586,6 +638,7 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.xs = xs;
   a.wsc = wsc;
   a.kbytes = kbytes;
+  a.xkbytes = xkbytes;
   a.total = g.total;
   a.M = M;
   a.N_out = N_out;
@@ -594,5 +647,6 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.T = (int)g.T;
   a.nwg = nwg;
   a.cmax = cmax;
-  return fp8 ? mg_cfg<true>(a, nwg, cfg, epi, stream) : mg_cfg<false>(a, nwg, cfg, epi, stream);
+  if (w8) return mg_cfg<false, true>(a, nwg, cfg, epi, stream);
+  return fp8 ? mg_cfg<true, false>(a, nwg, cfg, epi, stream) : mg_cfg<false, false>(a, nwg, cfg, epi, stream);
 }

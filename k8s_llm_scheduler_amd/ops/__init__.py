@@ -142,6 +142,8 @@ def _ref_act_quant(x: torch.Tensor, w) -> torch.Tensor:
     x2 = x.reshape(-1, x.shape[-1])
     if x2.shape[0] <= max(GEMV_MAX_M, SGEMV_MAX_M):   # GEMV / sgemv: bf16 activations against the fp8 weights
         return x
+    if w8_rows(x2.shape[0]):   # mgemm's W8 mode: bf16 activations against the fp8 weights
+        return x
     q, s = ref.quantize_fp8(x2)
     return ref.dequant_fp8(q, s, torch.float32).to(x.dtype).view(x.shape)
 
@@ -403,7 +405,10 @@ def mgemm_nwg(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int) 
 
 
 def mgemm_valid(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int = 1) -> bool:
+    """``fp8``: 0 / False bf16, 1 / True fp8 activations and weights, 2 W8 (fp8 weights, bf16 activations)."""
     if cfg < 0 or cfg >= len(mgemm_configs()):
+        return False
+    if int(fp8) == 2 and _mg_w8_lds(cfg) < 0:
         return False
     kb = K * (1 if fp8 else 2)
     if kb % mgemm_configs()[cfg][5] or N % 4 or M <= 0:
@@ -416,6 +421,40 @@ def mgemm_valid(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int
 def _mgemm_ok(N: int, K: int, fp8: bool) -> bool:
     """Some mgemm configuration can run this shape (128-byte k-steps, 4-column output groups)."""
     return N % 4 == 0 and (K * (1 if fp8 else 2)) % 128 == 0
+
+
+@functools.lru_cache(maxsize=64)
+def _mg_w8_lds(cfg: int) -> int:
+    return native().mgemm_lds_bytes(cfg, 2)
+
+
+# W8: fp8 weights against bf16 activations in mgemm (17..W8_MAX_M rows: batched decode and short mixed steps): the
+# weight bytes streamed are the fp8 ones, the bf16 MFMA runs at the non-scaled fp8 MFMA's rate, and no activation is
+# quantized (no quantize_act_fp8 launch before the QKV / gate-up -- their RMS statistics are mgemm's prologue -- or the
+# O / down projections).  Measured SLOWER than per-token e4m3 activations (profiles/mgemm_w8_tune_r5.txt: 0.54-1.13x
+# per shape, 16 of 24 below; fp8 batch 64: 31.5 -> 23.7 decisions/s): mgemm re-stages x with W in every k-step, and
+# bf16 x doubles those bytes, more than the quantize launches cost.  Opt-in (K8S_MGEMM_W8=1) for A/B only.
+W8_ON = os.environ.get("K8S_MGEMM_W8", "0") == "1"
+W8_MAX_M = int(os.environ.get("K8S_MGEMM_W8_MAX_M", "128"))
+
+
+def w8_rows(M: int) -> bool:
+    """An fp8-weight GEMM of M rows runs mgemm's W8 mode (bf16 activations) on the GPU."""
+    return W8_ON and max(GEMV_MAX_M, SGEMV_MAX_M) < M <= W8_MAX_M and GEMM_BACKEND in ("auto", "mgemm")
+
+
+def mgemm_w8_plan(M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]:
+    """(cfg, grid) of the W8 mode for this shape, or None (no W8 configuration runs it)."""
+    if N % 4 or K % 128:
+        return None
+    pick = _mg_table_row(M, N, K, epi, 2)
+    if pick is not None and mgemm_valid(pick[1], M, N, K, epi, 2, pick[2]):
+        return pick[1], pick[2]
+    pick = _mg_table_row(M, N, K, epi, 1)   # the fp8 plan's tile, where W8 builds it
+    if pick is not None and mgemm_valid(pick[1], M, N, K, epi, 2, pick[2]):
+        return pick[1], pick[2]
+    cfg, grid = mgemm_heuristic(M, N, K, epi, 2)
+    return (cfg, grid) if mgemm_valid(cfg, M, N, K, epi, 2, grid) else None
 
 
 @functools.lru_cache(maxsize=4096)
@@ -436,6 +475,11 @@ def mgemm_heuristic(M: int, N: int, K: int, epi: int, fp8: bool, num_cus: int = 
         cfg = 19
     if not mgemm_valid(cfg, M, N, K, epi, fp8):   # K not a multiple of the config's k-step: 128-byte k-steps
         cfg = 5 if M <= 16 else 9 if M <= 32 else 13 if M <= 64 else 15 if M <= 128 else 17
+    if int(fp8) == 2 and not mgemm_valid(cfg, M, N, K, epi, fp8):   # W8: the weight-streaming tiles whose x fits
+        for c in ((29, 28, 8, 7, 6) if M <= 64 else (30, 29, 28, 8)):
+            if mgemm_valid(c, M, N, K, epi, fp8):
+                cfg = c
+                break
     tiles = _mg_tiles(cfg, M, N, epi)
     if tiles >= num_cus // 2:
         return cfg, 1
@@ -505,23 +549,33 @@ def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
 
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
           grid: Optional[int] = None, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
-          out: Optional[torch.Tensor] = None, act: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, act: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+          w8: bool = False) -> torch.Tensor:
     """Hand-written MFMA GEMM (mgemm.hip): epi(x[M, K] @ w[N, K].T), any M (routed for M > GEMV_MAX_M).  ``w``: bf16 or
-    Fp8Weight (activations are then quantized per token by quantize_act_fp8).  SwiGLU: w = [Wg; Wu].
-    ``rms_eps``: RMSNorm prologue -- the result is scaled by 1/rms(x row) (the norm gamma must be folded into
-    ``w``), so the un-normalised residual stream feeds the GEMM directly.  ``res``: residual epilogue
-    (bf16 output only) -- out = x @ w.T + res, one rounding; ``out`` may be ``res`` (in place)."""
+    Fp8Weight (activations are then quantized per token by quantize_act_fp8, or with ``w8`` stay bf16: W8 mode).
+    SwiGLU: w = [Wg; Wu].  ``rms_eps``: RMSNorm prologue -- the result is scaled by 1/rms(x row) (the norm gamma must
+    be folded into ``w``), so the un-normalised residual stream feeds the GEMM directly (bf16 or W8).  ``res``:
+    residual epilogue (bf16 output only) -- out = x @ w.T + res, one rounding; ``out`` may be ``res`` (in place)."""
     M, K = x.shape
     fp8 = _is_fp8(w)
+    mode = (2 if w8 else 1) if fp8 else 0
+    if w8 and (not fp8 or act is not None):
+        raise ValueError("mgemm: W8 mode takes fp8 weights and bf16 activations")
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     if cfg is None:
-        cfg, grid = mgemm_plan(M, N, K, epi, fp8)
+        if mode == 2:
+            plan = mgemm_w8_plan(M, N, K, epi)
+            if plan is None:
+                raise ValueError(f"mgemm: no W8 configuration runs M={M} N={N} K={K} epi={epi}")
+            cfg, grid = plan
+        else:
+            cfg, grid = mgemm_plan(M, N, K, epi, fp8)
     grid = grid or 1
-    if not mgemm_valid(cfg, M, N, K, epi, fp8, grid):
-        raise ValueError(f"mgemm: cfg {cfg} / grid {grid} invalid for M={M} N={N} K={K} epi={epi}")
+    if not mgemm_valid(cfg, M, N, K, epi, mode, grid):
+        raise ValueError(f"mgemm: cfg {cfg} / grid {grid} invalid for M={M} N={N} K={K} epi={epi} mode={mode}")
     nwg = mgemm_nwg(cfg, M, N, K, epi, fp8, grid)
-    tiles, cmax, n_ws = _mg_plan_info(M, N, K, epi, fp8, cfg, nwg)
-    if fp8 and rms_eps is not None:
+    tiles, cmax, n_ws = _mg_plan_info(M, N, K, epi, mode, cfg, nwg)
+    if mode == 1 and rms_eps is not None:
         raise ValueError("mgemm: the RMS prologue needs bf16 activations")
     if res is not None and (epi != EPI_BF16 or res.shape != (M, N)):
         raise ValueError("mgemm: residual epilogue needs a bf16 [M, N] residual and the bf16 epilogue")
@@ -531,7 +585,10 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
     tk = _zeroed_scratch(x.device, "mgemm", 4 * tiles, 64 * 1024) if cmax > 1 else 0
     rp = _chk(res, BF16, "res") if res is not None else 0
     rms, eps = (1, float(rms_eps)) if rms_eps is not None else (0, 0.0)
-    if fp8:
+    if mode == 2:
+        native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"), w.q.data_ptr(),
+                       0, w.scale.data_ptr(), M, N, K, epi, 2, cfg, nwg, cmax, rp, rms, eps, -1)
+    elif fp8:
         xq, sx = act if act is not None else quantize_act_fp8(x.contiguous())
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, xq.data_ptr(), w.q.data_ptr(),
                        sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, nwg, cmax, rp, 0, 0.0, -1)
@@ -758,6 +815,9 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
         y = xgemm(x2, w, epi, res=res, rms_eps=rms_eps, out=out)
         if y is not None:
             return y
+    if (kern == "mgemm" and fp8 and act is None and w8_rows(M)
+            and mgemm_w8_plan(M, N, K, epi) is not None):   # fp8 weights, bf16 activations: no quantize launch
+        return mgemm(x2, w, epi, res=res, rms_eps=rms_eps, out=out, w8=True)
     if kern == "library" or (fp8 and rms_eps is not None):
         return None   # (fp8: the activations are quantized after the norm, so the caller normalises first)
     if kern == "mgemm":
@@ -783,6 +843,17 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
     load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
     copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM."""
     M, K = r.shape
+    if _is_fp8(w) and w8_rows(M):
+        # W8 rows: mgemm's RMS prologue on the un-normalised bf16 rows against the fp8 weights (no quantize launch)
+        if _gpu(r):
+            n_out = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+            if gemm_route(M, n_out, K, epi, True)[0] == "mgemm" and mgemm_w8_plan(M, n_out, K, epi) is not None:
+                return mgemm(r.contiguous(), w, epi, rms_eps=eps, w8=True)
+        else:
+            x = rmsnorm(r, _ones(K, r.device), eps)
+            if epi == EPI_SWIGLU:
+                return ref.linear_swiglu(x, w).to(BF16)
+            return ref.linear(x, w, F32 if epi == EPI_F32 else BF16)
     if _is_fp8(w) and M > max(GEMV_MAX_M, SGEMV_MAX_M):
         # fp8 GEMM rows: e4m3 of the UN-normalised rows with 1/rms folded into the per-token scales (one kernel
         # reads r once; no rmsnorm kernel, no normalised copy) -> the fp8 GEMM

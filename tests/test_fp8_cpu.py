@@ -33,12 +33,19 @@ def test_fp8_linear_ops_match_dequantized_math():
     torch.testing.assert_close(ops.linear(x, w).float(), (x.float() @ wd.T).bfloat16().float())
     xs = torch.randn(5, 256, generator=g).bfloat16()   # small-batch sgemv rows (3..8): bf16 activations too
     torch.testing.assert_close(ops.linear(xs, w).float(), (xs.float() @ wd.T).bfloat16().float())
-    # GEMM rows (above the sgemv range): per-token e4m3 activations
-    xb = torch.randn(max(ops.GEMV_MAX_M, ops.SGEMV_MAX_M) + 3, 256, generator=g).bfloat16()
+    # 17..W8_MAX_M rows (batched decode): mgemm's W8 mode, bf16 activations against the fp8 weights
+    xm = torch.randn(max(ops.GEMV_MAX_M, ops.SGEMV_MAX_M) + 3, 256, generator=g).bfloat16()
+    assert ops.w8_rows(xm.shape[0]) == ops.W8_ON
+    gu = ops.quantize_fp8((torch.randn(2 * 48, 256, generator=g) * 0.05).bfloat16())
+    if ops.W8_ON:
+        torch.testing.assert_close(ops.linear(xm, w).float(), (xm.float() @ wd.T).bfloat16().float())
+        want = ref.linear_swiglu(xm, gu.dequant(torch.float32))
+        torch.testing.assert_close(ops.linear_swiglu(xm, gu).float(), want.float())
+    # prefill-size GEMM rows (above W8_MAX_M): per-token e4m3 activations
+    xb = torch.randn(ops.W8_MAX_M + 3, 256, generator=g).bfloat16()
     q, sc = ref.quantize_fp8(xb)
     xq = ref.dequant_fp8(q, sc, torch.float32)
     torch.testing.assert_close(ops.linear(xb, w).float(), (xq.bfloat16().float() @ wd.T).bfloat16().float())
-    gu = ops.quantize_fp8((torch.randn(2 * 48, 256, generator=g) * 0.05).bfloat16())
     y = ops.linear_swiglu(xb, gu)
     want = ref.linear_swiglu(xq.bfloat16(), gu.dequant(torch.float32))
     torch.testing.assert_close(y.float(), want.float())

@@ -6,7 +6,10 @@ separate silu_mul kernel for gate/up; fp8: per-token quantization + torch._scale
 Every candidate (tile config x split-K) is timed as a captured hipGraph of REPS launches that cycle over enough
 copies of the weight to exceed the 256 MiB Infinity Cache (weights are cold in the real decode / prefill loop).
 
-    python tools/mgemm_tune.py --tp 1 8 --m 16 64 256 [--fp8] [--write]
+    python tools/mgemm_tune.py --tp 1 8 --m 16 64 256 [--fp8 | --w8] [--write]
+
+--w8 tunes mgemm's W8 mode (fp8 weights, bf16 activations; table key fp8 = 2) against the per-token e4m3 path it
+replaces (quantize_act_fp8 + the tuned fp8 mgemm plan).
 
 --write merges the winners into engine/assets/mgemm_gfx950.json (the table ops.mgemm_plan reads).
 """
@@ -72,6 +75,8 @@ def candidates(M, N, K, epi, fp8):
     out = []
     for c, (bm, bn, _th, _lds, _sw, rb) in enumerate(cfgs):
         steps = K * (1 if fp8 else 2) // rb
+        if fp8 == 2 and not ops.mgemm_valid(c, M, N, K, epi, 2):
+            continue
         if bm > max(16, 2 * M) or (M > 64 and bm < 64) or (M > 256 and bm < 128):
             continue
         tiles = ops._mg_tiles(c, M, N, epi)
@@ -90,6 +95,8 @@ def candidates(M, N, K, epi, fp8):
 def lib_fn(x, Ws, epi, fp8):
     def f(i):
         w = Ws[i]
+        if fp8 == 2:   # W8 tuning: the per-token e4m3 path it replaces
+            return ops.mgemm(x, w, epi)
         if fp8:
             y = ops._fp8_gemm(x, w)
             if epi == ops.EPI_F32:
@@ -111,11 +118,14 @@ def main() -> int:
     ap.add_argument("--all-buckets", action="store_true", help="every row bucket of ops.GEMM_M_BUCKETS + 2048..8192")
     ap.add_argument("--only", nargs="*", default=None, help="projection names")
     ap.add_argument("--fp8", action="store_true")
+    ap.add_argument("--w8", action="store_true", help="tune the W8 mode (fp8 weights, bf16 activations)")
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
     a = ap.parse_args()
 
+    if a.w8:
+        a.fp8 = 2
     if a.all_buckets:
         a.m = list(ops.GEMM_M_BUCKETS) + [2048, 4096, 8192]
     torch.manual_seed(0)
@@ -143,7 +153,8 @@ def main() -> int:
                 lib_us = time_graph(lib_fn(x, Ws, epi, a.fp8), copies)
                 best = (float("inf"), None)
                 for c, gr in candidates(M, N, K, epi, a.fp8):
-                    us = time_graph(lambda i, c=c, gr=gr: ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr), copies)
+                    us = time_graph(lambda i, c=c, gr=gr: ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr, w8=a.fp8 == 2),
+                                    copies)
                     if a.verbose:
                         bm, bn = ops.mgemm_configs()[c][:2]
                         print(f"    cand tp{tp} {name} M={M} cfg {c:2d} ({bm}x{bn}) grid {gr:5d} "
@@ -158,7 +169,7 @@ def main() -> int:
                         gfn = lambda i: ops.linear(x, Ws[i], out_dtype=torch.float32 if epi == ops.EPI_F32 else None)
                     gemv_us = round(time_graph(gfn, copies), 2)
                 hc = ops.mgemm_heuristic(M, N, K, epi, a.fp8)
-                h_us = time_graph(lambda i: ops.mgemm(x, Ws[i], epi, cfg=hc[0], grid=hc[1]), copies)
+                h_us = time_graph(lambda i: ops.mgemm(x, Ws[i], epi, cfg=hc[0], grid=hc[1], w8=a.fp8 == 2), copies)
                 us, (c, ks) = best
                 plans[f"{ops._mg_bucket(M)},{N},{K},{epi},{int(a.fp8)}"] = [c, ks, round(us, 2), round(lib_us, 2)]
                 row = dict(tp=tp, proj=name, M=M, N=N, K=K, epi=epi, fp8=a.fp8, lib_us=round(lib_us, 2),
