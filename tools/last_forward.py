@@ -6,7 +6,9 @@ counts; this reads the per-dispatch trace (``*kernel_trace.csv``) instead and is
 
 * prefill: the contiguous run of dispatches that ends with the last prefill-attention / big-GEMM kernel, back to the
   decode GEMV that precedes it;
-* decode: the dispatches between the last two embedding kernels.
+* decode: the dispatches between the last two embedding kernels, plus a per-layer view: the kernels of one decoder
+  layer in launch order (the period between decode-attention launches), each averaged over the middle layers, so
+  projections that share a kernel template (O and down) are told apart.
 
     python tools/last_forward.py <kernel_trace.csv>
 """
@@ -63,7 +65,28 @@ def main() -> int:
     emb = [i for i, (n, _, _) in enumerate(rows) if "embedding_kernel" in n]
     if len(emb) >= 2:
         table(rows[emb[-2]:emb[-1]], "last decode step")
+        layer_view(rows[emb[-2]:emb[-1]])
     return 0
+
+
+def layer_view(rows) -> None:
+    att = [i for i, (n, _, _) in enumerate(rows)
+           if any(k in n for k in ("decode_fused", "decode_split", "decode_persist", "paged_decode"))]
+    if len(att) < 4:
+        return
+    per = att[1] - att[0]
+    if any(b - a != per for a, b in zip(att, att[1:])):
+        return
+    mid = att[1:-1]                 # layers with a full period on both sides
+    print(f"== per-layer view of the last decode step: {per} kernels per layer, mean over {len(mid)} layers "
+          f"(offsets from the attention launch)")
+    tot = 0.0
+    for off in range(-1, per - 1):
+        d = [(rows[i + off][2] - rows[i + off][1]) / 1e3 for i in mid if 0 <= i + off < len(rows)]
+        gap = [(rows[i + off][1] - rows[i + off - 1][2]) / 1e3 for i in mid if 1 <= i + off < len(rows)]
+        tot += sum(d) / len(d)
+        print(f"  {off:+d} {sum(d) / len(d):8.2f} us (gap before {sum(gap) / len(gap):5.2f})  {short(rows[mid[0] + off][0])}")
+    print(f"  layer kernel time {tot:.2f} us")
 
 
 if __name__ == "__main__":
