@@ -406,6 +406,8 @@ def test_bench_self_launch_rehearsal_prefill_on_captured_xgmi(world):
         pytest.skip("no GPU")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, PYTHONPATH=root, K8S_TP_BACKEND="gloo", K8S_TP_COMM="xgmi", OMP_NUM_THREADS="2")
+    if world == 2:   #  the 2-rank rehearsal runs the all-reduce autotune too
+        env["K8S_COMM_AUTOTUNE"] = "force"
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--preset", "tiny-tp8",
@@ -415,3 +417,14 @@ def test_bench_self_launch_rehearsal_prefill_on_captured_xgmi(world):
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["n_gpus"] == world and d["config"]["parallelism"] == f"tp{world}", d
     assert d["prefill_graph_replays"] >= 3 and d["rccl_calls_timed"] == 0, d
+    # the self-diagnosing start-up: stage timings of rank 0 and the slowest rank, the transport
+    # self-tests, the transport of every timed all-reduce, and (world 2) the autotune table
+    want = {"process_group", "xgmi_open", "xgmi_selftest", "fused_ar_selftest", "engine_build", "graph_capture",
+            "warmup"} | ({"comm_autotune"} if world == 2 else set())
+    assert want <= set(d["init_stages"]["rank0"]) and want <= set(d["init_stages"]["slowest"]), d["init_stages"]
+    assert d["tp_comm"]["xgmi"] == "self-test passed", d["tp_comm"]
+    assert d["tp_comm"]["fused_gemv_ar_selftest"] in ("passed", "failed"), d["tp_comm"]
+    assert any(k.startswith(("prefill:xgmi", "decode:xgmi", "decode:fused_gemv_ar")) for k in d["allreduce_transports"]), \
+        d["allreduce_transports"]
+    if world == 2:
+        assert d["tp_comm"].get("allreduce_us"), d["tp_comm"]
