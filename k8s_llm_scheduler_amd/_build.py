@@ -6,7 +6,11 @@ pybind11 bindings are host code, and only ``torch_stream.cpp`` sees PyTorch head
 the current PyTorch HIP stream).  Objects are cached under ``build/`` and rebuilt when a source
 or any header is newer.  Cross-compiles without a GPU.
 
-    python -m k8s_llm_scheduler_amd._build [-j N] [--force] [-v]
+    python -m k8s_llm_scheduler_amd._build [-j N] [--force] [-v] [--checked]
+
+``--checked`` builds the bounds-checked variant ``ops/_C_checked*.so`` (``-DK8S_CHECKED``, objects under
+``build/native_checked``; loaded instead of ``_C`` when ``K8S_CHECKED=1``): kernels range-check every index they
+derive from data and record violations for the host (csrc/kernels/common.h).
 """
 
 from __future__ import annotations
@@ -27,8 +31,8 @@ ARCH = os.environ.get("K8S_HIP_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
-def ext_path() -> Path:
-    return PKG / "ops" / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+def ext_path(checked: bool = False) -> Path:
+    return PKG / "ops" / (("_C_checked" if checked else "_C") + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
 def _torch_dirs():
@@ -57,13 +61,16 @@ def _run(cmd: List[str], verbose: bool) -> None:
         raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
-def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> Path:
+def build(jobs: int = 0, force: bool = False, verbose: bool = False, checked: bool = False) -> Path:
     import pybind11
 
     tinc, tlib, cxx11 = _torch_dirs()
-    BUILD.mkdir(parents=True, exist_ok=True)
+    bdir = BUILD.parent / "native_checked" if checked else BUILD
+    bdir.mkdir(parents=True, exist_ok=True)
     headers = _headers()
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", f"-D_GLIBCXX_USE_CXX11_ABI={int(cxx11)}"]
+    if checked:
+        common += ["-DK8S_CHECKED", "-DK8S_MODULE_NAME=_C_checked"]
     py_inc = sysconfig.get_paths()["include"]
     units = []
     for src in sorted((CSRC / "kernels").glob("*.hip")):
@@ -76,7 +83,7 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> Path:
     objs = []
     todo = []
     for src, flags in units:
-        obj = BUILD / (src.relative_to(CSRC).as_posix().replace("/", "__") + ".o")
+        obj = bdir / (src.relative_to(CSRC).as_posix().replace("/", "__") + ".o")
         objs.append(obj)
         if force or _stale(obj, src, headers):
             todo.append([HIPCC, *common, *flags, "-c", str(src), "-o", str(obj)])
@@ -84,7 +91,7 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> Path:
     with cf.ThreadPoolExecutor(max_workers=n) as ex:
         for f in [ex.submit(_run, c, verbose) for c in todo]:
             f.result()
-    out = ext_path()
+    out = ext_path(checked)
     if todo or force or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
         tmp = out.with_suffix(".tmp.so")
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs),
@@ -98,8 +105,9 @@ def main(argv=None) -> int:
     ap.add_argument("-j", "--jobs", type=int, default=0)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--checked", action="store_true", help="bounds-checked kernels: ops/_C_checked*.so")
     a = ap.parse_args(argv)
-    p = build(a.jobs, a.force, a.verbose)
+    p = build(a.jobs, a.force, a.verbose, a.checked)
     print(p)
     return 0
 

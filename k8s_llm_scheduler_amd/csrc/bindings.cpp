@@ -38,6 +38,13 @@ void k8s_gemv_plan(int M, int N_out, int K, int epi, int mode, int* ks_out, int*
 int k8s_sgemv(void* out, void* partial, const void* x, const void* W, const float* wscale, const void* res, int M,
               int N, int K, int epi, int norm, float eps, hipStream_t s);
 long long k8s_sgemv_workspace(int M, int N, int K, int epi, int fp8);
+// checked builds (common.h K8S_CHECKED): every instrumented unit's device record pointer; -1 in release builds
+int k8s_check_bind_misc(void* rec);
+int k8s_check_bind_rope_kv(void* rec);
+int k8s_check_bind_attn_decode_fused(void* rec);
+int k8s_check_bind_attn_decode_split(void* rec);
+int k8s_check_bind_attn_prefill(void* rec);
+int k8s_check_bind_attn_decode(void* rec);
 int k8s_gemv_set_loop(int wg_per_cu);
 int k8s_gemv_set_wide(int on);
 int k8s_pgemm_set_prio(int mode);
@@ -131,7 +138,23 @@ inline void check(int rc, const char* what) {
 
 }  // namespace
 
-PYBIND11_MODULE(_C, m) {
+#ifndef K8S_MODULE_NAME
+#define K8S_MODULE_NAME _C
+#endif
+PYBIND11_MODULE(K8S_MODULE_NAME, m) {
+#ifdef K8S_CHECKED
+  m.attr("checked") = true;
+#else
+  m.attr("checked") = false;
+#endif
+  // point every instrumented unit at one device record (ops.check_*); returns 0, or nonzero in release builds
+  m.def("check_bind", [](uintptr_t rec) {
+    int rc = 0;
+    for (auto f : {k8s_check_bind_misc, k8s_check_bind_rope_kv, k8s_check_bind_attn_decode_fused,
+                   k8s_check_bind_attn_decode_split, k8s_check_bind_attn_prefill, k8s_check_bind_attn_decode})
+      rc |= f(reinterpret_cast<void*>(rec));
+    return rc;
+  });
   m.doc() = "gfx950 HIP kernels and native runtime of k8s_llm_scheduler_amd";
   m.attr("ARCH") = "gfx950";
 

@@ -10,6 +10,8 @@
 // the tokens to attend to (the current token's K/V is already in the cache).
 #include "common.h"
 
+#define K8S_CHK_THIS_UNIT 6
+
 namespace k8sllm {
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -31,7 +33,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   __shared__ float tmp[16][G];
 
   const int b = blockIdx.z, kvh = blockIdx.y, p = blockIdx.x;
-  const int ctx = context_lens[b];
+  int ctx = context_lens[b];
+  K8S_CHECK_MAX(ctx, max_blocks * block_size, K8S_CHK_CTX);
   const int start = p * PART;
   if (start >= ctx) return;
   const int n = min(PART, ctx - start);
@@ -58,7 +61,9 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     for (int st = 0; st < QSTEPS; ++st) {
       const int i = wid * TOK_W + st * TPW + tok_in_wave;
       const int tt = start + min(i, n - 1);
-      const int slot = bt[tt / block_size] * block_size + tt % block_size;
+      int blk = bt[tt / block_size];
+      K8S_CHECK_RANGE(blk, 0, K8S_CHK_BLOCK, 0);
+      const int slot = blk * block_size + tt % block_size;
       kreg[st] = *reinterpret_cast<const u32x4*>(k_cache + ((size_t)slot * nkv + kvh) * D + sub * 8);
     }
 #pragma unroll
@@ -133,7 +138,9 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     for (int k = 0; k < TOK_W; ++k) {
       const int i = wid * TOK_W + k;
       const int tt = start + min(i, n - 1);
-      const int slot = bt[tt / block_size] * block_size + tt % block_size;
+      int blk = bt[tt / block_size];
+      K8S_CHECK_RANGE(blk, 0, K8S_CHK_BLOCK, 0);
+      const int slot = blk * block_size + tt % block_size;
       vreg[k] = *reinterpret_cast<const uint32_t*>(v_cache + ((size_t)slot * nkv + kvh) * D + d0);
     }
 #pragma unroll
@@ -195,6 +202,8 @@ __global__ void __launch_bounds__(D) paged_decode_reduce_kernel(bf16_t* __restri
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+K8S_CHECK_UNIT(attn_decode)
 
 // workspace: part_acc [B, nq, pmax, D] fp32 and part_ml [B, nq, pmax, 2] fp32 (unused if pmax == 1)
 extern "C" int k8s_paged_decode_attention(void* out, void* part_acc, void* part_ml, const void* q, const void* k_cache,

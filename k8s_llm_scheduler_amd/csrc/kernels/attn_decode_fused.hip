@@ -24,6 +24,8 @@
 // caches [num_slots, nkv, D] bf16; context_lens[b] INCLUDES the new token (pos = ctx - 1).
 #include "common.h"
 
+#define K8S_CHK_THIS_UNIT 3
+
 namespace k8sllm {
 
 constexpr float LOG2E_F = 1.4426950408889634f;
@@ -73,12 +75,15 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
     tblk[t] = (int)__builtin_amdgcn_raw_buffer_load_b32(rs_bt, min((start + wbase) / 16 + t, max_blocks - 1) * 4, 0, 0);
   static_assert(NTILE == 4, "four block ids per wave");
   asm volatile("" : "+v"(ctx_v), "+v"(tblk[0]), "+v"(tblk[1]), "+v"(tblk[2]), "+v"(tblk[3]));
-  const int ctx = __builtin_amdgcn_readfirstlane(ctx_v);
+  int ctx = __builtin_amdgcn_readfirstlane(ctx_v);
   if (ctx <= 0 || start >= ctx) return;
+  K8S_CHECK_MAX(ctx, max_blocks * 16, K8S_CHK_CTX);
   const int n = min(PART, ctx - start);
   const int wn = max(0, min(TW, n - wbase));  // live tokens of this wave (wave-uniform)
   bf16x8 kf[NTILE][D / 32];
   if (wn > 0) {
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) K8S_CHECK_RANGE(tblk[t], 0, K8S_CHK_BLOCK, 0);
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
       const bf16_t* kp = k_cache + (size_t)(tblk[t] * 16 + li) * kvs + (size_t)kvh * D + g4 * 8;
@@ -105,7 +110,9 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
   const int nq = nkv * G;
   const bf16_t* row = qkv + (size_t)b * (nq + 2 * nkv) * D;
   const float* cs = cos_sin + (size_t)pos * D;
-  const int pslot = bt[pos / 16] * 16 + pos % 16;
+  int pblk = bt[pos / 16];
+  K8S_CHECK_RANGE(pblk, 0, K8S_CHK_BLOCK, 0);
+  const int pslot = pblk * 16 + pos % 16;
 
   // ---- prologue: RoPE (two rotation pairs per item), zero padding heads, clear accumulators
   for (int i = tid; i < 16 * (HALF / 2) + 2 * (HALF / 2); i += NT) {
@@ -345,6 +352,8 @@ __global__ void __launch_bounds__(D) decode_merge_kernel(bf16_t* __restrict__ ou
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+K8S_CHECK_UNIT(attn_decode_fused)
 
 // part_acc [B, nq, pmax, D] f32 / part_ml [B, nq, pmax, 2] f32 (needed when pmax > 1).
 // part: context tokens per workgroup, 1024 (16 waves, ~137 KB of LDS: one workgroup per CU) or 512 (8 waves,

@@ -25,6 +25,8 @@
 // launch and restored to zero by every launch.
 #include "common.h"
 
+#define K8S_CHK_THIS_UNIT 4
+
 namespace k8sllm {
 
 namespace {
@@ -109,7 +111,7 @@ __device__ __forceinline__ void split_body(
   for (int t = 0; t < 4; ++t)
     tblk[t] = (int)__builtin_amdgcn_raw_buffer_load_b32(split_rsrc(bt), min(start / 16 + t, max_blocks - 1) * 4, 0, 0);
   asm volatile("" : "+v"(ctx_v), "+v"(tblk[0]), "+v"(tblk[1]), "+v"(tblk[2]), "+v"(tblk[3]));
-  const int ctx = __builtin_amdgcn_readfirstlane(ctx_v);
+  int ctx = __builtin_amdgcn_readfirstlane(ctx_v);
   const int nq = nkv * G;
   const bf16_t* row = qkv + (size_t)b * (nq + 2 * nkv) * D;
   bf16_t xa[G], xb[G];
@@ -124,6 +126,9 @@ __device__ __forceinline__ void split_body(
     if (SIGNAL && ctx <= 0 && c == 0) signal_done(done, lane);   // padded row: nothing to wait for
     return;
   }
+  K8S_CHECK_MAX(ctx, max_blocks * 16, K8S_CHK_CTX);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) K8S_CHECK_RANGE(tblk[t], 0, K8S_CHK_BLOCK, 0);
   TR(1);
 
   // ---- every K and V load of the chunk, issued before anything is consumed
@@ -160,7 +165,9 @@ __device__ __forceinline__ void split_body(
   {
     const int p = lane;
     const float cp = cs[p], sp = cs[HALF + p];
-    const int pslot = owner ? bt[pos / 16] * 16 + pos % 16 : 0;
+    int pblk = owner ? bt[pos / 16] : 0;
+    K8S_CHECK_RANGE(pblk, 0, K8S_CHK_BLOCK, 0);
+    const int pslot = pblk * 16 + pos % 16;
 #pragma unroll
     for (int h = 0; h < 16; ++h) {
       bf16_t lo = 0, hi = 0;
@@ -518,6 +525,8 @@ __global__ void __launch_bounds__(256) decode_split_oproj_kernel(
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+K8S_CHECK_UNIT(attn_decode_split)
 
 #ifdef K8S_ATTN_TRACE
 extern "C" int k8s_attn_trace_set(unsigned long long* p) {

@@ -29,6 +29,8 @@
 
 #include "common.h"
 
+#define K8S_CHK_THIS_UNIT 5
+
 namespace k8sllm {
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
@@ -51,7 +53,8 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_kernel(
   const int s = blockIdx.z, kvh = blockIdx.y, tile = blockIdx.x;
   const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
   if (tile * QT >= qlen) return;
-  const int ctx = context_lens[s];
+  int ctx = context_lens[s];
+  K8S_CHECK_MAX(ctx, max_blocks * block_size, K8S_CHK_CTX);
   const int qstart = ctx - qlen;  // absolute position of query 0
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -72,7 +75,10 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_kernel(
   int nbt[CPT];
   auto load_bt = [&](int t) {
 #pragma unroll
-    for (int c = 0; c < CPT; ++c) nbt[c] = bt[min(t * KT + (tid + NT * c) / (D / 8), ctx - 1) / block_size];
+    for (int c = 0; c < CPT; ++c) {
+      nbt[c] = bt[min(t * KT + (tid + NT * c) / (D / 8), ctx - 1) / block_size];
+      K8S_CHECK_RANGE(nbt[c], 0, K8S_CHK_BLOCK, 0);
+    }
   };
   auto fetch = [&](int t) {   // tile t's K/V with the ids in nbt, then tile t + 1's ids
 #pragma unroll
@@ -231,6 +237,8 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_kernel(
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+K8S_CHECK_UNIT(attn_prefill)
 
 extern "C" int k8s_paged_prefill_attention(void* out, const void* q, const void* k_cache, const void* v_cache,
                                            const int* cu_q, const int* context_lens, const int* block_tables,

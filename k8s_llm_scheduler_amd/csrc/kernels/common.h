@@ -63,6 +63,86 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
 // Uniform in (0, 1): 24 random bits, never 0.
 __device__ __forceinline__ float u01(uint32_t h) { return ((h >> 8) + 0.5f) * (1.0f / 16777216.0f); }
 
+// ---- checked builds (python -m k8s_llm_scheduler_amd._build --checked -> ops/_C_checked*.so, loaded with
+// K8S_CHECKED=1): every index a kernel derives from DATA (block tables, slot mappings, token ids, context lengths) is
+// range-checked before it addresses memory.  A violation is recorded in a device record the host reads after each
+// engine step (ops.check_read) and the index is clamped to a valid one, so the kernel finishes without touching
+// memory it does not own -- the bounds-assert debug build of SURVEY.md section 5 (race detection / sanitizers), with
+// no trap: a trapping kernel would take the device down for every process on it.  Release builds compile none of it.
+struct K8sCheck {
+  unsigned count;         // violations since the last reset
+  unsigned code, line;    // the first one: check code (K8S_CHK_*), source line
+  unsigned unit;          // translation unit (K8S_CHK_UNIT_*)
+  long long value;        // the offending value
+  long long kv_slots;     // bounds, set by the host: KV-cache slots (blocks x block size)
+  long long num_blocks;   // KV-cache blocks
+  long long vocab;        // embedding rows
+};
+enum { K8S_CHK_SLOT = 1, K8S_CHK_BLOCK = 2, K8S_CHK_CTX = 3, K8S_CHK_TOKEN = 4 };
+
 }  // namespace k8sllm
+
+#ifdef K8S_CHECKED
+// One record pointer per translation unit (kernels are built without relocatable device code); K8S_CHECK_UNIT
+// defines the unit's bind function, k8s_check_bind (bindings) points every unit at the same record.
+static __device__ k8sllm::K8sCheck* g_k8s_check;
+__device__ __noinline__ static void k8s_check_fail(unsigned unit, unsigned code, unsigned line, long long v) {
+  k8sllm::K8sCheck* c = g_k8s_check;
+  if (c == nullptr) return;
+  // the record is written with vector memory instructions only: the address is forced into VGPRs
+  unsigned long long a = reinterpret_cast<unsigned long long>(c);
+  asm volatile("" : "+v"(a));
+  k8sllm::K8sCheck* cv = reinterpret_cast<k8sllm::K8sCheck*>(a);
+  const unsigned old = __hip_atomic_fetch_add(&cv->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == 0) {
+    __hip_atomic_store(&cv->code, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cv->line, line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cv->unit, unit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cv->value, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__device__ __forceinline__ static long long k8s_bound(int code) {
+  const k8sllm::K8sCheck* c = g_k8s_check;
+  if (c == nullptr) return 0x7fffffffffffffffLL;
+  return code == k8sllm::K8S_CHK_SLOT ? c->kv_slots : code == k8sllm::K8S_CHK_BLOCK ? c->num_blocks : c->vocab;
+}
+// var must lie in [lo, bound(code)); otherwise record it and set var = fallback
+#define K8S_CHECK_RANGE(var, lo, code, fallback)                                          \
+  do {                                                                                    \
+    if ((long long)(var) < (long long)(lo) || (long long)(var) >= k8s_bound(code)) {      \
+      k8s_check_fail(K8S_CHK_THIS_UNIT, (code), __LINE__, (long long)(var));              \
+      (var) = (fallback);                                                                 \
+    }                                                                                     \
+  } while (0)
+// var must be <= maxv (a bound the kernel knows itself); otherwise record it and set var = maxv
+#define K8S_CHECK_MAX(var, maxv, code)                                                    \
+  do {                                                                                    \
+    if ((long long)(var) > (long long)(maxv)) {                                           \
+      k8s_check_fail(K8S_CHK_THIS_UNIT, (code), __LINE__, (long long)(var));              \
+      (var) = (maxv);                                                                     \
+    }                                                                                     \
+  } while (0)
+// a condition that must hold (no clamp: the caller handles the failure)
+#define K8S_CHECK_TRUE(cond, code, value)                                                 \
+  do {                                                                                    \
+    if (!(cond)) k8s_check_fail(K8S_CHK_THIS_UNIT, (code), __LINE__, (long long)(value)); \
+  } while (0)
+#define K8S_CHECK_UNIT(name)                                                              \
+  extern "C" int k8s_check_bind_##name(void* rec) {                                       \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_k8s_check), &rec, sizeof(rec));            \
+  }
+#else
+#define K8S_CHECK_RANGE(var, lo, code, fallback) \
+  do {                                           \
+  } while (0)
+#define K8S_CHECK_TRUE(cond, code, value) \
+  do {                                    \
+  } while (0)
+#define K8S_CHECK_MAX(var, maxv, code) \
+  do {                                 \
+  } while (0)
+#define K8S_CHECK_UNIT(name) \
+  extern "C" int k8s_check_bind_##name(void*) { return -1; }
+#endif
 
 #define K8S_CHECK_LAUNCH() (void)hipGetLastError()

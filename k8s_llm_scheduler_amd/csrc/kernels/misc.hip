@@ -2,6 +2,7 @@
 // and deterministic weight initialisation (hash-uniform, identical on any device / TP split).
 #include "common.h"
 
+#define K8S_CHK_THIS_UNIT 1
 namespace k8sllm {
 
 // out[t, :] = table[ids[t], :]   (rows of H bf16, H % 8 == 0)
@@ -9,6 +10,7 @@ __global__ void embedding_kernel(bf16_t* __restrict__ out, const int* __restrict
                                  const bf16_t* __restrict__ table, int H, int vocab) {
   const int t = blockIdx.x;
   int id = ids[t];
+  K8S_CHECK_RANGE(id, 0, K8S_CHK_TOKEN, 0);
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
   const u32x4* src = reinterpret_cast<const u32x4*>(table + (size_t)id * H);
   u32x4* dst = reinterpret_cast<u32x4*>(out + (size_t)t * H);
@@ -66,6 +68,8 @@ __global__ __launch_bounds__(256) void prefetch_kernel(const u32x4* __restrict__
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+K8S_CHECK_UNIT(misc)
 
 extern "C" int k8s_prefetch(const void* p, long long bytes, int blocks, void* sink, hipStream_t stream) {
   if (bytes < 16 || blocks < 1) return 0;

@@ -11,6 +11,8 @@
 // Rotation is "rotate-half" (HF Llama): x' = x*cos + rotate_half(x)*sin, pairs (i, i + D/2).
 #include "common.h"
 
+#define K8S_CHK_THIS_UNIT 2
+
 namespace k8sllm {
 
 __global__ void __launch_bounds__(256) rope_kv_kernel(
@@ -23,11 +25,15 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(
   if (positions != nullptr) {
     pos = positions[t];
     slot = slot_mapping[t];
+    if (slot >= 0) K8S_CHECK_RANGE(slot, 0, K8S_CHK_SLOT, -1);   // (checked builds: a bad slot is not written)
   } else {
-    const int ctx = context_lens[t];
+    int ctx = context_lens[t];
     if (ctx <= 0) return;  // padded batch row
+    K8S_CHECK_MAX(ctx, max_blocks * block_size, K8S_CHK_CTX);
     pos = ctx - 1;
-    slot = block_tables[(size_t)t * max_blocks + pos / block_size] * block_size + pos % block_size;
+    int blk = block_tables[(size_t)t * max_blocks + pos / block_size];
+    K8S_CHECK_RANGE(blk, 0, K8S_CHK_BLOCK, 0);
+    slot = blk * block_size + pos % block_size;
   }
   const int half = D >> 1;
   const int q4 = half >> 2;  // groups of 4 pairs per head
@@ -74,6 +80,8 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+K8S_CHECK_UNIT(rope_kv)
 
 extern "C" int k8s_rope_kv_write(void* q_out, void* k_cache, void* v_cache, const void* qkv, const float* cos_sin,
                                  const int* positions, const int* slot_mapping, const int* context_lens,

@@ -742,7 +742,7 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
                     self.fault = None
                     raise CollectiveError(f"injected collective failure on rank {self.control.rank}")
                 return out
-            except (CollectiveError, EngineStalled) as e:
+            except (CollectiveError, EngineStalled, ops.KernelCheckError) as e:
                 self._fail(str(e))
                 raise
 

@@ -89,6 +89,11 @@ class GraphCaptureMixin:
             for Tb in PREFILL_GRAPH_BUCKETS:
                 if Tb in self.prefill_graphs or not self._prefill_bucket_capturable(Tb):
                     continue
+                if Tb > self.max_blocks_per_seq * self.block_size:
+                    # no chunk of one sequence needs it, and its capture chunk (context Tb) would index past the
+                    # block table and the RoPE table (found by the bounds-checked build, K8S_CHECKED=1): such a
+                    # chunk runs eagerly
+                    continue
                 # a harmless chunk: Tb tokens of one sequence over block 0 whose K/V all go to the
                 # scratch block (block 0 is only read)
                 self._fill_prefill_state([0] * Tb, list(range(Tb)), [self.scratch_slot] * Tb, Tb, [0], Tb)

@@ -110,6 +110,7 @@ class RecoveryMixin:
         if self._trace_steps:
             self.recovery_trace.append((time.monotonic(), f"fetch {what}: waiting"))
         self._wait_device(what)
+        ops.check_raise(self.device)   # checked builds: a kernel's out-of-range index fails the step
         if self._pf_events:
             self._account_prefill()
         return outs

@@ -200,6 +200,8 @@ class LlamaModel:
         self.block_size = block_size
         self.kv_cache = torch.zeros(self.cfg.num_layers, 2, num_blocks * block_size, self.nkv, self.D,
                                     dtype=self.dtype, device=self.device)
+        if ops.CHECKED and self.device.type == "cuda":   # bounds of the checked kernels (K8S_CHECKED=1)
+            ops.check_enable(self.device, num_blocks * block_size, num_blocks, self.cfg.vocab)
         return self.kv_cache
 
     def kv_bytes_per_block(self, block_size: int) -> int:

@@ -12,7 +12,7 @@ import functools
 import importlib
 import math
 import os
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -20,8 +20,11 @@ from . import reference as ref
 
 _C = None
 _C_ERR: Optional[BaseException] = None
+# K8S_CHECKED=1 loads the bounds-checked build (python -m k8s_llm_scheduler_amd._build --checked): kernels range-check
+# every index they derive from data and record violations, which the engine raises after each step (check_raise)
+CHECKED = os.environ.get("K8S_CHECKED", "0") == "1"
 try:  # torch must be imported first: the extension binds to torch's HIP runtime
-    _C = importlib.import_module("k8s_llm_scheduler_amd.ops._C")
+    _C = importlib.import_module("k8s_llm_scheduler_amd.ops._C_checked" if CHECKED else "k8s_llm_scheduler_amd.ops._C")
 except Exception as e:  # pragma: no cover - reported loudly on first GPU use
     _C_ERR = e
 
@@ -52,6 +55,61 @@ def native():
 
 def available() -> bool:
     return _C is not None
+
+
+# ----------------------------------------------------------------------------- checked builds
+class KernelCheckError(RuntimeError):
+    """A checked kernel saw an index derived from data outside its bounds (csrc/kernels/common.h K8S_CHECKED)."""
+
+
+CHECK_CODES = {1: "KV slot", 2: "KV block id", 3: "context length beyond the block table", 4: "token id"}
+CHECK_UNITS = {1: "misc.hip (embedding)", 2: "rope_kv.hip", 3: "attn_decode_fused.hip", 4: "attn_decode_split.hip",
+               5: "attn_prefill.hip", 6: "attn_decode.hip"}
+_CHECK_REC: Dict[int, torch.Tensor] = {}
+
+
+def check_enable(device, kv_slots: int, num_blocks: int, vocab: int) -> bool:
+    """Checked builds: point every instrumented kernel unit at a fresh device record with these bounds (the model
+    calls this when it allocates its KV cache).  False in release builds."""
+    if _C is None or not getattr(_C, "checked", False):
+        return False
+    dev = torch.device(device)
+    rec = torch.zeros(6, dtype=torch.int64, device=dev)   # K8sCheck: count/code/line/unit, value, 3 bounds
+    rec[3], rec[4], rec[5] = int(kv_slots), int(num_blocks), int(vocab)
+    with torch.cuda.device(dev):
+        if _C.check_bind(rec.data_ptr()) != 0:
+            raise RuntimeError("check_bind failed: the checked extension could not bind its device record")
+    _CHECK_REC[dev.index if dev.index is not None else torch.cuda.current_device()] = rec
+    return True
+
+
+def check_read(device) -> Optional[dict]:
+    """The first recorded violation since the last read (and the count), or None; resets the record.  Waits for the
+    device work enqueued so far (call it after a step's results were fetched)."""
+    dev = torch.device(device)
+    rec = _CHECK_REC.get(dev.index if dev.index is not None else torch.cuda.current_device())
+    if rec is None:
+        return None
+    words = rec[:3].cpu()
+    head = words[:2].view(torch.int32)   # count, code, line, unit
+    count = int(head[0])
+    if count == 0:
+        return None
+    out = {"count": count, "code": int(head[1]), "line": int(head[2]), "unit": int(head[3]), "value": int(words[2]),
+           "what": CHECK_CODES.get(int(head[1]), "?"), "where": CHECK_UNITS.get(int(head[3]), "?")}
+    rec[:3].zero_()
+    return out
+
+
+def check_raise(device) -> None:
+    """Raise KernelCheckError if a checked kernel recorded a violation (no-op in release builds)."""
+    if not CHECKED:
+        return
+    v = check_read(device)
+    if v is not None:
+        raise KernelCheckError(f"{v['count']} bounds violation(s); first: {v['what']} = {v['value']} out of range in "
+                               f"{v['where']} line {v['line']} (the index was clamped, nothing was written out of "
+                               f"bounds)")
 
 
 class Fp8Weight:
