@@ -86,7 +86,7 @@ enum { K8S_CHK_SLOT = 1, K8S_CHK_BLOCK = 2, K8S_CHK_CTX = 3, K8S_CHK_TOKEN = 4 }
 // One record pointer per translation unit (kernels are built without relocatable device code); K8S_CHECK_UNIT
 // defines the unit's bind function, k8s_check_bind (bindings) points every unit at the same record.
 static __device__ k8sllm::K8sCheck* g_k8s_check;
-__device__ __noinline__ static void k8s_check_fail(unsigned unit, unsigned code, unsigned line, long long v) {
+__device__ __forceinline__ static void k8s_check_fail(unsigned unit, unsigned code, unsigned line, long long v) {
   k8sllm::K8sCheck* c = g_k8s_check;
   if (c == nullptr) return;
   // the record is written with vector memory instructions only: the address is forced into VGPRs
