@@ -54,6 +54,7 @@ int k8s_gemv_fp8(void* out, void* partial, const void* x, const void* W, const f
 int k8s_quantize_fp8_rows(void* q, float* scale, const void* w, int N, int K, hipStream_t s);
 int k8s_quantize_act_fp8(void* q, float* scale, const void* x, int T, int K, hipStream_t s);
 int k8s_quantize_act_fp8_rms(void* q, float* scale, const void* x, int T, int K, int rms, float eps, hipStream_t s);
+int k8s_quantize_act_mx(void* q, void* e8, const void* x, int T, int K, hipStream_t s);
 int k8s_dequant_fp8_rows(void* w, const void* q, const float* scale, int N, int K, hipStream_t s);
 int k8s_gemv(void* out, void* partial, const void* x, const void* W, int M, int N_out, int K, int epi, hipStream_t s);
 int k8s_gemv_rms(void* out, void* partial, const void* x, const void* W, const float* wscale, int M, int N_out, int K,
@@ -104,7 +105,7 @@ int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, int cfg, int 
                         long long* ws_elems);
 int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs, const float* wsc,
               int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax, const void* res, int rms,
-              float eps, hipStream_t s);
+              float eps, void* oq, void* oe, hipStream_t s);
 int k8s_pgemm4_num_configs();
 int k8s_pgemm4_config(int cfg, int* bp, int* bq, int* lds_bytes);
 int k8s_pgemm4_plan(int M, int N_out, int K, int epi, int cfg, int splits, int* nwg, long long* slab_elems);
@@ -218,6 +219,9 @@ PYBIND11_MODULE(K8S_MODULE_NAME, m) {
   });
   m.def("quantize_act_fp8", [](uintptr_t q, uintptr_t scale, uintptr_t x, int T, int K, int64_t s) {
     check(k8s_quantize_act_fp8(P(q), P<float>(scale), P(x), T, K, S(s)), "quantize_act_fp8");
+  });
+  m.def("quantize_act_mx", [](uintptr_t q, uintptr_t e8, uintptr_t x, int T, int K, int64_t s) {
+    check(k8s_quantize_act_mx(P(q), P(e8), P(x), T, K, S(s)), "quantize_act_mx");
   });
   m.def("quantize_act_fp8_rms", [](uintptr_t q, uintptr_t scale, uintptr_t x, int T, int K, int rms, float eps,
                                    int64_t s) {
@@ -362,11 +366,14 @@ PYBIND11_MODULE(K8S_MODULE_NAME, m) {
   });
   m.def("mgemm", [](uintptr_t out, uintptr_t ws, uintptr_t tickets, uintptr_t x, uintptr_t W, uintptr_t xs,
                     uintptr_t wsc, int M, int N, int K, int epi, int fp8, int cfg, int nwg, int cmax, uintptr_t res,
-                    int rms, float eps, int64_t s) {
+                    int rms, float eps, int64_t s, uintptr_t oq, uintptr_t oe) {
     check(k8s_mgemm(P(out), P<float>(ws), P<unsigned>(tickets), P(x), P(W), P<float>(xs), P<float>(wsc), M, N, K,
-                    epi, fp8, cfg, nwg, cmax, P(res), rms, eps, S(s)),
+                    epi, fp8, cfg, nwg, cmax, P(res), rms, eps, P(oq), P(oe), S(s)),
           "mgemm");
-  });
+  }, py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("x"), py::arg("W"), py::arg("xs"), py::arg("wsc"),
+     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("fp8"), py::arg("cfg"), py::arg("nwg"),
+     py::arg("cmax"), py::arg("res"), py::arg("rms"), py::arg("eps"), py::arg("s"), py::arg("oq") = 0,
+     py::arg("oe") = 0);
 
   m.def("pgemm4_configs", []() {
     py::list out;

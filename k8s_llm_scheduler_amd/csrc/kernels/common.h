@@ -40,6 +40,25 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+// OCP MX e4m3 (K16 block-scaled activations; fp8.hip has the format): one E8M0 byte per 32 values, the smallest
+// power of two >= max|block| / 448 (127 for an all-zero block, clamped to [1, 253]), and the exact reciprocal.
+__device__ __forceinline__ uint32_t mx_e8m0(float amax) {
+  const uint32_t b = __float_as_uint(amax * (1.f / 448.f));
+  uint32_t e = (b >> 23) + ((b & 0x7fffffu) != 0u);
+  if (amax == 0.f) e = 127u;
+  return min(max(e, 1u), 253u);
+}
+__device__ __forceinline__ float mx_inv_scale(uint32_t e) { return __uint_as_float((254u - e) << 23); }
+// 4 fp32 values x inv -> 4 e4m3 bytes (one dword), saturated, round-to-nearest-even
+__device__ __forceinline__ uint32_t mx_pack4(float a, float b, float c, float d, float inv) {
+  auto cl = [&](float t) { return fminf(fmaxf(t * inv, -448.f), 448.f); };
+  int p = __builtin_amdgcn_cvt_pk_fp8_f32(cl(a), cl(b), 0, false);
+  p = __builtin_amdgcn_cvt_pk_fp8_f32(cl(c), cl(d), p, true);
+  return (uint32_t)p;
+}
+// bf16 rounding of an fp32 value (MX producers quantize the bf16 value the bf16 path would have stored)
+__device__ __forceinline__ float bf_round(float f) { return bf2f(f2bf(f)); }
+
 // Block-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats of LDS.
 __device__ __forceinline__ float block_sum(float v, float* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;

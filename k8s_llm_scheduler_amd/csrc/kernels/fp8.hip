@@ -136,9 +136,57 @@ __global__ void __launch_bounds__(256) quantize_act_fp8_kernel(uint8_t* __restri
   }
 }
 
+// K16, block-scaled (OCP MX e4m3, "MXFP8"): every 32 consecutive values of a row share one E8M0 scale (a biased
+// power-of-two exponent byte), the smallest power of two >= max|block| / 448, so x / 2^(e - 127) is exact in fp32 and
+// fits e4m3 without saturating.  The scales feed the scale operand of v_mfma_scale_f32_16x16x128_f8f6f4 directly
+// (one byte per lane = one 32-value block of one row; mgemm / pgemm MX mode), and a block is local to any producer
+// tile that covers 32 features of a row -- the SwiGLU epilogues and the attention kernels emit this format
+// themselves (no per-row absmax pass).  This kernel is the stand-alone form (tests, and producers without a fused
+// form): one thread per block.
+__global__ void __launch_bounds__(256) quantize_act_mx_kernel(uint8_t* __restrict__ q, uint8_t* __restrict__ e8,
+                                                              const bf16_t* __restrict__ x, long long blocks) {
+  const long long b = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (b >= blocks) return;
+  const u32x4* src = reinterpret_cast<const u32x4*>(x + b * 32);
+  float v[32];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const u32x4 d = src[c];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[c * 8 + 2 * j] = lo_bf(d[j]);
+      v[c * 8 + 2 * j + 1] = hi_bf(d[j]);
+    }
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
+  const uint32_t e = mx_e8m0(amax);
+  const float inv = mx_inv_scale(e);
+  u32x4 o0, o1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o0[j] = mx_pack4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3], inv);
+    o1[j] = mx_pack4(v[16 + 4 * j], v[17 + 4 * j], v[18 + 4 * j], v[19 + 4 * j], inv);
+  }
+  reinterpret_cast<u32x4*>(q + b * 32)[0] = o0;
+  reinterpret_cast<u32x4*>(q + b * 32)[1] = o1;
+  e8[b] = (uint8_t)e;
+}
+
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+// x bf16 [T][K] -> q e4m3 [T][K] + e8 E8M0 [T][K / 32] (K % 32 == 0).
+extern "C" int k8s_quantize_act_mx(void* q, void* e8, const void* x, int T, int K, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (K <= 0 || K % 32 != 0) return -1;
+  const long long blocks = (long long)T * (K / 32);
+  quantize_act_mx_kernel<<<(unsigned)((blocks + 255) / 256), 256, 0, s>>>(
+      static_cast<uint8_t*>(q), static_cast<uint8_t*>(e8), static_cast<const bf16_t*>(x), blocks);
+  return (int)hipGetLastError();
+}
 
 // rms != 0: the row's 1/rms (eps) is folded into its scale (see quantize_act_fp8_kernel).
 extern "C" int k8s_quantize_act_fp8_rms(void* q, float* scale, const void* x, int T, int K, int rms, float eps,

@@ -30,6 +30,16 @@
 //    bf16 one, the same rate as the non-scaled fp8 MFMA.  The weight bytes streamed are the fp8 ones; the RMS
 //    prologue works as for bf16 (the un-normalised residual is the x operand), so the fp8 QKV / gate-up / O /
 //    down projections of a 17-128-row decode step launch no quantize kernel.
+//  * MX activations (host mode fp8 = 3): x is OCP MX e4m3 -- one E8M0 scale per 32 values of a row (fp8.hip), as
+//    the SwiGLU epilogue below and the attention kernels write it -- and the MFMA is the block-scaled
+//    v_mfma_scale_f32_16x16x128_f8f6f4: lane (li, g) holds k 16 g.. and 64 + 16 g.. of its row and passes the scale
+//    byte of block g as its B scale (the weights' per-row scale stays in the epilogue, unit A scales).  The
+//    scale bytes ride the x ring: one 4-byte LDS-DMA per (row, 128-value subtile) per k-step.  Twice the MFMA rate
+//    of the non-scaled fp8 form, and no per-token absmax pass anywhere.
+//  * MX output (SwiGLU epilogue, mx_out): the h = silu(g) * u values of 32 consecutive features of a row sit in
+//    the lanes of one 16-lane column group of two adjacent fragments (the configurations whose per-wave feature
+//    span is a multiple of 32): a 4-step shuffle max gives the block's E8M0 scale and every lane stores its e4m3
+//    bytes -- the down projection's input is produced already quantized.
 #include "common.h"
 
 namespace k8sllm {
@@ -38,6 +48,8 @@ namespace {
 enum { MG_BF16 = 0, MG_F32 = 1, MG_SWIGLU = 2 };
 
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
 
 __device__ __forceinline__ float mg_silu(float g) { return g / (1.f + __expf(-g)); }
 
@@ -73,6 +85,9 @@ struct MgArgs {
   const uint8_t* W;      // [rows][K] bf16 or e4m3
   const float* xs;       // fp8 activations: [M] per-token activation scales
   const float* wsc;      // fp8: [rows] per-row weight scales
+  const uint8_t* xe;     // MX activations: [M][K / 32] E8M0 block scales
+  uint8_t* oq;           // MX output (SwiGLU): e4m3 [M][N_out] ...
+  uint8_t* oe;           // ... and its E8M0 block scales [M][N_out / 32] (bf16 out not written)
   long long kbytes;      // bytes per row of W (and of x, except W8: x rows are bf16, xkbytes)
   long long xkbytes;     // bytes per row of x
   long long total;       // tiles * T work items (one item = one tile x one 128-byte k-step)
@@ -94,7 +109,8 @@ __device__ __forceinline__ int mg_swz_rb(int r) {
   return RB == 64 ? ((r >> 2) & 3) : RB == 128 ? ((r >> 1) & 7) : (r & 15);
 }
 
-template <int BM, int BN, int WM, int WN, int WK, int RB, int S, int EPI, bool FP8, bool W8 = false>
+template <int BM, int BN, int WM, int WN, int WK, int RB, int S, int EPI, bool FP8, bool W8 = false, bool MX = false,
+          bool MXO = false>
 __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   constexpr int NW = WM * WN * WK;
   constexpr int FM = BM / (WM * 16), FN = BN / (WN * 16);
@@ -104,14 +120,21 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert(WN == 1 || WN == 2 || WN == 4, "the RMS prologue splits a fragment's 4 dot2 over WN waves");
   static_assert(RB == 64 || RB == 128 || RB == 256 || RB == 512, "row bytes per k-step");
   static_assert(!(FP8 && W8), "W8: fp8 weights with bf16 activations");
+  static_assert(!MX || FP8, "MX: e4m3 activations with E8M0 block scales");
+  static_assert(!MXO || (EPI == MG_SWIGLU && (FN / 2) % 2 == 0), "MX output: SwiGLU, 32-feature spans per wave");
   constexpr int XRB = W8 ? 2 * RB : RB;              // x row bytes per k-step (W8: RB bf16 values)
   constexpr int CPR = RB / 16, XCPR = XRB / 16;      // 16-byte chunks per staged W / x row
   constexpr int KS = (FP8 || W8) ? RB / 32 : RB / 64;   // k32 MFMA steps per k-step (RB = 64: one)
   static_assert(KS % WK == 0, "k32 steps split evenly over WK waves");
-  constexpr int WREG = BN * RB, STAGE_B = BN * RB + BM * XRB;
+  constexpr int KS4 = RB / 128;                      // MX: 128-value subtiles per k-step, one scaled MFMA each
+  static_assert(!MX || (KS4 >= 1 && KS4 % WK == 0), "MX: subtiles split evenly over WK waves");
+  constexpr int SD = MX ? BM * KS4 : 0;              // MX: scale dwords per stage (row r, subtile d: r * KS4 + d)
+  static_assert(SD % NW == 0, "scale dwords per wave");
+  constexpr int WREG = BN * RB, XREG = BM * XRB, STAGE_B = BN * RB + BM * XRB + SD * 4;
   static_assert((BN * CPR) % NW == 0 && (BM * XCPR) % NW == 0, "chunks per wave");
   constexpr int WCH = BN * CPR / NW, XCH = BM * XCPR / NW;  // 16-byte chunks per wave per stage
-  constexpr int WI = (WCH + 63) / 64, XI = (XCH + 63) / 64, LPS = WI + XI;
+  constexpr int SCH = SD / NW;                              // MX: scale dwords per wave per stage
+  constexpr int WI = (WCH + 63) / 64, XI = (XCH + 63) / 64, SI = (SCH + 63) / 64, LPS = WI + XI + SI;
   static_assert((S - 2) * LPS <= 63, "vmcnt range");
   static_assert(WK == 1 || (WK - 1) * FN * FM * 64 * 16 * WM * WN <= S * STAGE_B, "LDS reduction space");
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the launch stub (its lambdas use device builtins)
@@ -158,7 +181,8 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     // lane-linear LDS destination); the host checks that every operand spans < 4 GiB
     const uint8_t* wseg = a.W + (long long)kb * RB;
     const uint8_t* xseg = a.x + (long long)kb * XRB;
-    uint32_t woff[WI], xoff[XI];
+    const uint8_t* eseg = MX ? a.xe + (long long)kb * (RB / 32) : nullptr;
+    uint32_t woff[WI], xoff[XI], soff[SI > 0 ? SI : 1];
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
       const int p = wid * WCH + min(i * 64 + lane, WCH - 1);
@@ -178,6 +202,12 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
       const int r = p / XCPR, c = (p % XCPR) ^ mg_swz_rb<XRB>(p / XCPR);
       xoff[i] = (uint32_t)min(mt * BM + r, a.M - 1) * (uint32_t)a.xkbytes + (uint32_t)(c * 16);
     }
+#pragma unroll
+    for (int i = 0; i < SI; ++i) {   // MX: the 4 scale bytes of (row r, subtile d) of a k-step
+      const int p = wid * SCH + min(i * 64 + lane, SCH - 1);
+      const int r = p / KS4, d = p % KS4;
+      soff[i] = (uint32_t)min(mt * BM + r, a.M - 1) * (uint32_t)(a.xkbytes >> 5) + (uint32_t)(d * 4);
+    }
 
     auto issue = [&](int t, int stage) {
       char* sb = lds + stage * STAGE_B;
@@ -196,6 +226,16 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
           __builtin_amdgcn_global_load_lds(
               xb + xoff[i], (__attribute__((address_space(3))) void*)(sb + WREG + (wid * XCH + i * 64) * 16), 16, 0,
               0);
+      }
+      if constexpr (MX) {
+        const uint8_t* eb = eseg + (long long)t * (RB / 32);
+#pragma unroll
+        for (int i = 0; i < SI; ++i) {
+          if (SCH % 64 == 0 || i * 64 + lane < SCH)
+            __builtin_amdgcn_global_load_lds(
+                eb + soff[i], (__attribute__((address_space(3))) void*)(sb + WREG + XREG + (wid * SCH + i * 64) * 4),
+                4, 0, 0);
+        }
       }
     };
 
@@ -258,6 +298,36 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
                   ss[j] = __builtin_amdgcn_fdot2_f32_bf16(v2, v2, ss[j], false);
                 }
               }
+          }
+        } else if constexpr (MX) {
+          if (q < KS4 / WK) {
+            // operand layout of the 16x16x128 f8f6f4 MFMA (measured, tools/experiments/mx_scale_probe.hip): lane
+            // (li, g) holds k = 16 g .. +16 in bytes 0-15 and k = 64 + 16 g .. +16 in bytes 16-31, and the scale of
+            // 32-value block b of row li is lane li + 16 b's -- so chunks 8 kk4 + g and 8 kk4 + 4 + g in natural k
+            // order, and lane g passes the scale byte of block g
+            const int kk4 = q * WK + wk, c0 = kk4 * 8 + g;
+            const int* sl = reinterpret_cast<const int*>(xb + XREG);
+            i32x8 af[FN], bx[FM];
+            int sc[FM];
+            auto frag32 = [&](const char* rowp, int row) {
+              const i32x4 lo4 = *reinterpret_cast<const i32x4*>(rowp + ((c0 ^ mg_swz_rb<RB>(row)) << 4));
+              const i32x4 hi4 = *reinterpret_cast<const i32x4*>(rowp + (((c0 + 4) ^ mg_swz_rb<RB>(row)) << 4));
+              return i32x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+            };
+#pragma unroll
+            for (int f = 0; f < FN; ++f) af[f] = frag32(wb + arow[f] * RB, arow[f]);
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+              const int r = brow0 + j * 16;
+              bx[j] = frag32(xb + r * RB, r);
+              sc[j] = sl[r * KS4 + kk4] >> (8 * g);   // this lane's block scale in byte 0 (op_sel 0)
+            }
+#pragma unroll
+            for (int f = 0; f < FN; ++f)
+#pragma unroll
+              for (int j = 0; j < FM; ++j)
+                acc[f][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[f], bx[j], acc[f][j], 0, 0, 0,
+                                                                             0x7f7f7f7f, 0, sc[j]);
           }
         } else {
           const int c = kk * 2 + (g >> 1), hb = (g & 1) * 8;
@@ -408,9 +478,36 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     for (int j = 0; j < FM; ++j) {
       const int m = mt * BM + wm * (BM / WM) + j * 16 + li;
       if (m >= a.M) continue;
-      float sx = FP8 ? a.xs[m] : 1.f;
+      float sx = (FP8 && !MX) ? a.xs[m] : 1.f;
       if (do_rms) sx = rsqrtf(rss[wm * (BM / WM) + j * 16 + li] / (float)(a.xkbytes >> 1) + a.eps);
-      if constexpr (EPI == MG_SWIGLU) {
+      if constexpr (MXO) {   // 32-feature blocks = fragment pairs (2 b, 2 b + 1); the block's lanes share li
+#pragma unroll
+        for (int b = 0; b < FN / 4; ++b) {
+          const int nb = nt * (BN / 2) + wn * (BN / 2 / WN) + b * 32;   // first feature of the block
+          if (nb >= a.N_out) continue;                                   // N_out % 32 == 0: whole blocks only
+          float v[8];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int f = 2 * b + h, n0 = nb + h * 16 + 4 * g;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              float gt = acc[f][j][i] * sx * a.wsc[n0 + i], up = acc[f + FN / 2][j][i] * sx * a.wsc[a.half_rows + n0 + i];
+              v[4 * h + i] = bf_round(mg_silu(gt) * up);
+            }
+          }
+          float amax = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+          amax = fmaxf(amax, __shfl_xor(amax, 16, WAVE));
+          amax = fmaxf(amax, __shfl_xor(amax, 32, WAVE));
+          const uint32_t e = mx_e8m0(amax);
+          const float inv = mx_inv_scale(e);
+          uint8_t* orow = a.oq + (long long)m * a.N_out;
+          *reinterpret_cast<uint32_t*>(orow + nb + 4 * g) = mx_pack4(v[0], v[1], v[2], v[3], inv);
+          *reinterpret_cast<uint32_t*>(orow + nb + 16 + 4 * g) = mx_pack4(v[4], v[5], v[6], v[7], inv);
+          if (g == 0) a.oe[(long long)m * (a.N_out >> 5) + (nb >> 5)] = (uint8_t)e;
+        }
+      } else if constexpr (EPI == MG_SWIGLU) {
 #pragma unroll
         for (int f = 0; f < FN / 2; ++f) {
           const int n0 = nt * (BN / 2) + wn * (BN / 2 / WN) + f * 16 + 4 * g;
@@ -501,45 +598,64 @@ constexpr MgCfg kMgCfgs[] = {
     {64, 64, 2, 2, 1, 128, 4},    // 29
     {64, 128, 1, 4, 1, 128, 4},   // 30
     {64, 64, 2, 2, 2, 128, 4},    // 31  8 waves, k-shared
+    // --- weight-streaming tiles whose waves span whole 32-feature SwiGLU blocks (the MX-output epilogue)
+    {64, 64, 2, 1, 2, 256, 4},    // 32
+    {32, 64, 1, 1, 4, 512, 3},    // 33
+    {64, 128, 2, 2, 1, 128, 6},   // 34
+    {16, 64, 1, 1, 4, 512, 3},    // 35
+    {128, 64, 2, 1, 2, 256, 3},   // 36
 };
 constexpr int kMgNumCfgs = sizeof(kMgCfgs) / sizeof(kMgCfgs[0]);
 
-// LDS bytes of config c in mode (0 bf16, 1 fp8 x and W, 2 W8: fp8 W, bf16 x)
+// LDS bytes of config c in mode (0 bf16, 1 fp8 x and W, 2 W8: fp8 W, bf16 x, 3 MX: fp8 W, MX x)
 constexpr int mg_lds_bytes(const MgCfg c, int mode) {
-  return c.s * (c.bn * c.rb + c.bm * c.rb * (mode == 2 ? 2 : 1)) + 16 + c.wk * c.wn * c.bm * 4;
+  return c.s * (c.bn * c.rb + c.bm * c.rb * (mode == 2 ? 2 : 1) + (mode == 3 ? c.bm * (c.rb / 32) : 0)) + 16 +
+         c.wk * c.wn * c.bm * 4;
 }
 // W8 is built for the weight-streaming configurations (batched decode) only
-constexpr bool mg_w8_cfg(int c) { return c <= 14 || c >= 28; }
+constexpr bool mg_w8_cfg(int c) { return c <= 14 || (c >= 28 && c <= 31); }
+// MX activations: 128-value subtiles split evenly over the k-sharing waves, scale dwords evenly over all waves
+constexpr bool mg_mx_cfg(int c) {
+  return kMgCfgs[c].rb >= 128 && (kMgCfgs[c].rb / 128) % kMgCfgs[c].wk == 0 &&
+         (kMgCfgs[c].bm * (kMgCfgs[c].rb / 128)) % (kMgCfgs[c].wm * kMgCfgs[c].wn * kMgCfgs[c].wk) == 0 &&
+         mg_lds_bytes(kMgCfgs[c], 3) <= 160 * 1024;
+}
+// SwiGLU with MX output: every wave's feature span is whole 32-feature blocks
+constexpr bool mg_mxo_cfg(int c) { return (kMgCfgs[c].bn / (kMgCfgs[c].wn * 16)) % 4 == 0; }
 
-template <int C, int EPI, bool FP8, bool W8>
+template <int C, int EPI, bool FP8, bool W8, bool MX, bool MXO>
 int mg_launch(const MgArgs& a, int grid, hipStream_t s) {
   constexpr bool ok = (EPI != MG_SWIGLU || (kMgCfgs[C].bn / (kMgCfgs[C].wn * 16)) % 2 == 0) &&
-                      (!W8 || (mg_w8_cfg(C) && mg_lds_bytes(kMgCfgs[C], 2) <= 160 * 1024));
+                      (!W8 || (mg_w8_cfg(C) && mg_lds_bytes(kMgCfgs[C], 2) <= 160 * 1024)) &&
+                      (!MX || mg_mx_cfg(C)) && (!MXO || (EPI == MG_SWIGLU && mg_mxo_cfg(C)));
   if constexpr (!ok) {
     return -2;
   } else {
     hipLaunchKernelGGL((mgemm_kernel<kMgCfgs[C].bm, kMgCfgs[C].bn, kMgCfgs[C].wm, kMgCfgs[C].wn, kMgCfgs[C].wk,
-                                      kMgCfgs[C].rb, kMgCfgs[C].s, EPI, FP8, W8>),
+                                      kMgCfgs[C].rb, kMgCfgs[C].s, EPI, FP8, W8, MX, MXO>),
                        dim3(grid), dim3(64 * kMgCfgs[C].wm * kMgCfgs[C].wn * kMgCfgs[C].wk), 0, s, a);
     return (int)hipGetLastError();
   }
 }
 
-template <int C, bool FP8, bool W8>
-int mg_epi(const MgArgs& a, int grid, int epi, hipStream_t s) {
+template <int C, bool FP8, bool W8, bool MX>
+int mg_epi(const MgArgs& a, int grid, int epi, bool mxo, hipStream_t s) {
+  if constexpr (FP8) {   // MX output: the SwiGLU epilogue of the fp8 and MX modes
+    if (mxo) return epi == MG_SWIGLU ? mg_launch<C, MG_SWIGLU, FP8, W8, MX, true>(a, grid, s) : -2;
+  }
   switch (epi) {
-    case MG_BF16: return mg_launch<C, MG_BF16, FP8, W8>(a, grid, s);
-    case MG_F32: return mg_launch<C, MG_F32, FP8, W8>(a, grid, s);
-    case MG_SWIGLU: return mg_launch<C, MG_SWIGLU, FP8, W8>(a, grid, s);
+    case MG_BF16: return mg_launch<C, MG_BF16, FP8, W8, MX, false>(a, grid, s);
+    case MG_F32: return mg_launch<C, MG_F32, FP8, W8, MX, false>(a, grid, s);
+    case MG_SWIGLU: return mg_launch<C, MG_SWIGLU, FP8, W8, MX, false>(a, grid, s);
   }
   return -2;
 }
 
-template <bool FP8, bool W8, int C = 0>
-int mg_cfg(const MgArgs& a, int grid, int cfg, int epi, hipStream_t s) {
+template <bool FP8, bool W8, bool MX, int C = 0>
+int mg_cfg(const MgArgs& a, int grid, int cfg, int epi, bool mxo, hipStream_t s) {
   if constexpr (C < kMgNumCfgs) {
-    if (cfg == C) return mg_epi<C, FP8, W8>(a, grid, epi, s);
-    return mg_cfg<FP8, W8, C + 1>(a, grid, cfg, epi, s);
+    if (cfg == C) return mg_epi<C, FP8, W8, MX>(a, grid, epi, mxo, s);
+    return mg_cfg<FP8, W8, MX, C + 1>(a, grid, cfg, epi, mxo, s);
   } else {
     return -4;
   }
@@ -549,11 +665,28 @@ int mg_cfg(const MgArgs& a, int grid, int cfg, int epi, hipStream_t s) {
 
 extern "C" int k8s_mgemm_num_configs() { return kMgNumCfgs; }
 
-// LDS bytes of a config in a mode (0 bf16, 1 fp8, 2 W8); -1: the config is not built for that mode.
+namespace {
+constexpr bool mg_mx_ok(int c) { return c < kMgNumCfgs && mg_mx_cfg(c); }
+template <int C = 0>
+bool mg_mx_valid(int cfg) {
+  if constexpr (C < kMgNumCfgs) return cfg == C ? mg_mx_ok(C) : mg_mx_valid<C + 1>(cfg);
+  else return false;
+}
+template <int C = 0>
+bool mg_mxo_valid(int cfg) {
+  if constexpr (C < kMgNumCfgs) return cfg == C ? mg_mxo_cfg(C) : mg_mxo_valid<C + 1>(cfg);
+  else return false;
+}
+}  // namespace
+
+// LDS bytes of a config in a mode (0 bf16, 1 fp8, 2 W8, 3 MX activations); -1: the config is not built for that
+// mode.  Mode 4: 0 if the config's SwiGLU epilogue can write MX output, else -1.
 extern "C" int k8s_mgemm_lds_bytes(int cfg, int mode) {
-  if (cfg < 0 || cfg >= kMgNumCfgs || mode < 0 || mode > 2) return -1;
+  if (cfg < 0 || cfg >= kMgNumCfgs || mode < 0 || mode > 4) return -1;
+  if (mode == 4) return mg_mxo_valid(cfg) ? 0 : -1;
   const int b = mg_lds_bytes(kMgCfgs[cfg], mode);
   if (mode == 2 && (!mg_w8_cfg(cfg) || b > 160 * 1024)) return -1;
+  if (mode == 3 && !mg_mx_valid(cfg)) return -1;
   return b;
 }
 
@@ -605,16 +738,21 @@ extern "C" int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, in
 
 // out[M, N_out] = epi(x[M, K] . W^T) with `nwg` workgroups streaming equal shares of the
 // (tile, k-step) items.  fp8 = 1: x / W are e4m3 bytes with per-row scales xs / wsc; fp8 = 2 (W8): W is e4m3
-// with row scales wsc, x is bf16 (no activation scales; the RMS prologue is allowed).
+// with row scales wsc, x is bf16 (no activation scales; the RMS prologue is allowed); fp8 = 3 (MX): W e4m3 with row
+// scales wsc, x MX e4m3 with its E8M0 block scales [M][K / 32] in xs (bytes).  oq / oe (fp8 = 1 or 3, SwiGLU): the
+// output is written as MX e4m3 [M][N_out] + E8M0 [M][N_out / 32] instead of bf16 (out unused).
 // SwiGLU: W holds 2 * N_out rows ([gate; up]); out has N_out columns.
 extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs,
                          const float* wsc, int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax,
-                         const void* res, int rms, float eps, hipStream_t stream) {
+                         const void* res, int rms, float eps, void* oq, void* oe, hipStream_t stream) {
   if (cfg < 0 || cfg >= kMgNumCfgs || M <= 0 || N_out <= 0 || K <= 0 || nwg <= 0 || cmax < 1) return -1;
   if (N_out % 4 != 0) return -1;
-  if (fp8 < 0 || fp8 > 2) return -1;
-  const bool w8 = fp8 == 2;
-  const long long kbytes = (long long)K * (fp8 ? 1 : 2), xkbytes = (long long)K * (fp8 == 1 ? 1 : 2);
+  if (fp8 < 0 || fp8 > 3) return -1;
+  const bool w8 = fp8 == 2, mx = fp8 == 3, mxo = oq != nullptr;
+  if (mxo && (oe == nullptr || epi != MG_SWIGLU || (fp8 != 1 && fp8 != 3) || N_out % 32 != 0 || !mg_mxo_valid(cfg)))
+    return -7;
+  if (mx && (K % 128 != 0 || !mg_mx_valid(cfg))) return -7;
+  const long long kbytes = (long long)K * (fp8 ? 1 : 2), xkbytes = (long long)K * ((fp8 == 1 || fp8 == 3) ? 1 : 2);
   if (kbytes % kMgCfgs[cfg].rb != 0) return -1;
   if (w8 && k8s_mgemm_lds_bytes(cfg, 2) < 0) return -4;
   const MgGeom g = mg_geom(M, N_out, K, epi, fp8, cfg);
@@ -622,10 +760,10 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   if (cmax > 1 && (ws == nullptr || tickets == nullptr)) return -3;
   const long long wrows = epi == MG_SWIGLU ? 2LL * N_out : (long long)N_out;
   if (wrows * kbytes >= (1LL << 32) || (long long)M * xkbytes >= (1LL << 32)) return -5;  // 32-bit DMA offsets
-  if (fp8 == 1 && (xs == nullptr || wsc == nullptr)) return -3;
+  if ((fp8 == 1 || fp8 == 3) && (xs == nullptr || wsc == nullptr)) return -3;
   if (w8 && wsc == nullptr) return -3;
   if (res != nullptr && epi != MG_BF16) return -6;   // residual epilogue: bf16 output only
-  if (rms && fp8 == 1) return -6;                    // fp8 activations are quantized before the GEMM
+  if (rms && (fp8 == 1 || fp8 == 3)) return -6;      // fp8 activations are quantized before the GEMM
   MgArgs a;
   a.res = static_cast<const bf16_t*>(res);
   a.rms = rms;
@@ -637,6 +775,9 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.W = static_cast<const uint8_t*>(W);
   a.xs = xs;
   a.wsc = wsc;
+  a.xe = mx ? reinterpret_cast<const uint8_t*>(xs) : nullptr;
+  a.oq = static_cast<uint8_t*>(oq);
+  a.oe = static_cast<uint8_t*>(oe);
   a.kbytes = kbytes;
   a.xkbytes = xkbytes;
   a.total = g.total;
@@ -647,6 +788,8 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.T = (int)g.T;
   a.nwg = nwg;
   a.cmax = cmax;
-  if (w8) return mg_cfg<false, true>(a, nwg, cfg, epi, stream);
-  return fp8 ? mg_cfg<true, false>(a, nwg, cfg, epi, stream) : mg_cfg<false, false>(a, nwg, cfg, epi, stream);
+  if (w8) return mg_cfg<false, true, false>(a, nwg, cfg, epi, false, stream);
+  if (mx) return mg_cfg<true, false, true>(a, nwg, cfg, epi, mxo, stream);
+  return fp8 ? mg_cfg<true, false, false>(a, nwg, cfg, epi, mxo, stream)
+             : mg_cfg<false, false, false>(a, nwg, cfg, epi, false, stream);
 }

@@ -183,6 +183,53 @@ def quantize_act_fp8(x: torch.Tensor, rms_eps: Optional[float] = None) -> Tuple[
     return q, s
 
 
+class MxAct:
+    """OCP MX e4m3 activations (K16 block-scaled; fp8.hip): ``q`` [M, K] uint8 e4m3 bit patterns, ``e`` [M, K / 32]
+    uint8 E8M0 exponents, x[m, k] ~= e4m3(q[m, k]) * 2^(e[m, k // 32] - 127).  The O and down projections of the fp8
+    GEMM rows take their input in this form: the SwiGLU epilogue (mgemm / pgemm ``mx_out``) and the attention
+    output write it, and the GEMMs feed the E8M0 bytes to the block-scaled MFMA's scale operand (mgemm / pgemm MX
+    mode) -- no per-token absmax pass, no quantize launch between a producer and its consumer."""
+
+    __slots__ = ("q", "e")
+
+    def __init__(self, q: torch.Tensor, e: torch.Tensor):
+        if (q.dtype != torch.uint8 or e.dtype != torch.uint8 or q.dim() != 2 or q.shape[1] % 32
+                or e.shape != (q.shape[0], q.shape[1] // 32)):
+            raise ValueError("MxAct needs q [M, K] uint8 (K % 32 == 0) and e [M, K / 32] uint8")
+        self.q, self.e = q, e
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    @property
+    def device(self):
+        return self.q.device
+
+    @property
+    def is_cuda(self) -> bool:
+        return self.q.is_cuda
+
+    def dequant(self, dtype=BF16) -> torch.Tensor:
+        return ref.dequant_mx(self.q, self.e, torch.float32).to(dtype)
+
+
+# K8S_MX=0: the fp8 O / down GEMM rows take per-token e4m3 activations (a quantize_act_fp8 launch each) instead of
+# the MX form their producers write.
+MX_ON = os.environ.get("K8S_MX", "1") != "0"
+
+
+def quantize_act_mx(x: torch.Tensor) -> MxAct:
+    """bf16 [M, K] -> MxAct (stand-alone form of what the fused producers write; K % 32 == 0)."""
+    if not x.is_cuda:
+        return MxAct(*ref.quantize_mx(x))
+    M, K = x.shape
+    q = torch.empty(M, K, dtype=torch.uint8, device=x.device)
+    e = torch.empty(M, K // 32, dtype=torch.uint8, device=x.device)
+    native().quantize_act_mx(q.data_ptr(), e.data_ptr(), _chk(x, BF16, "x"), M, K, -1)
+    return MxAct(q, e)
+
+
 def _fp8_gemm(x: torch.Tensor, w: "Fp8Weight", out_dtype=None, act=None) -> torch.Tensor:
     """K8S_GEMM=library only (the A/B oracle): per-token e4m3 activations (``act`` = (q, scale) when already
     quantized) x row-scaled e4m3 weights on hipBLASLt's row-wise scaled fp8 GEMM (torch._scaled_mm), bf16 out."""
@@ -462,11 +509,14 @@ def mgemm_nwg(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int) 
     return max(1, min(nwg, total))
 
 
-def mgemm_valid(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int = 1) -> bool:
-    """``fp8``: 0 / False bf16, 1 / True fp8 activations and weights, 2 W8 (fp8 weights, bf16 activations)."""
+def mgemm_valid(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int = 1, mx_out: bool = False) -> bool:
+    """``fp8``: 0 / False bf16, 1 / True fp8 activations and weights, 2 W8 (fp8 weights, bf16 activations), 3 MX
+    activations (fp8 weights).  ``mx_out``: the SwiGLU epilogue writes MX e4m3 (fp8 / MX modes)."""
     if cfg < 0 or cfg >= len(mgemm_configs()):
         return False
-    if int(fp8) == 2 and _mg_w8_lds(cfg) < 0:
+    if int(fp8) in (2, 3) and _mg_mode_lds(cfg, int(fp8)) < 0:
+        return False
+    if mx_out and (epi != EPI_SWIGLU or int(fp8) not in (1, 3) or N % 32 or _mg_mode_lds(cfg, 4) < 0):
         return False
     kb = K * (1 if fp8 else 2)
     if kb % mgemm_configs()[cfg][5] or N % 4 or M <= 0:
@@ -481,9 +531,15 @@ def _mgemm_ok(N: int, K: int, fp8: bool) -> bool:
     return N % 4 == 0 and (K * (1 if fp8 else 2)) % 128 == 0
 
 
-@functools.lru_cache(maxsize=64)
+@functools.lru_cache(maxsize=256)
+def _mg_mode_lds(cfg: int, mode: int) -> int:
+    """LDS bytes of a configuration in a mode (2 W8, 3 MX activations; 4: 0 if its SwiGLU epilogue writes MX
+    output), -1 where the configuration is not built for it."""
+    return native().mgemm_lds_bytes(cfg, mode)
+
+
 def _mg_w8_lds(cfg: int) -> int:
-    return native().mgemm_lds_bytes(cfg, 2)
+    return _mg_mode_lds(cfg, 2)
 
 
 # W8: fp8 weights against bf16 activations in mgemm (17..W8_MAX_M rows: batched decode and short mixed steps): the
@@ -513,6 +569,31 @@ def mgemm_w8_plan(M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]
         return pick[1], pick[2]
     cfg, grid = mgemm_heuristic(M, N, K, epi, 2)
     return (cfg, grid) if mgemm_valid(cfg, M, N, K, epi, 2, grid) else None
+
+
+def mgemm_mx_plan(M: int, N: int, K: int, epi: int, act_mx: bool, mx_out: bool) -> Optional[Tuple[int, int]]:
+    """(cfg, grid) for fp8 weights with MX activations (``act_mx``) and / or MX SwiGLU output, or None: the tuned fp8
+    plan where that configuration runs the mode, else the fp8 heuristic's, else the first weight-streaming / MFMA-dense
+    configuration that does (same grid rule)."""
+    mode = 3 if act_mx else 1
+    if K % 128:
+        return None
+    pick = _mg_table_row(M, N, K, epi, 1)
+    if pick is not None and mgemm_valid(pick[1], M, N, K, epi, mode, pick[2], mx_out):
+        return pick[1], pick[2]
+    cfg, grid = mgemm_heuristic(M, N, K, epi, 1)
+    if mgemm_valid(cfg, M, N, K, epi, mode, grid, mx_out):
+        return cfg, grid
+    order = (12, 11, 8, 3, 2, 0, 13, 9, 5, 14, 15, 16, 19, 22) if M <= 128 else (15, 19, 22, 16, 17, 12)
+    for c in order:
+        if mgemm_valid(c, M, N, K, epi, mode, 1, mx_out):
+            tiles = _mg_tiles(c, M, N, epi)
+            steps = K // mgemm_configs()[c][5]
+            split = 1
+            while tiles * split * 2 <= 512 and steps // (split * 2) >= 8:
+                split *= 2
+            return c, split
+    return None
 
 
 @functools.lru_cache(maxsize=4096)
@@ -607,18 +688,24 @@ def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
 
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
           grid: Optional[int] = None, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
-          out: Optional[torch.Tensor] = None, act: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-          w8: bool = False) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, act=None, w8: bool = False, mx_out: bool = False):
     """Hand-written MFMA GEMM (mgemm.hip): epi(x[M, K] @ w[N, K].T), any M (routed for M > GEMV_MAX_M).  ``w``: bf16 or
     Fp8Weight (activations are then quantized per token by quantize_act_fp8, or with ``w8`` stay bf16: W8 mode).
     SwiGLU: w = [Wg; Wu].  ``rms_eps``: RMSNorm prologue -- the result is scaled by 1/rms(x row) (the norm gamma must
     be folded into ``w``), so the un-normalised residual stream feeds the GEMM directly (bf16 or W8).  ``res``:
-    residual epilogue (bf16 output only) -- out = x @ w.T + res, one rounding; ``out`` may be ``res`` (in place)."""
+    residual epilogue (bf16 output only) -- out = x @ w.T + res, one rounding; ``out`` may be ``res`` (in place).
+    ``act``: an :class:`MxAct` (mode 3, the block-scaled MFMA) or the (e4m3, per-token scale) pair of quantize_act_fp8.
+    ``mx_out`` (fp8 weights, SwiGLU): returns the output as an :class:`MxAct` written by the epilogue."""
+    if isinstance(x, MxAct):
+        act = x
     M, K = x.shape
     fp8 = _is_fp8(w)
-    mode = (2 if w8 else 1) if fp8 else 0
+    act_mx = isinstance(act, MxAct)
+    mode = (2 if w8 else 3 if act_mx else 1) if fp8 else 0
     if w8 and (not fp8 or act is not None):
         raise ValueError("mgemm: W8 mode takes fp8 weights and bf16 activations")
+    if (act_mx or mx_out) and not fp8:
+        raise ValueError("mgemm: MX activations / output need fp8 weights")
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     if cfg is None:
         if mode == 2:
@@ -626,35 +713,54 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
             if plan is None:
                 raise ValueError(f"mgemm: no W8 configuration runs M={M} N={N} K={K} epi={epi}")
             cfg, grid = plan
+        elif act_mx or mx_out:
+            plan = mgemm_mx_plan(M, N, K, epi, act_mx, mx_out)
+            if plan is None:
+                raise ValueError(f"mgemm: no MX configuration runs M={M} N={N} K={K} epi={epi}")
+            cfg, grid = plan
         else:
             cfg, grid = mgemm_plan(M, N, K, epi, fp8)
     grid = grid or 1
-    if not mgemm_valid(cfg, M, N, K, epi, mode, grid):
-        raise ValueError(f"mgemm: cfg {cfg} / grid {grid} invalid for M={M} N={N} K={K} epi={epi} mode={mode}")
+    if not mgemm_valid(cfg, M, N, K, epi, mode, grid, mx_out):
+        raise ValueError(f"mgemm: cfg {cfg} / grid {grid} invalid for M={M} N={N} K={K} epi={epi} mode={mode}"
+                         f"{' mx_out' if mx_out else ''}")
     nwg = mgemm_nwg(cfg, M, N, K, epi, fp8, grid)
     tiles, cmax, n_ws = _mg_plan_info(M, N, K, epi, mode, cfg, nwg)
     if mode == 1 and rms_eps is not None:
         raise ValueError("mgemm: the RMS prologue needs bf16 activations")
     if res is not None and (epi != EPI_BF16 or res.shape != (M, N)):
         raise ValueError("mgemm: residual epilogue needs a bf16 [M, N] residual and the bf16 epilogue")
+    mxo = None
+    if mx_out:
+        if res is not None:
+            raise ValueError("mgemm: MX output is the SwiGLU epilogue's")
+        mxo = MxAct(torch.empty(M, N, dtype=torch.uint8, device=x.device),
+                    torch.empty(M, N // 32, dtype=torch.uint8, device=x.device))
+        out = mxo.q   # (not written as bf16)
     if out is None:
         out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
     ws = torch.empty(n_ws, dtype=F32, device=x.device) if n_ws > 0 else None
     tk = _zeroed_scratch(x.device, "mgemm", 4 * tiles, 64 * 1024) if cmax > 1 else 0
     rp = _chk(res, BF16, "res") if res is not None else 0
     rms, eps = (1, float(rms_eps)) if rms_eps is not None else (0, 0.0)
-    if mode == 2:
+    oq, oe = (mxo.q.data_ptr(), mxo.e.data_ptr()) if mxo is not None else (0, 0)
+    if act_mx:
+        if act.shape != (M, K) or not act.q.is_cuda:
+            raise ValueError(f"mgemm: MX activations {tuple(act.shape)} for x {(M, K)}")
+        native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, act.q.data_ptr(), w.q.data_ptr(),
+                       act.e.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 3, cfg, nwg, cmax, rp, 0, 0.0, -1, oq, oe)
+    elif mode == 2:
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"), w.q.data_ptr(),
                        0, w.scale.data_ptr(), M, N, K, epi, 2, cfg, nwg, cmax, rp, rms, eps, -1)
     elif fp8:
         xq, sx = act if act is not None else quantize_act_fp8(x.contiguous())
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, xq.data_ptr(), w.q.data_ptr(),
-                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, nwg, cmax, rp, 0, 0.0, -1)
+                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, nwg, cmax, rp, 0, 0.0, -1, oq, oe)
     else:
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"),
                        _chk(w, BF16, "w"), 0, 0, M, N, K, epi, 0, cfg, nwg, cmax, rp, rms, eps, -1)
     del ws
-    return out
+    return mxo if mxo is not None else out
 
 
 # ----------------------------------------------------------------------------- big-tile MFMA GEMM (prefill rows)

@@ -183,6 +183,31 @@ def dequant_fp8(q: torch.Tensor, scale: torch.Tensor, dtype=torch.float32) -> to
     return (q.view(torch.float8_e4m3fn).float() * scale.float()[:, None]).to(dtype)
 
 
+MX_BLOCK = 32
+
+
+def quantize_mx(x: torch.Tensor):
+    """OCP MX e4m3 (fp8.hip quantize_act_mx_kernel): every 32 consecutive values of a row share the E8M0 scale
+    e = the smallest power of two >= max|block| / 448 (byte 127 + log2; 127 for an all-zero block, clamped to
+    [1, 253]).  Returns (q [M, K] uint8 e4m3 bit patterns, e [M, K / 32] uint8)."""
+    M, K = x.shape
+    xf = x.float().reshape(M, K // MX_BLOCK, MX_BLOCK)
+    amax = xf.abs().amax(dim=-1)
+    bits = (amax * (1.0 / FP8_MAX)).contiguous().view(torch.int32)
+    e = (bits >> 23) + ((bits & 0x7FFFFF) != 0).to(torch.int32)
+    e = torch.where(amax == 0, torch.full_like(e, 127), e).clamp(1, 253)
+    inv = torch.ldexp(torch.ones_like(amax), (127 - e).float())
+    q = (xf * inv[..., None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8).reshape(M, K), e.to(torch.uint8)
+
+
+def dequant_mx(q: torch.Tensor, e: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    M, K = q.shape
+    s = torch.ldexp(torch.ones(e.shape, dtype=torch.float32, device=q.device), e.float() - 127)
+    v = q.view(torch.float8_e4m3fn).float().reshape(M, K // MX_BLOCK, MX_BLOCK) * s[..., None]
+    return v.reshape(M, K).to(dtype)
+
+
 def _wf(w) -> torch.Tensor:
     """fp32 view of a weight: a plain tensor or an ops.Fp8Weight (duck-typed: .q / .scale)."""
     if hasattr(w, "scale") and hasattr(w, "q"):

@@ -1,0 +1,109 @@
+"""K16 block-scaled activations (OCP MX e4m3, one E8M0 scale per 32 values): the stand-alone quantizer against the
+CPU reference bit for bit, mgemm's MX mode (block-scaled 16x16x128 MFMA, the scales as its B scale operand) against
+the fp32 oracle of the dequantized operands for every configuration built for it, and the SwiGLU epilogue's MX output
+against quantizing the same GEMM's bf16 output (bit for bit)."""
+
+import pytest
+import torch
+
+from k8s_llm_scheduler_amd import ops
+from k8s_llm_scheduler_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _act(M, K, seed, spread=True):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(M, K, generator=g)
+    if spread:   # block magnitudes over 2^-8 .. 2^8, some all-zero blocks, one huge value
+        x = x * torch.pow(2.0, torch.randint(-8, 9, (M, K // 32), generator=g).float()).repeat_interleave(32, 1)
+        x[0, :32] = 0
+        x[-1, 5] = 3.0e4
+    return x.to(torch.bfloat16)
+
+
+def _weights(rows, K, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return ops.quantize_fp8(((torch.rand(rows, K, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16).to(DEV))
+
+
+@pytest.mark.parametrize("M,K", [(1, 32), (17, 256), (64, 8192), (130, 3584), (7, 28672)])
+def test_quantize_act_mx_matches_reference_bit_for_bit(M, K):
+    x = _act(M, K, M + K)
+    a = ops.quantize_act_mx(x.to(DEV))
+    q, e = ref.quantize_mx(x)
+    assert torch.equal(a.e.cpu(), e)
+    assert torch.equal(a.q.cpu(), q)
+    back = a.dequant(torch.float32).cpu()
+    blk = torch.ldexp(torch.ones(e.shape), e.float() - 127).repeat_interleave(32, 1)   # the block scales
+    err = (back - x.float()).abs()
+    assert bool((err <= 16 * blk).all())             # half an e4m3 ulp of the top binade (32), scaled
+    normal = x.float().abs() >= 2 ** -6 * blk          # e4m3 normal range: relative error <= 2^-4
+    assert bool((err[normal] <= 2 ** -4 * x.float().abs()[normal] + 1e-30).all())
+
+
+def _mx_oracle(act, w, epi):
+    xr = ref.dequant_mx(act.q.cpu(), act.e.cpu(), torch.float32)
+    y = xr @ ref.dequant_fp8(w.q.cpu(), w.scale.cpu(), torch.float32).t()
+    if epi == ops.EPI_SWIGLU:
+        n = y.shape[1] // 2
+        y = torch.nn.functional.silu(y[:, :n]) * y[:, n:]
+    return y
+
+
+@pytest.mark.parametrize("epi", [ops.EPI_BF16, ops.EPI_F32, ops.EPI_SWIGLU])
+def test_mgemm_mx_every_config(epi):
+    """MX activations x row-scaled e4m3 weights on every configuration built for the mode, one-workgroup-per-tile /
+    split-K / stream-K grids, partial M tiles, the residual epilogue."""
+    K, N = 1024, 192
+    rows = 2 * N if epi == ops.EPI_SWIGLU else N
+    w = _weights(rows, K, 11)
+    n_cfg = 0
+    for cfg, (bm, *_rest) in enumerate(ops.mgemm_configs()):
+        if not ops.mgemm_valid(cfg, 64, N, K, epi, 3):
+            continue
+        n_cfg += 1
+        for M in (17, bm + 7):
+            act = ops.quantize_act_mx(_act(M, K, cfg * 100 + M, spread=False).to(DEV))
+            exp = _mx_oracle(act, w, epi)
+            for grid in (1, 4, -7, -256):
+                if not ops.mgemm_valid(cfg, M, N, K, epi, 3, grid):
+                    continue
+                y = ops.mgemm(act, w, epi, cfg=cfg, grid=grid).float().cpu()
+                err = (y - exp).abs().max().item()
+                assert err <= 1e-2 * exp.abs().max().item(), f"cfg {cfg} grid {grid} M {M}: {err}"
+                if epi == ops.EPI_BF16:
+                    res = ((torch.rand(M, N, device=DEV) * 2 - 1) * 8).to(torch.bfloat16)
+                    want = exp + res.float().cpu()
+                    out = ops.mgemm(act, w, epi, cfg=cfg, grid=grid, res=res, out=res)
+                    err = (out.float().cpu() - want).abs().max().item()
+                    assert err <= 1e-2 * want.abs().max().item(), f"res cfg {cfg} grid {grid} M {M}: {err}"
+    assert n_cfg >= 6
+
+
+@pytest.mark.parametrize("act_mx", [False, True])
+def test_mgemm_swiglu_mx_output_is_the_quantized_bf16_output(act_mx):
+    """The SwiGLU epilogue's MX output equals quantize_act_mx of the bf16 output of the same launch plan, bit for
+    bit (same accumulation, the bf16 value is what gets quantized), for per-token and MX activations."""
+    K, N = 1024, 256
+    w = _weights(2 * N, K, 5)
+    n_cfg = 0
+    for cfg in range(len(ops.mgemm_configs())):
+        mode = 3 if act_mx else 1
+        if not ops.mgemm_valid(cfg, 64, N, K, ops.EPI_SWIGLU, mode, 1, mx_out=True):
+            continue
+        n_cfg += 1
+        for M in (19, 64):
+            x = _act(M, K, cfg + M, spread=False).to(DEV)
+            act = ops.quantize_act_mx(x) if act_mx else ops.quantize_act_fp8(x)
+            for grid in (1, 4, -256):
+                if not ops.mgemm_valid(cfg, M, N, K, ops.EPI_SWIGLU, mode, grid, mx_out=True):
+                    continue
+                y = ops.mgemm(x, w, ops.EPI_SWIGLU, cfg=cfg, grid=grid, act=act)
+                mx = ops.mgemm(x, w, ops.EPI_SWIGLU, cfg=cfg, grid=grid, act=act, mx_out=True)
+                q, e = ref.quantize_mx(y.cpu())
+                assert torch.equal(mx.e.cpu(), e), f"cfg {cfg} grid {grid} M {M}"
+                assert torch.equal(mx.q.cpu(), q), f"cfg {cfg} grid {grid} M {M}"
+    assert n_cfg >= 2
