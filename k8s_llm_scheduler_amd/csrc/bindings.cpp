@@ -117,7 +117,7 @@ int k8s_pgemm_plan(int M, int N_out, int K, int epi, int fp8, int cfg, int split
                    int* tickets);
 int k8s_pgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs, const float* wsc,
               int M, int N_out, int K, int epi, int fp8, int cfg, int splits, int group_m, const void* res, int rms,
-              float eps, hipStream_t s);
+              float eps, void* oq, void* oe, hipStream_t s);
 }
 
 namespace {
@@ -414,11 +414,14 @@ PYBIND11_MODULE(K8S_MODULE_NAME, m) {
   });
   m.def("pgemm", [](uintptr_t out, uintptr_t ws, uintptr_t tickets, uintptr_t x, uintptr_t W, uintptr_t xs,
                     uintptr_t wsc, int M, int N, int K, int epi, int fp8, int cfg, int splits, int group_m,
-                    uintptr_t res, int rms, float eps, int64_t s) {
+                    uintptr_t res, int rms, float eps, int64_t s, uintptr_t oq, uintptr_t oe) {
     check(k8s_pgemm(P(out), P<float>(ws), P<unsigned>(tickets), P(x), P(W), P<float>(xs), P<float>(wsc), M, N, K,
-                    epi, fp8, cfg, splits, group_m, P(res), rms, eps, S(s)),
+                    epi, fp8, cfg, splits, group_m, P(res), rms, eps, P(oq), P(oe), S(s)),
           "pgemm");
-  });
+  }, py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("x"), py::arg("W"), py::arg("xs"), py::arg("wsc"),
+     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("fp8"), py::arg("cfg"), py::arg("splits"),
+     py::arg("group_m"), py::arg("res"), py::arg("rms"), py::arg("eps"), py::arg("s"), py::arg("oq") = 0,
+     py::arg("oe") = 0);
 
   using k8sllm::RcclComm;
   py::class_<RcclComm>(m, "RcclComm")

@@ -34,6 +34,12 @@
 //    row-major slab and k8s_pgemm_reduce (pgemm4.hip) sums the slabs in slice order (deterministic) and runs the
 //    epilogue over every CU.  The alternative in-launch form (K8S_PGEMM_ROWSLAB=0) publishes fragment-order slabs
 //    (agent release + arrival ticket) and the last arriving slice reduces them; the ticket is reset by the reducer.
+//  * MX activations (fp8 = 3; K16 block-scaled, fp8.hip): the x bytes are OCP MX e4m3 and the E8M0 byte of each
+//    32-value block is the B scale of the scaled MFMA (the lane holding that block's scale: li + 16 b, see
+//    tools/experiments/mx_scale_probe.hip).  The tile's scale dwords (one per token row and k-tile) ride region QB0
+//    as one 4-byte LDS-DMA per wave and are read in phase 0 with the QB0 fragments (the region's last reader).
+//  * MX output (SwiGLU, mx_out): each wave's features come in 32-feature blocks (fragment pairs), so the epilogue
+//    writes e4m3 + E8M0 directly (4-lane shuffle max) -- the down projection's input, quantized by its producer.
 //  * RMS prologue (bf16): the un-normalised residual stream is the x operand; the x fragments every wave
 //    already holds give the row sums of squares (v_dot2_f32_bf16, waves 0-3 for QB0, 4-7 for QB1), and the
 //    epilogue scales by 1 / rms (the norm gamma is folded into W at load time).
@@ -68,6 +74,9 @@ __device__ __forceinline__ void pg_vm_wait(int n) {
     case 8: pg_vmcnt<8>(); break;
     case 9: pg_vmcnt<9>(); break;
     case 10: pg_vmcnt<10>(); break;
+    case 11: pg_vmcnt<11>(); break;
+    case 12: pg_vmcnt<12>(); break;
+    case 13: pg_vmcnt<13>(); break;
     default: pg_vmcnt<0>(); break;
   }
 }
@@ -85,8 +94,8 @@ __device__ __forceinline__ void pg_barrier() {
 __device__ __forceinline__ float pg_silu(float g) { return g / (1.f + __expf(-g)); }
 
 // LDS-DMA instructions issued after region (u0, y0) up to and including region (u1, y1) in issue order
-// (k-tile major; region types y = 0 QB0, 1 PA0, 2 QB1, 3 PA1), counting only k-tiles < n.
-template <int GP, int GQ>
+// (k-tile major; region types y = 0 QB0 (+ GS scale loads), 1 PA0, 2 QB1, 3 PA1), counting only k-tiles < n.
+template <int GP, int GQ, int GS = 0>
 __device__ __forceinline__ int pg_after(int u0, int y0, int u1, int y1, int n) {
   int c = 0;
   int u = u0, y = y0 + 1;
@@ -96,7 +105,7 @@ __device__ __forceinline__ int pg_after(int u0, int y0, int u1, int y1, int n) {
       ++u;
       continue;
     }
-    if (u < n) c += (y & 1) ? GP : GQ;
+    if (u < n) c += (y & 1) ? GP : y == 0 ? GQ + GS : GQ;
     ++y;
   }
   return c;
@@ -112,6 +121,9 @@ struct PgArgs {
   const uint8_t* W;      // [rows][K] bf16 or e4m3
   const float* xs;       // fp8: [M] per-token scales
   const float* wsc;      // fp8: [rows] per-row scales
+  const uint8_t* xe;     // MX activations: [M][K / 32] E8M0 block scales
+  uint8_t* oq;           // MX output (SwiGLU): e4m3 [M][N_out] + E8M0 [M][N_out / 32]
+  uint8_t* oe;
   uint32_t kbytes;       // bytes per row of x and W
   int M, N_out, half_rows, K;
   int m_tiles, n_tiles, kt, splits, group_m, nwg;
@@ -122,18 +134,25 @@ struct PgArgs {
                          // sums [splits][M]) and k8s_pgemm_reduce (all CUs) combines them -- no last-arriver tail
 };
 
-template <int FP, int FQ, int EPI, bool FP8, bool RMS>
+template <int FP, int FQ, int EPI, bool FP8, bool RMS, bool MX = false, bool MXO = false>
 __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   constexpr int BP = 64 * FP, BQ = 128 * FQ;         // weight rows, tokens per tile
   constexpr int RP = BP / 2, RQ = BQ / 2;            // rows per PA / QB region
   constexpr int GP = RP / 64, GQ = RQ / 64;          // 16-byte DMA instructions per thread per region
-  constexpr int STAGE = (BP + BQ) * 128;
+  constexpr int GS = MX ? 1 : 0;                     // MX: one 4-byte scale LDS-DMA per wave with QB0
+  constexpr int SCH = BQ / 8;                        // MX: scale dwords (token rows) per wave
+  constexpr int OFF_SC = (BP + BQ) * 128;            // MX: the stage's [BQ] scale dwords
+  constexpr int STAGE = (BP + BQ) * 128 + (MX ? BQ * 4 : 0);
   constexpr int OFF_QB0 = 0, OFF_PA0 = RQ * 128, OFF_QB1 = (RQ + RP) * 128, OFF_PA1 = (2 * RQ + RP) * 128;
   constexpr int NA = 2 * FP, NB = 2 * FQ;            // fragments per wave along P / Q
   constexpr int SLAB = BP * BQ + BQ;
-  constexpr int STEADY0 = 3 * GP + 2 * GQ, STEADY1 = 2 * GP + 3 * GQ;
-  static_assert(GP >= 1 && GQ >= 1 && STEADY0 <= 10 && STEADY1 <= 10, "tile shape");
+  // counted waits (see phase()): j = 0 waits for QB1(t), j = 1 for PA1(t), j = 3 for PA0(t + 1)
+  constexpr int STEADY0 = 3 * GP + 2 * GQ + GS, STEADY1 = 2 * GP + 3 * GQ + 2 * GS, STEADY3 = 2 * GP + 3 * GQ + GS;
+  static_assert(GP >= 1 && GQ >= 1 && STEADY0 <= 13 && STEADY1 <= 13, "tile shape");
   static_assert(!(FP8 && RMS), "fp8 activations are quantized before the GEMM");
+  static_assert(!MX || FP8, "MX: e4m3 activations");
+  static_assert(!MXO || (EPI == PG_SWIGLU && FP8 && FP % 2 == 0), "MX output: SwiGLU fragment pairs");
+  static_assert(SCH <= 64, "scale dwords per wave");
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the launch stub
   __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + 64 + BQ * 4];
   unsigned* flag = reinterpret_cast<unsigned*>(lds + 2 * STAGE);
@@ -159,7 +178,9 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   const int n = (int)((long long)(slice + 1) * a.kt / a.splits) - kt0;
 
   // ---- per-thread DMA sources (byte offsets from the operand bases; the host checks < 4 GiB)
-  uint32_t oq0[GQ], oq1[GQ], op0[GP], op1[GP];
+  uint32_t oq0[GQ], oq1[GQ], op0[GP], op1[GP], osc = 0;
+  if constexpr (MX)   // token row wid * SCH + lane of the tile, k-tile kt0 (4 scale bytes = the k-tile's 4 blocks)
+    osc = (uint32_t)min(mt * BQ + wid * SCH + min(lane, SCH - 1), a.M - 1) * (a.kbytes >> 5) + (uint32_t)(kt0 * 4);
 #pragma unroll
   for (int i = 0; i < GQ; ++i) {
     const int p = i * 512 + tid, r = p >> 3, c = (p & 7) ^ ((r >> 1) & 7);
@@ -200,7 +221,16 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     char* dst = lds + (u & 1) * STAGE + wid * 1024 +
                 (y == 0 ? OFF_QB0 : y == 1 ? OFF_PA0 : y == 2 ? OFF_QB1 : OFF_PA1);
     const uint32_t kb = (uint32_t)u * 128u;
-    if constexpr (y == 0) dma(a.x + kb, oq0, dst, std::integral_constant<int, GQ>{});
+    if constexpr (y == 0) {
+      dma(a.x + kb, oq0, dst, std::integral_constant<int, GQ>{});
+      if constexpr (MX) {
+        if (lane < SCH)
+          __builtin_amdgcn_global_load_lds(a.xe + osc + u * 4,
+                                           (__attribute__((address_space(3))) void*)(lds + (u & 1) * STAGE + OFF_SC +
+                                                                                     wid * SCH * 4),
+                                           4, 0, 0);
+      }
+    }
     if constexpr (y == 1) dma(a.W + kb, op0, dst, std::integral_constant<int, GP>{});
     if constexpr (y == 2) dma(a.x + kb, oq1, dst, std::integral_constant<int, GQ>{});
     if constexpr (y == 3) dma(a.W + kb, op1, dst, std::integral_constant<int, GP>{});
@@ -214,7 +244,9 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   const int swz = li >> 1;
   int lo[2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) lo[h] = li * 128 + ((((FP8 ? 2 * g : 4 * h + g) + (FP8 ? h : 0)) ^ swz) << 4);
+  // lane (li, g): bf16 k32 step h = chunk 4 h + g; fp8 (one 16x16x128 step) chunks g and 4 + g, the scaled MFMA's
+  // operand layout (k 16 g.. in bytes 0-15, 64 + 16 g.. in bytes 16-31; tools/experiments/mx_scale_probe.hip)
+  for (int h = 0; h < 2; ++h) lo[h] = li * 128 + (((4 * h + g) ^ swz) << 4);
   const int pbase = wr * (BP / 4) * 128, qbase = wc * (BQ / 8) * 128;
 
   // operand registers: bf16 [k32 step][fragment]; fp8 [fragment] x two 16-byte halves
@@ -228,6 +260,9 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   float ss[FQ];
 #pragma unroll
   for (int f = 0; f < FQ; ++f) ss[f] = 0.f;
+  int sc[2][FQ];   // MX: this lane's B scale (block g of its token row) per x fragment of the current k-tile
+#pragma unroll
+  for (int f = 0; f < FQ; ++f) sc[0][f] = sc[1][f] = 0x7f7f7f7f;
 
   auto read_frags = [&](const char* rb, frag_t* d0, frag_t* d1, auto NF_) {
     constexpr int NF = decltype(NF_)::value;
@@ -258,7 +293,7 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
           f32x4& c = acc[ah * FP + fp][bh * FQ + fq];
           if constexpr (FP8) {
             c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(Ar[0][fp], bh ? B1r[0][fq] : B0r[0][fq], c, 0, 0, 0,
-                                                                 0x7f7f7f7f, 0, 0x7f7f7f7f);
+                                                                 0x7f7f7f7f, 0, MX ? sc[bh][fq] : 0x7f7f7f7f);
           } else {
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ar[kk][fp], bh ? B1r[kk][fq] : B0r[kk][fq], c, 0, 0, 0);
           }
@@ -288,6 +323,13 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     if constexpr (j == 0) {
       read_frags(sb + OFF_QB0 + qbase, B0r[0], B0r[FP8 ? 0 : 1], NFQ{});
       read_frags(sb + OFF_PA0 + pbase, Ar[0], Ar[FP8 ? 0 : 1], NFP{});
+      if constexpr (MX) {   // both halves' scales now: the region is refilled in phase 1
+        const int* scl = reinterpret_cast<const int*>(sb + OFF_SC);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int f = 0; f < FQ; ++f) sc[h][f] = scl[wc * (BQ / 4) + h * (BQ / 8) + f * 16 + li] >> (8 * g);
+      }
       if (t + 1 < n) issue(Y3{}, t + 1);
     } else if constexpr (j == 1) {
       read_frags(sb + OFF_QB1 + qbase, B1r[0], B1r[FP8 ? 0 : 1], NFQ{});
@@ -301,11 +343,11 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     // the regions the next phase reads are complete for this wave (counted: the newer DMA stays in flight)
     if constexpr (j != 2) {
       if (t + 2 < n) {
-        pg_vmcnt<j == 0 ? STEADY0 : STEADY1>();
+        pg_vmcnt<j == 0 ? STEADY0 : j == 1 ? STEADY1 : STEADY3>();
       } else {
-        const int c = j == 0 ? pg_after<GP, GQ>(t, 2, t + 1, 3, n)
-                    : j == 1 ? pg_after<GP, GQ>(t, 3, t + 2, 0, n)
-                             : pg_after<GP, GQ>(t + 1, 1, t + 2, 2, n);
+        const int c = j == 0 ? pg_after<GP, GQ, GS>(t, 2, t + 1, 3, n)
+                    : j == 1 ? pg_after<GP, GQ, GS>(t, 3, t + 2, 0, n)
+                             : pg_after<GP, GQ, GS>(t + 1, 1, t + 2, 2, n);
         pg_vm_wait(c);
       }
     }
@@ -338,7 +380,7 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     issue(Y1{}, 1);
     issue(Y2{}, 1);
   }
-  pg_vm_wait(pg_after<GP, GQ>(0, 1, 1, 2, n));
+  pg_vm_wait(pg_after<GP, GQ, GS>(0, 1, 1, 2, n));
   pg_barrier();
   if (late) __builtin_amdgcn_s_barrier();   // stagger waves 4-7 by one barrier (wave-uniform branch)
   if (a.prio == 1 && late) __builtin_amdgcn_s_setprio(1);
@@ -458,9 +500,36 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     const int m = mt * BQ + mloc;
     if (m >= a.M) continue;
     float sx = 1.f;
-    if constexpr (FP8) sx = a.xs[m];
+    if constexpr (FP8 && !MX) sx = a.xs[m];
     if constexpr (RMS) sx = rsqrtf(rss[mloc] / (float)a.K + a.eps);
-    if constexpr (EPI == PG_SWIGLU) {
+    if constexpr (MXO) {   // 32-feature blocks = fragment pairs (2 b, 2 b + 1); the block's lanes share li
+#pragma unroll
+      for (int b = 0; b < FP / 2; ++b) {
+        const int nb = nt * (BP / 2) + wr * (BP / 4) + b * 32;
+        if (nb >= a.N_out) continue;   // N_out % 32 == 0: whole blocks
+        float v[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int fp = 2 * b + h, f0 = nb + 16 * h + 4 * g;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float gt = acc[fp][bq][i] * sx * a.wsc[f0 + i], up = acc[FP + fp][bq][i] * sx * a.wsc[a.half_rows + f0 + i];
+            v[4 * h + i] = bf_round(pg_silu(gt) * up);
+          }
+        }
+        float amax = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+        amax = fmaxf(amax, __shfl_xor(amax, 16, WAVE));
+        amax = fmaxf(amax, __shfl_xor(amax, 32, WAVE));
+        const uint32_t e = mx_e8m0(amax);
+        const float inv = mx_inv_scale(e);
+        uint8_t* orow = a.oq + (size_t)m * a.N_out;
+        *reinterpret_cast<uint32_t*>(orow + nb + 4 * g) = mx_pack4(v[0], v[1], v[2], v[3], inv);
+        *reinterpret_cast<uint32_t*>(orow + nb + 16 + 4 * g) = mx_pack4(v[4], v[5], v[6], v[7], inv);
+        if (g == 0) a.oe[(size_t)m * (a.N_out >> 5) + (nb >> 5)] = (uint8_t)e;
+      }
+    } else if constexpr (EPI == PG_SWIGLU) {
 #pragma unroll
       for (int fp = 0; fp < FP; ++fp) {
         const int f0 = nt * (BP / 2) + wr * (BP / 4) + fp * 16 + 4 * g;
@@ -524,20 +593,29 @@ constexpr PgCfg kPgCfgs[] = {
 };
 constexpr int kPgNumCfgs = sizeof(kPgCfgs) / sizeof(kPgCfgs[0]);
 
-template <int C, int EPI, bool FP8, bool RMS>
+template <int C, int EPI, bool FP8, bool RMS, bool MX = false, bool MXO = false>
 int pg_launch(const PgArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((pgemm_kernel<kPgCfgs[C].fp, kPgCfgs[C].fq, EPI, FP8, RMS>), dim3(a.nwg), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((pgemm_kernel<kPgCfgs[C].fp, kPgCfgs[C].fq, EPI, FP8, RMS, MX, MXO>), dim3(a.nwg), dim3(512), 0,
+                     s, a);
   return (int)hipGetLastError();
+}
+
+template <int C, bool MX>
+int pg_epi_f8(const PgArgs& a, int epi, bool mxo, hipStream_t s) {
+  if (mxo) return epi == PG_SWIGLU ? pg_launch<C, PG_SWIGLU, true, false, MX, true>(a, s) : -2;
+  switch (epi) {
+    case PG_BF16: return pg_launch<C, PG_BF16, true, false, MX>(a, s);
+    case PG_F32: return pg_launch<C, PG_F32, true, false, MX>(a, s);
+    case PG_SWIGLU: return pg_launch<C, PG_SWIGLU, true, false, MX>(a, s);
+  }
+  return -2;
 }
 
 template <int C, bool FP8>
 int pg_epi(const PgArgs& a, int epi, int rms, hipStream_t s) {
   if constexpr (FP8) {
-    switch (epi) {
-      case PG_BF16: return pg_launch<C, PG_BF16, true, false>(a, s);
-      case PG_F32: return pg_launch<C, PG_F32, true, false>(a, s);
-      case PG_SWIGLU: return pg_launch<C, PG_SWIGLU, true, false>(a, s);
-    }
+    const bool mxo = a.oq != nullptr;
+    return a.xe != nullptr ? pg_epi_f8<C, true>(a, epi, mxo, s) : pg_epi_f8<C, false>(a, epi, mxo, s);
   } else {
     if (rms) {
       switch (epi) {
@@ -603,7 +681,8 @@ extern "C" int k8s_pgemm_set_row_slabs(int on) {
   return old;
 }
 extern "C" int k8s_pgemm_reduce(void* out, const void* res, const float* slab, int splits, int M, int N_out, int K,
-                                int epi, int rms, float eps, const float* xs, const float* wsc, hipStream_t s);
+                                int epi, int rms, float eps, const float* xs, const float* wsc, void* oq, void* oe,
+                                hipStream_t s);
 
 extern "C" int k8s_pgemm_num_configs() { return kPgNumCfgs; }
 
@@ -629,12 +708,18 @@ extern "C" int k8s_pgemm_plan(int M, int N_out, int K, int epi, int fp8, int cfg
   return 0;
 }
 
-// out[M, N_out] = epi(x[M, K] . W^T).  fp8: x / W are e4m3 bytes with per-row scales xs / wsc.  SwiGLU: W holds
-// 2 * N_out rows ([gate; up]).  res: bf16 residual added in the bf16 epilogue (may alias out).  rms: bf16 RMS
-// prologue (out scaled by 1 / rms(x row); the norm gamma is folded into W).
+// out[M, N_out] = epi(x[M, K] . W^T).  fp8 = 1: x / W are e4m3 bytes with per-row scales xs / wsc; fp8 = 3: x is
+// MX e4m3 with its E8M0 block scales [M][K / 32] in xs (bytes), W e4m3 with row scales wsc.  SwiGLU: W holds
+// 2 * N_out rows ([gate; up]); oq / oe (fp8): the output as MX e4m3 [M][N_out] + E8M0 [M][N_out / 32] (out unused).
+// res: bf16 residual added in the bf16 epilogue (may alias out).  rms: bf16 RMS prologue (out scaled by 1 / rms(x
+// row); the norm gamma is folded into W).
 extern "C" int k8s_pgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs,
                          const float* wsc, int M, int N_out, int K, int epi, int fp8, int cfg, int splits,
-                         int group_m, const void* res, int rms, float eps, hipStream_t stream) {
+                         int group_m, const void* res, int rms, float eps, void* oq, void* oe, hipStream_t stream) {
+  if (fp8 < 0 || fp8 > 3 || fp8 == 2) return -1;
+  const bool mx = fp8 == 3;
+  if (oq != nullptr && (oe == nullptr || !fp8 || epi != PG_SWIGLU || N_out % 32 != 0)) return -7;
+  fp8 = fp8 ? 1 : 0;
   int nwg, nt;
   long long nws;
   if (k8s_pgemm_plan(M, N_out, K, epi, fp8, cfg, splits, &nwg, &nws, &nt) != 0) return -1;
@@ -655,6 +740,9 @@ extern "C" int k8s_pgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.W = static_cast<const uint8_t*>(W);
   a.xs = xs;
   a.wsc = wsc;
+  a.xe = mx ? reinterpret_cast<const uint8_t*>(xs) : nullptr;
+  a.oq = static_cast<uint8_t*>(oq);
+  a.oe = static_cast<uint8_t*>(oe);
   a.kbytes = (uint32_t)kbytes;
   a.M = M;
   a.N_out = N_out;
@@ -671,6 +759,6 @@ extern "C" int k8s_pgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.row_slabs = splits > 1 && g_pg_row_slabs;
   const int rc = fp8 ? pg_cfg<true>(a, cfg, epi, 0, stream) : pg_cfg<false>(a, cfg, epi, rms, stream);
   if (rc != 0 || !a.row_slabs) return rc;
-  return k8s_pgemm_reduce(out, res, ws, splits, M, N_out, K, epi, rms, eps, fp8 ? xs : nullptr, fp8 ? wsc : nullptr,
-                          stream);
+  return k8s_pgemm_reduce(out, res, ws, splits, M, N_out, K, epi, rms, eps, (fp8 && !mx) ? xs : nullptr,
+                          fp8 ? wsc : nullptr, oq, oe, stream);
 }

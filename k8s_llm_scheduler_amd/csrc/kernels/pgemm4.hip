@@ -295,15 +295,18 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
 
 // Split-K combine: out[m, 4 q .. 4 q + 3] = epi(sum over slices of the slabs), slices in order.  One thread per
 // 4 output features of one token; x scaling (RMS) and the residual as in the main kernel's epilogue.
-template <int EPI, bool RMS, bool FP8>
+// MXO (SwiGLU, fp8 weights): the output is MX e4m3 + E8M0 -- the 8 threads of a 32-feature block (adjacent, one
+// wave) take the block's max by shuffles.  FP8 with xs == nullptr: MX activations (their scales were the MFMA's).
+template <int EPI, bool RMS, bool FP8, bool MXO = false>
 __global__ void __launch_bounds__(256) pgemm_reduce_kernel(void* __restrict__ out, const bf16_t* res,
                                                            const float* __restrict__ slab, int splits, int M,
                                                            int N_out, int half_rows, int wrows, int K, float eps,
                                                            const float* __restrict__ xs,
-                                                           const float* __restrict__ wsc) {
+                                                           const float* __restrict__ wsc, uint8_t* __restrict__ oq,
+                                                           uint8_t* __restrict__ oe) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   const int qn = N_out / 4;
-  if (idx >= (long long)M * qn) return;
+  if (idx >= (long long)M * qn) return;   // MXO: M * qn is a multiple of 8, so a block's 8 threads exit together
   const int m = (int)(idx / qn), n0 = (int)(idx - (long long)m * qn) * 4;
   const size_t stride = (size_t)M * wrows;
   f32x4 s = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
@@ -318,7 +321,7 @@ __global__ void __launch_bounds__(256) pgemm_reduce_kernel(void* __restrict__ ou
     for (int k = 0; k < splits; ++k) t += slab[(size_t)splits * stride + (size_t)k * M + m];
     sx = rsqrtf(t / (float)K + eps);
   }
-  if (FP8) sx *= xs[m];
+  if (FP8 && xs != nullptr) sx *= xs[m];
   float v[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -329,11 +332,20 @@ __global__ void __launch_bounds__(256) pgemm_reduce_kernel(void* __restrict__ ou
         up *= wsc[half_rows + n0 + e];
       }
       v[e] = p4_silu(gt) * up;
+      if (MXO) v[e] = bf_round(v[e]);
     } else {
       v[e] = s[e] * sx * (FP8 ? wsc[n0 + e] : 1.f);
     }
   }
-  if (EPI == P4_F32) {
+  if constexpr (MXO) {
+    float amax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, WAVE));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, WAVE));
+    amax = fmaxf(amax, __shfl_xor(amax, 4, WAVE));
+    const uint32_t e = mx_e8m0(amax);
+    *reinterpret_cast<uint32_t*>(oq + (size_t)m * N_out + n0) = mx_pack4(v[0], v[1], v[2], v[3], mx_inv_scale(e));
+    if ((n0 & 31) == 0) oe[(size_t)m * (N_out >> 5) + (n0 >> 5)] = (uint8_t)e;
+  } else if (EPI == P4_F32) {
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + (size_t)m * N_out + n0) = f32x4{v[0], v[1], v[2], v[3]};
   } else {
     if (EPI == P4_BF16 && res != nullptr) {
@@ -398,12 +410,13 @@ int p4_cfg(const P4Args& a, int cfg, int epi, int rms, hipStream_t s) {
   }
 }
 
-template <int EPI, bool RMS, bool FP8>
+template <int EPI, bool RMS, bool FP8, bool MXO = false>
 int reduce_launch(void* out, const void* res, const float* slab, int splits, int M, int N_out, int half_rows,
-                  int wrows, int K, float eps, const float* xs, const float* wsc, hipStream_t s) {
+                  int wrows, int K, float eps, const float* xs, const float* wsc, void* oq, void* oe, hipStream_t s) {
   const long long items = (long long)M * (N_out / 4);
-  hipLaunchKernelGGL((pgemm_reduce_kernel<EPI, RMS, FP8>), dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s,
-                     out, static_cast<const bf16_t*>(res), slab, splits, M, N_out, half_rows, wrows, K, eps, xs, wsc);
+  hipLaunchKernelGGL((pgemm_reduce_kernel<EPI, RMS, FP8, MXO>), dim3((unsigned)((items + 255) / 256)), dim3(256), 0,
+                     s, out, static_cast<const bf16_t*>(res), slab, splits, M, N_out, half_rows, wrows, K, eps, xs,
+                     wsc, static_cast<uint8_t*>(oq), static_cast<uint8_t*>(oe));
   return (int)hipGetLastError();
 }
 }  // namespace
@@ -411,12 +424,19 @@ int reduce_launch(void* out, const void* res, const float* slab, int splits, int
 // Split-K combine of pgemm slabs (also used by the fp8 kernel): slab = [splits][M][wrows] fp32, then (rms)
 // [splits][M] row sums of squares.
 extern "C" int k8s_pgemm_reduce(void* out, const void* res, const float* slab, int splits, int M, int N_out, int K,
-                                int epi, int rms, float eps, const float* xs, const float* wsc, hipStream_t s) {
+                                int epi, int rms, float eps, const float* xs, const float* wsc, void* oq, void* oe,
+                                hipStream_t s) {
   if (splits < 1 || M <= 0 || N_out <= 0 || N_out % 4) return -1;
   const int half = epi == P4_SWIGLU ? N_out : 0, wrows = epi == P4_SWIGLU ? 2 * N_out : N_out;
-  const bool fp8 = xs != nullptr;
+  const bool fp8 = wsc != nullptr;   // (xs == nullptr with fp8: MX activations)
   if (rms && fp8) return -6;
-#define K8S_RED(E, R, F) return reduce_launch<E, R, F>(out, res, slab, splits, M, N_out, half, wrows, K, eps, xs, wsc, s)
+  if (oq != nullptr) {
+    if (!fp8 || epi != P4_SWIGLU || oe == nullptr || N_out % 32) return -7;
+    return reduce_launch<P4_SWIGLU, false, true, true>(out, res, slab, splits, M, N_out, half, wrows, K, eps, xs, wsc,
+                                                      oq, oe, s);
+  }
+#define K8S_RED(E, R, F) \
+  return reduce_launch<E, R, F>(out, res, slab, splits, M, N_out, half, wrows, K, eps, xs, wsc, nullptr, nullptr, s)
   if (fp8) {
     switch (epi) {
       case P4_BF16: K8S_RED(P4_BF16, false, true);
@@ -499,5 +519,6 @@ extern "C" int k8s_pgemm4(void* out, float* slab, const void* x, const void* W, 
   a.eps = eps;
   int rc = p4_cfg(a, cfg, epi, rms, stream);
   if (rc != 0 || splits == 1) return rc;
-  return k8s_pgemm_reduce(out, res, slab, splits, M, N_out, K, epi, rms, eps, nullptr, nullptr, stream);
+  return k8s_pgemm_reduce(out, res, slab, splits, M, N_out, K, epi, rms, eps, nullptr, nullptr, nullptr, nullptr,
+                          stream);
 }

@@ -788,12 +788,18 @@ def pgemm_tiles(cfg: int, M: int, N: int, epi: int) -> int:
 
 def pgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: int = 0, splits: int = 1, group_m: int = 4,
           res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
-          out: Optional[torch.Tensor] = None, act: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, act=None, mx_out: bool = False):
     """Big-tile MFMA GEMM (pgemm.hip): epi(x[M, K] @ w[N, K].T) for prefill-size M.  Same contract as :func:`mgemm`
-    (bf16 or Fp8Weight, SwiGLU with w = [Wg; Wu], residual epilogue, RMS prologue with the gamma folded into w);
-    ``splits`` k-slices per output tile, ``group_m`` m-tiles per tile-order group."""
+    (bf16 or Fp8Weight, SwiGLU with w = [Wg; Wu], residual epilogue, RMS prologue with the gamma folded into w, MX
+    activations / MX SwiGLU output with fp8 weights); ``splits`` k-slices per output tile, ``group_m`` m-tiles per
+    tile-order group."""
+    if isinstance(x, MxAct):
+        act = x
     M, K = x.shape
     fp8 = _is_fp8(w)
+    act_mx = isinstance(act, MxAct)
+    if (act_mx or mx_out) and not fp8:
+        raise ValueError("pgemm: MX activations / output need fp8 weights")
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     if not pgemm_ok(N, K, fp8):
         raise ValueError(f"pgemm: unsupported shape N={N} K={K}")
@@ -802,21 +808,36 @@ def pgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: int = 0, splits: int = 1
     if res is not None and (epi != EPI_BF16 or res.shape != (M, N)):
         raise ValueError("pgemm: residual epilogue needs a bf16 [M, N] residual and the bf16 epilogue")
     nwg, n_ws, n_tk = native().pgemm_plan(M, N, K, epi, int(fp8), cfg, splits)
+    mxo = None
+    if mx_out:
+        if epi != EPI_SWIGLU or N % 32 or res is not None:
+            raise ValueError("pgemm: MX output is the SwiGLU epilogue's (N % 32 == 0)")
+        mxo = MxAct(torch.empty(M, N, dtype=torch.uint8, device=x.device),
+                    torch.empty(M, N // 32, dtype=torch.uint8, device=x.device))
+        out = mxo.q   # (not written as bf16)
     if out is None:
         out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
     ws = torch.empty(n_ws, dtype=F32, device=x.device) if n_ws > 0 else None
     tk = _zeroed_scratch(x.device, "pgemm", 4 * n_tk, 64 * 1024) if n_tk > 0 else 0
     rp = _chk(res, BF16, "res") if res is not None else 0
     rms, eps = (1, float(rms_eps)) if rms_eps is not None else (0, 0.0)
-    if fp8:
+    oq, oe = (mxo.q.data_ptr(), mxo.e.data_ptr()) if mxo is not None else (0, 0)
+    if act_mx:
+        if act.shape != (M, K) or not act.q.is_cuda:
+            raise ValueError(f"pgemm: MX activations {tuple(act.shape)} for x {(M, K)}")
+        native().pgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, act.q.data_ptr(), w.q.data_ptr(),
+                       act.e.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 3, cfg, splits, group_m, rp, 0, 0.0, -1,
+                       oq, oe)
+    elif fp8:
         xq, sx = act if act is not None else quantize_act_fp8(x.contiguous())
         native().pgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, xq.data_ptr(), w.q.data_ptr(),
-                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, splits, group_m, rp, 0, 0.0, -1)
+                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, splits, group_m, rp, 0, 0.0, -1,
+                       oq, oe)
     else:
         native().pgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"),
                        _chk(w, BF16, "w"), 0, 0, M, N, K, epi, 0, cfg, splits, group_m, rp, rms, eps, -1)
     del ws
-    return out
+    return mxo if mxo is not None else out
 
 
 _P4_CFGS: Optional[list] = None

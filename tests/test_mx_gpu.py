@@ -107,3 +107,52 @@ def test_mgemm_swiglu_mx_output_is_the_quantized_bf16_output(act_mx):
                 assert torch.equal(mx.e.cpu(), e), f"cfg {cfg} grid {grid} M {M}"
                 assert torch.equal(mx.q.cpu(), q), f"cfg {cfg} grid {grid} M {M}"
     assert n_cfg >= 2
+
+
+@pytest.mark.parametrize("epi", [ops.EPI_BF16, ops.EPI_F32, ops.EPI_SWIGLU])
+def test_pgemm_mx_every_config(epi):
+    """pgemm's MX mode (prefill rows): every tile configuration, without and with split-K (row slabs + the reduce
+    kernel, and the in-launch last-arriver form), partial tiles, the residual epilogue, against the fp32 oracle."""
+    K, N = 1024, 320
+    rows = 2 * N if epi == ops.EPI_SWIGLU else N
+    w = _weights(rows, K, 13)
+    keep = ops.native().pgemm_set_row_slabs(-1)
+    try:
+        for cfg in range(len(ops.pgemm_configs())):
+            for M in (200, 300):
+                act = ops.quantize_act_mx(_act(M, K, cfg * 10 + M, spread=False).to(DEV))
+                exp = _mx_oracle(act, w, epi)
+                for splits, slabs in ((1, 1), (3, 1), (3, 0)):
+                    ops.native().pgemm_set_row_slabs(slabs)
+                    y = ops.pgemm(act, w, epi, cfg=cfg, splits=splits).float().cpu()
+                    err = (y - exp).abs().max().item()
+                    assert err <= 1e-2 * exp.abs().max().item(), f"cfg {cfg} splits {splits}/{slabs} M {M}: {err}"
+                    if epi == ops.EPI_BF16:
+                        res = ((torch.rand(M, N, device=DEV) * 2 - 1) * 8).to(torch.bfloat16)
+                        want = exp + res.float().cpu()
+                        out = ops.pgemm(act, w, epi, cfg=cfg, splits=splits, res=res, out=res)
+                        err = (out.float().cpu() - want).abs().max().item()
+                        assert err <= 1e-2 * want.abs().max().item(), f"res cfg {cfg} splits {splits} M {M}: {err}"
+    finally:
+        ops.native().pgemm_set_row_slabs(keep)
+
+
+@pytest.mark.parametrize("act_mx", [False, True])
+def test_pgemm_swiglu_mx_output_is_the_quantized_bf16_output(act_mx):
+    K, N = 1024, 256
+    w = _weights(2 * N, K, 17)
+    keep = ops.native().pgemm_set_row_slabs(-1)
+    try:
+        for cfg in range(len(ops.pgemm_configs())):
+            M = 300
+            x = _act(M, K, cfg, spread=False).to(DEV)
+            act = ops.quantize_act_mx(x) if act_mx else ops.quantize_act_fp8(x)
+            for splits, slabs in ((1, 1), (3, 1), (3, 0)):
+                ops.native().pgemm_set_row_slabs(slabs)
+                y = ops.pgemm(x, w, ops.EPI_SWIGLU, cfg=cfg, splits=splits, act=act)
+                mx = ops.pgemm(x, w, ops.EPI_SWIGLU, cfg=cfg, splits=splits, act=act, mx_out=True)
+                q, e = ref.quantize_mx(y.cpu())
+                assert torch.equal(mx.e.cpu(), e), f"cfg {cfg} splits {splits}/{slabs}"
+                assert torch.equal(mx.q.cpu(), q), f"cfg {cfg} splits {splits}/{slabs}"
+    finally:
+        ops.native().pgemm_set_row_slabs(keep)
