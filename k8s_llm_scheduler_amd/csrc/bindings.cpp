@@ -64,7 +64,7 @@ int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M,
 int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const void* qkv, const float* cos_sin,
                                void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
                                float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax, int part,
-                               hipStream_t s);
+                               void* oq, void* oe, hipStream_t s);
 long long k8s_decode_split_workspace(int B, int nq, int nkv, int pmax);
 int k8s_decode_persist_plan(int M, int H, int nq, int nkv, int I, int pmax, int* gl, int* grid);
 int k8s_decode_persist(const void* layers, int L, const void* x0, void* xout, int M, int H, int nq, int nkv, int I,
@@ -253,11 +253,16 @@ PYBIND11_MODULE(K8S_MODULE_NAME, m) {
   });
   m.def("decode_attention_fused", [](uintptr_t out, uintptr_t pacc, uintptr_t pml, uintptr_t qkv, uintptr_t cos_sin,
                                      uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx, float scale, int B, int nq,
-                                     int nkv, int D, int bs, int max_blocks, int pmax, int part, int64_t s) {
+                                     int nkv, int D, int bs, int max_blocks, int pmax, int part, int64_t s,
+                                     uintptr_t oq, uintptr_t oe) {
     check(k8s_decode_attention_fused(P(out), P(pacc), P(pml), P(qkv), P<float>(cos_sin), P(kc), P(vc), P<int>(bt),
-                                     P<int>(ctx), scale, B, nq, nkv, D, bs, max_blocks, pmax, part, S(s)),
+                                     P<int>(ctx), scale, B, nq, nkv, D, bs, max_blocks, pmax, part, P(oq), P(oe),
+                                     S(s)),
           "decode_attention_fused");
-  });
+  }, py::arg("out"), py::arg("pacc"), py::arg("pml"), py::arg("qkv"), py::arg("cos_sin"), py::arg("kc"),
+     py::arg("vc"), py::arg("bt"), py::arg("ctx"), py::arg("scale"), py::arg("B"), py::arg("nq"), py::arg("nkv"),
+     py::arg("D"), py::arg("bs"), py::arg("max_blocks"), py::arg("pmax"), py::arg("part"), py::arg("s"),
+     py::arg("oq") = 0, py::arg("oe") = 0);
   // layer-persistent decode (decode_persist.hip): plan -> (rc, granules per (layer, row), grid); rc < 0: not taken
   m.def("decode_persist_plan", [](int M, int H, int nq, int nkv, int I, int pmax) {
     int gl = 0, grid = 0;

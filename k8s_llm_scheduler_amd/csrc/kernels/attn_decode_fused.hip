@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_acc, float* __restrict__ part_ml, const bf16_t* __restrict__ qkv,
     const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ context_lens, float scale, int block_size,
-    int max_blocks, int nkv, int pmax) {
+    int max_blocks, int nkv, int pmax, uint8_t* __restrict__ oq, uint8_t* __restrict__ oe) {
   static_assert(D == 128 && G <= 16, "head_dim 128, group <= 16");
   static_assert(PART / NW == 64, "64 tokens per wave");
   constexpr int NT = NW * WAVE;
@@ -316,7 +316,11 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
     const int h = kvh * G + g;
     const float sacc_v = red[g][d];
     if (single) {
-      out[((size_t)b * nq + h) * D + d] = f2bf(sacc_v / L);
+      if (oq != nullptr) {   // MX output: the 32 lanes of (head, d / 32) form one half-wave (NT, D: multiples of 32)
+        mx_store_lane(oq, oe, b, h * D + d, nq * D, gridDim.z, bf_round(sacc_v / L));
+      } else {
+        out[((size_t)b * nq + h) * D + d] = f2bf(sacc_v / L);
+      }
     } else {
       float Mx = -INFINITY;
 #pragma unroll
@@ -332,7 +336,7 @@ template <int D>
 __global__ void __launch_bounds__(D) decode_merge_kernel(bf16_t* __restrict__ out, const float* __restrict__ part_acc,
                                                          const float* __restrict__ part_ml,
                                                          const int* __restrict__ context_lens, int part, int pmax,
-                                                         int nq) {
+                                                         int nq, uint8_t* __restrict__ oq, uint8_t* __restrict__ oe) {
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int ctx = context_lens[b];
   if (ctx <= part) return;  // single-partition rows were finished by the attention kernel
@@ -346,7 +350,8 @@ __global__ void __launch_bounds__(D) decode_merge_kernel(bf16_t* __restrict__ ou
     num += w * part_acc[(base + q) * D + d];
     den += w * part_ml[(base + q) * 2 + 1];
   }
-  out[((size_t)b * nq + h) * D + d] = f2bf(num / den);
+  if (oq != nullptr) mx_store_lane(oq, oe, b, h * D + d, nq * D, gridDim.y, bf_round(num / den));
+  else out[((size_t)b * nq + h) * D + d] = f2bf(num / den);
 }
 
 }  // namespace k8sllm
@@ -359,10 +364,13 @@ K8S_CHECK_UNIT(attn_decode_fused)
 // part: context tokens per workgroup, 1024 (16 waves, ~137 KB of LDS: one workgroup per CU) or 512 (8 waves,
 // ~73 KB: two per CU -- for batches whose (sequence, kv head) pairs outnumber the CUs, where the 16-wave
 // workgroups would run in two rounds).  pmax = ceil(max context / part).
+// oq / oe (optional): the output as MX e4m3 [B][nq * D] + E8M0 scales (common.h mx_scale_off layout) (K16: the fp8 O projection's input
+// quantized by its producer) instead of bf16.
 extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const void* qkv,
                                           const float* cos_sin, void* k_cache, void* v_cache, const int* block_tables,
                                           const int* context_lens, float scale, int B, int nq, int nkv, int D,
-                                          int block_size, int max_blocks, int pmax, int part, hipStream_t stream) {
+                                          int block_size, int max_blocks, int pmax, int part, void* oq, void* oe,
+                                          hipStream_t stream) {
   if (B <= 0) return 0;
   if (D != 128 || nq % nkv != 0) return -1;
   if (block_size != 16) return -4;  // the speculative K loads assume one 16-token block per tile
@@ -373,7 +381,8 @@ extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_
 #define L(GG, PP, WW)                                                                                       \
   decode_fused_kernel<128, GG, PP, WW><<<grid, WW * 64, 0, stream>>>(                                        \
       (bf16_t*)out, (float*)part_acc, (float*)part_ml, (const bf16_t*)qkv, cos_sin, (bf16_t*)k_cache,       \
-      (bf16_t*)v_cache, block_tables, context_lens, scale, block_size, max_blocks, nkv, pmax)
+      (bf16_t*)v_cache, block_tables, context_lens, scale, block_size, max_blocks, nkv, pmax, (uint8_t*)oq,   \
+      (uint8_t*)oe)
 #define LG(PP, WW)                 \
   switch (G) {                     \
     case 1: L(1, PP, WW); break;   \
@@ -392,6 +401,7 @@ extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_
 #undef L
   if (pmax > 1)
     decode_merge_kernel<128><<<dim3(nq, B), 128, 0, stream>>>((bf16_t*)out, (const float*)part_acc,
-                                                              (const float*)part_ml, context_lens, part, pmax, nq);
+                                                              (const float*)part_ml, context_lens, part, pmax, nq,
+                                                              (uint8_t*)oq, (uint8_t*)oe);
   return (int)hipGetLastError();
 }

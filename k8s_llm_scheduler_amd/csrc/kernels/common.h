@@ -58,6 +58,23 @@ __device__ __forceinline__ uint32_t mx_pack4(float a, float b, float c, float d,
 }
 // bf16 rounding of an fp32 value (MX producers quantize the bf16 value the bf16 path would have stored)
 __device__ __forceinline__ float bf_round(float f) { return bf2f(f2bf(f)); }
+// Byte offset of the E8M0 scale of 32-value block kb of row m in an [M][K] MX tensor.  Layout [K / 128][M][4]: the
+// four scales of a 128-value k-tile of a row form one dword, and the dwords of consecutive rows are adjacent -- so a
+// GEMM stages one k-tile's scales for a run of rows as one contiguous LDS-DMA (one cache line per 32 rows, not one
+// per row).
+__device__ __forceinline__ size_t mx_scale_off(size_t m, int kb, int M) {
+  return ((size_t)(kb >> 2) * (size_t)M + m) * 4 + (size_t)(kb & 3);
+}
+// MX store of one value per lane, the 32 lanes of an aligned half-wave holding one block (row m, columns col..,
+// col of the half-wave's first lane a multiple of 32): shuffle max, then one e4m3 byte per lane and the block's E8M0.
+__device__ __forceinline__ void mx_store_lane(uint8_t* oq, uint8_t* oe, size_t m, int col, int K, int M, float v) {
+  float amax = fabsf(v);
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  const uint32_t e = mx_e8m0(amax);
+  oq[m * (size_t)K + col] = (uint8_t)(mx_pack4(v, 0.f, 0.f, 0.f, mx_inv_scale(e)) & 0xffu);
+  if ((col & 31) == 0) oe[mx_scale_off(m, col >> 5, M)] = (uint8_t)e;
+}
 
 // Block-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats of LDS.
 __device__ __forceinline__ float block_sum(float v, float* red) {

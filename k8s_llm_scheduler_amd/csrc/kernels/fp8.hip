@@ -144,9 +144,11 @@ __global__ void __launch_bounds__(256) quantize_act_fp8_kernel(uint8_t* __restri
 // themselves (no per-row absmax pass).  This kernel is the stand-alone form (tests, and producers without a fused
 // form): one thread per block.
 __global__ void __launch_bounds__(256) quantize_act_mx_kernel(uint8_t* __restrict__ q, uint8_t* __restrict__ e8,
-                                                              const bf16_t* __restrict__ x, long long blocks) {
+                                                              const bf16_t* __restrict__ x, long long blocks, int M,
+                                                              int KB) {
   const long long b = (long long)blockIdx.x * 256 + threadIdx.x;
   if (b >= blocks) return;
+  const int m = (int)(b / KB), kb = (int)(b - (long long)m * KB);
   const u32x4* src = reinterpret_cast<const u32x4*>(x + b * 32);
   float v[32];
 #pragma unroll
@@ -171,20 +173,20 @@ __global__ void __launch_bounds__(256) quantize_act_mx_kernel(uint8_t* __restric
   }
   reinterpret_cast<u32x4*>(q + b * 32)[0] = o0;
   reinterpret_cast<u32x4*>(q + b * 32)[1] = o1;
-  e8[b] = (uint8_t)e;
+  e8[mx_scale_off(m, kb, M)] = (uint8_t)e;
 }
 
 }  // namespace k8sllm
 
 using namespace k8sllm;
 
-// x bf16 [T][K] -> q e4m3 [T][K] + e8 E8M0 [T][K / 32] (K % 32 == 0).
+// x bf16 [T][K] -> q e4m3 [T][K] + e8 E8M0 scales (layout [K / 128][T][4], common.h mx_scale_off; K % 128 == 0).
 extern "C" int k8s_quantize_act_mx(void* q, void* e8, const void* x, int T, int K, hipStream_t s) {
   if (T <= 0) return 0;
-  if (K <= 0 || K % 32 != 0) return -1;
+  if (K <= 0 || K % 128 != 0) return -1;
   const long long blocks = (long long)T * (K / 32);
   quantize_act_mx_kernel<<<(unsigned)((blocks + 255) / 256), 256, 0, s>>>(
-      static_cast<uint8_t*>(q), static_cast<uint8_t*>(e8), static_cast<const bf16_t*>(x), blocks);
+      static_cast<uint8_t*>(q), static_cast<uint8_t*>(e8), static_cast<const bf16_t*>(x), blocks, T, K / 32);
   return (int)hipGetLastError();
 }
 

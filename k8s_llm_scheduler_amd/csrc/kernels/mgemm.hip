@@ -38,8 +38,9 @@
 //    of the non-scaled fp8 form, and no per-token absmax pass anywhere.
 //  * MX output (SwiGLU epilogue, mx_out): the h = silu(g) * u values of 32 consecutive features of a row sit in
 //    the lanes of one 16-lane column group of two adjacent fragments (the configurations whose per-wave feature
-//    span is a multiple of 32): a 4-step shuffle max gives the block's E8M0 scale and every lane stores its e4m3
-//    bytes -- the down projection's input is produced already quantized.
+//    span is a multiple of 32), or of one fragment in each of two neighbouring waves (16 features per wave: the
+//    row absmax goes through LDS, one barrier): a shuffle max gives the block's E8M0 scale and every lane stores
+//    its e4m3 bytes -- the down projection's input is produced already quantized.
 #include "common.h"
 
 namespace k8sllm {
@@ -85,9 +86,9 @@ struct MgArgs {
   const uint8_t* W;      // [rows][K] bf16 or e4m3
   const float* xs;       // fp8 activations: [M] per-token activation scales
   const float* wsc;      // fp8: [rows] per-row weight scales
-  const uint8_t* xe;     // MX activations: [M][K / 32] E8M0 block scales
+  const uint8_t* xe;     // MX activations: E8M0 block scales, [K / 128][M] dwords (mx_scale_off)
   uint8_t* oq;           // MX output (SwiGLU): e4m3 [M][N_out] ...
-  uint8_t* oe;           // ... and its E8M0 block scales [M][N_out / 32] (bf16 out not written)
+  uint8_t* oe;           // ... and its E8M0 block scales, mx_scale_off layout (bf16 out not written)
   long long kbytes;      // bytes per row of W (and of x, except W8: x rows are bf16, xkbytes)
   long long xkbytes;     // bytes per row of x
   long long total;       // tiles * T work items (one item = one tile x one 128-byte k-step)
@@ -121,7 +122,8 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert(RB == 64 || RB == 128 || RB == 256 || RB == 512, "row bytes per k-step");
   static_assert(!(FP8 && W8), "W8: fp8 weights with bf16 activations");
   static_assert(!MX || FP8, "MX: e4m3 activations with E8M0 block scales");
-  static_assert(!MXO || (EPI == MG_SWIGLU && (FN / 2) % 2 == 0), "MX output: SwiGLU, 32-feature spans per wave");
+  static_assert(!MXO || (EPI == MG_SWIGLU && ((FN / 2) % 2 == 0 || (FN == 2 && WN % 2 == 0 && WK == 1))),
+                "MX output: SwiGLU, 32-feature spans per wave or per wave pair");
   constexpr int XRB = W8 ? 2 * RB : RB;              // x row bytes per k-step (W8: RB bf16 values)
   constexpr int CPR = RB / 16, XCPR = XRB / 16;      // 16-byte chunks per staged W / x row
   constexpr int KS = (FP8 || W8) ? RB / 32 : RB / 64;   // k32 MFMA steps per k-step (RB = 64: one)
@@ -181,7 +183,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     // lane-linear LDS destination); the host checks that every operand spans < 4 GiB
     const uint8_t* wseg = a.W + (long long)kb * RB;
     const uint8_t* xseg = a.x + (long long)kb * XRB;
-    const uint8_t* eseg = MX ? a.xe + (long long)kb * (RB / 32) : nullptr;
+    const uint8_t* eseg = MX ? a.xe + (long long)kb * KS4 * a.M * 4 : nullptr;   // [K / 128][M] scale dwords
     uint32_t woff[WI], xoff[XI], soff[SI > 0 ? SI : 1];
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
@@ -206,7 +208,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     for (int i = 0; i < SI; ++i) {   // MX: the 4 scale bytes of (row r, subtile d) of a k-step
       const int p = wid * SCH + min(i * 64 + lane, SCH - 1);
       const int r = p / KS4, d = p % KS4;
-      soff[i] = (uint32_t)min(mt * BM + r, a.M - 1) * (uint32_t)(a.xkbytes >> 5) + (uint32_t)(d * 4);
+      soff[i] = ((uint32_t)d * (uint32_t)a.M + (uint32_t)min(mt * BM + r, a.M - 1)) * 4u;
     }
 
     auto issue = [&](int t, int stage) {
@@ -228,7 +230,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
               0);
       }
       if constexpr (MX) {
-        const uint8_t* eb = eseg + (long long)t * (RB / 32);
+        const uint8_t* eb = eseg + (long long)t * KS4 * a.M * 4;
 #pragma unroll
         for (int i = 0; i < SI; ++i) {
           if (SCH % 64 == 0 || i * 64 + lane < SCH)
@@ -473,6 +475,43 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     if (do_rms) mg_barrier();   // row totals visible to every wave's epilogue
     if (wk != 0) continue;
 
+    if constexpr (MXO && FN == 2) {
+      // MX output, 16 SwiGLU features per wave: a 32-feature block is waves wn and wn ^ 1 (same rows); each wave
+      // parks its rows' absmax in rss (free in fp8 modes), one barrier, then both take the pair's max
+      float v[FM][4], am[FM];
+      const int n0 = nt * (BN / 2) + wn * 16 + 4 * g;
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int m = min(mt * BM + wm * (BM / WM) + j * 16 + li, a.M - 1);
+        const float sxx = MX ? 1.f : a.xs[m];
+        am[j] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[j][i] = 0.f;
+          if (n0 < a.N_out) {
+            const float gt = acc[0][j][i] * sxx * a.wsc[n0 + i], up = acc[1][j][i] * sxx * a.wsc[a.half_rows + n0 + i];
+            v[j][i] = bf_round(mg_silu(gt) * up);
+          }
+          am[j] = fmaxf(am[j], fabsf(v[j][i]));
+        }
+        am[j] = fmaxf(am[j], __shfl_xor(am[j], 16, WAVE));
+        am[j] = fmaxf(am[j], __shfl_xor(am[j], 32, WAVE));
+        rss[wn * BM + wm * (BM / WM) + j * 16 + li] = am[j];
+      }
+      mg_barrier();
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int m = mt * BM + wm * (BM / WM) + j * 16 + li;
+        if (m >= a.M || n0 >= a.N_out) continue;   // N_out % 32 == 0: a wave pair is in or out together
+        const float amax = fmaxf(am[j], rss[(wn ^ 1) * BM + wm * (BM / WM) + j * 16 + li]);
+        const uint32_t e = mx_e8m0(amax);
+        *reinterpret_cast<uint32_t*>(a.oq + (long long)m * a.N_out + n0) =
+            mx_pack4(v[j][0], v[j][1], v[j][2], v[j][3], mx_inv_scale(e));
+        if (g == 0 && (wn & 1) == 0) a.oe[mx_scale_off(m, n0 >> 5, a.M)] = (uint8_t)e;
+      }
+      continue;
+    }
+
     // ---- epilogue: lane holds out[m = brow][n = 4 g + i], i < 4, of every fragment pair
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
@@ -480,7 +519,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
       if (m >= a.M) continue;
       float sx = (FP8 && !MX) ? a.xs[m] : 1.f;
       if (do_rms) sx = rsqrtf(rss[wm * (BM / WM) + j * 16 + li] / (float)(a.xkbytes >> 1) + a.eps);
-      if constexpr (MXO) {   // 32-feature blocks = fragment pairs (2 b, 2 b + 1); the block's lanes share li
+      if constexpr (MXO && FN != 2) {   // 32-feature blocks = fragment pairs (2 b, 2 b + 1); the block's lanes share li
 #pragma unroll
         for (int b = 0; b < FN / 4; ++b) {
           const int nb = nt * (BN / 2) + wn * (BN / 2 / WN) + b * 32;   // first feature of the block
@@ -505,7 +544,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
           uint8_t* orow = a.oq + (long long)m * a.N_out;
           *reinterpret_cast<uint32_t*>(orow + nb + 4 * g) = mx_pack4(v[0], v[1], v[2], v[3], inv);
           *reinterpret_cast<uint32_t*>(orow + nb + 16 + 4 * g) = mx_pack4(v[4], v[5], v[6], v[7], inv);
-          if (g == 0) a.oe[(long long)m * (a.N_out >> 5) + (nb >> 5)] = (uint8_t)e;
+          if (g == 0) a.oe[mx_scale_off(m, nb >> 5, a.M)] = (uint8_t)e;
         }
       } else if constexpr (EPI == MG_SWIGLU) {
 #pragma unroll
@@ -621,7 +660,10 @@ constexpr bool mg_mx_cfg(int c) {
          mg_lds_bytes(kMgCfgs[c], 3) <= 160 * 1024;
 }
 // SwiGLU with MX output: every wave's feature span is whole 32-feature blocks
-constexpr bool mg_mxo_cfg(int c) { return (kMgCfgs[c].bn / (kMgCfgs[c].wn * 16)) % 4 == 0; }
+constexpr bool mg_mxo_cfg(int c) {
+  return (kMgCfgs[c].bn / (kMgCfgs[c].wn * 16)) % 4 == 0 ||
+         (kMgCfgs[c].bn / (kMgCfgs[c].wn * 16) == 2 && kMgCfgs[c].wn % 2 == 0 && kMgCfgs[c].wk == 1);
+}
 
 template <int C, int EPI, bool FP8, bool W8, bool MX, bool MXO>
 int mg_launch(const MgArgs& a, int grid, hipStream_t s) {
@@ -739,8 +781,8 @@ extern "C" int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, in
 // out[M, N_out] = epi(x[M, K] . W^T) with `nwg` workgroups streaming equal shares of the
 // (tile, k-step) items.  fp8 = 1: x / W are e4m3 bytes with per-row scales xs / wsc; fp8 = 2 (W8): W is e4m3
 // with row scales wsc, x is bf16 (no activation scales; the RMS prologue is allowed); fp8 = 3 (MX): W e4m3 with row
-// scales wsc, x MX e4m3 with its E8M0 block scales [M][K / 32] in xs (bytes).  oq / oe (fp8 = 1 or 3, SwiGLU): the
-// output is written as MX e4m3 [M][N_out] + E8M0 [M][N_out / 32] instead of bf16 (out unused).
+// scales wsc, x MX e4m3 with its E8M0 block scales in xs (bytes, mx_scale_off layout).  oq / oe (fp8 = 1 or 3, SwiGLU): the
+// output is written as MX e4m3 [M][N_out] + E8M0 (mx_scale_off layout) instead of bf16 (out unused).
 // SwiGLU: W holds 2 * N_out rows ([gate; up]); out has N_out columns.
 extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs,
                          const float* wsc, int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax,
@@ -749,7 +791,7 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   if (N_out % 4 != 0) return -1;
   if (fp8 < 0 || fp8 > 3) return -1;
   const bool w8 = fp8 == 2, mx = fp8 == 3, mxo = oq != nullptr;
-  if (mxo && (oe == nullptr || epi != MG_SWIGLU || (fp8 != 1 && fp8 != 3) || N_out % 32 != 0 || !mg_mxo_valid(cfg)))
+  if (mxo && (oe == nullptr || epi != MG_SWIGLU || (fp8 != 1 && fp8 != 3) || N_out % 128 != 0 || !mg_mxo_valid(cfg)))
     return -7;
   if (mx && (K % 128 != 0 || !mg_mx_valid(cfg))) return -7;
   const long long kbytes = (long long)K * (fp8 ? 1 : 2), xkbytes = (long long)K * ((fp8 == 1 || fp8 == 3) ? 1 : 2);

@@ -121,8 +121,8 @@ struct PgArgs {
   const uint8_t* W;      // [rows][K] bf16 or e4m3
   const float* xs;       // fp8: [M] per-token scales
   const float* wsc;      // fp8: [rows] per-row scales
-  const uint8_t* xe;     // MX activations: [M][K / 32] E8M0 block scales
-  uint8_t* oq;           // MX output (SwiGLU): e4m3 [M][N_out] + E8M0 [M][N_out / 32]
+  const uint8_t* xe;     // MX activations: E8M0 block scales, [K / 128][M] dwords (mx_scale_off)
+  uint8_t* oq;           // MX output (SwiGLU): e4m3 [M][N_out] + E8M0 (mx_scale_off layout)
   uint8_t* oe;
   uint32_t kbytes;       // bytes per row of x and W
   int M, N_out, half_rows, K;
@@ -179,8 +179,8 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
 
   // ---- per-thread DMA sources (byte offsets from the operand bases; the host checks < 4 GiB)
   uint32_t oq0[GQ], oq1[GQ], op0[GP], op1[GP], osc = 0;
-  if constexpr (MX)   // token row wid * SCH + lane of the tile, k-tile kt0 (4 scale bytes = the k-tile's 4 blocks)
-    osc = (uint32_t)min(mt * BQ + wid * SCH + min(lane, SCH - 1), a.M - 1) * (a.kbytes >> 5) + (uint32_t)(kt0 * 4);
+  if constexpr (MX)   // token row wid * SCH + lane of the tile, k-tile kt0: [K / 128][M] scale dwords
+    osc = ((uint32_t)kt0 * (uint32_t)a.M + (uint32_t)min(mt * BQ + wid * SCH + min(lane, SCH - 1), a.M - 1)) * 4u;
 #pragma unroll
   for (int i = 0; i < GQ; ++i) {
     const int p = i * 512 + tid, r = p >> 3, c = (p & 7) ^ ((r >> 1) & 7);
@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
       dma(a.x + kb, oq0, dst, std::integral_constant<int, GQ>{});
       if constexpr (MX) {
         if (lane < SCH)
-          __builtin_amdgcn_global_load_lds(a.xe + osc + u * 4,
+          __builtin_amdgcn_global_load_lds(a.xe + (osc + (uint32_t)u * (uint32_t)a.M * 4u),   // saddr + 32-bit voffset
                                            (__attribute__((address_space(3))) void*)(lds + (u & 1) * STAGE + OFF_SC +
                                                                                      wid * SCH * 4),
                                            4, 0, 0);
@@ -260,9 +260,11 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   float ss[FQ];
 #pragma unroll
   for (int f = 0; f < FQ; ++f) ss[f] = 0.f;
-  int sc[2][FQ];   // MX: this lane's B scale (block g of its token row) per x fragment of the current k-tile
-#pragma unroll
-  for (int f = 0; f < FQ; ++f) sc[0][f] = sc[1][f] = 0x7f7f7f7f;
+  // MX: this lane's B scales (block g of its token row) for the 2 * FQ x fragments of the current k-tile, packed
+  // one byte each into ONE register (byte h * FQ + f; the MFMA's op_sel picks it) -- the kernel sits at the VGPR
+  // limit, and four separate registers spilled inside the main loop (scratch loads there drain the LDS-DMA ring)
+  static_assert(!MX || FQ <= 2, "MX: 2 * FQ scale bytes per register");
+  int scp = 0x7f7f7f7f;
 
   auto read_frags = [&](const char* rb, frag_t* d0, frag_t* d1, auto NF_) {
     constexpr int NF = decltype(NF_)::value;
@@ -292,8 +294,12 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
         for (int fq = 0; fq < FQ; ++fq) {
           f32x4& c = acc[ah * FP + fp][bh * FQ + fq];
           if constexpr (FP8) {
-            c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(Ar[0][fp], bh ? B1r[0][fq] : B0r[0][fq], c, 0, 0, 0,
-                                                                 0x7f7f7f7f, 0, MX ? sc[bh][fq] : 0x7f7f7f7f);
+            if (fq == 0)
+              c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(Ar[0][fp], bh ? B1r[0][fq] : B0r[0][fq], c, 0, 0, 0,
+                                                                   0x7f7f7f7f, bh * FQ, scp);
+            else
+              c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(Ar[0][fp], bh ? B1r[0][fq] : B0r[0][fq], c, 0, 0, 0,
+                                                                   0x7f7f7f7f, (bh * FQ + 1) & 3, scp);
           } else {
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ar[kk][fp], bh ? B1r[kk][fq] : B0r[kk][fq], c, 0, 0, 0);
           }
@@ -328,7 +334,10 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int f = 0; f < FQ; ++f) sc[h][f] = scl[wc * (BQ / 4) + h * (BQ / 8) + f * 16 + li] >> (8 * g);
+          for (int f = 0; f < FQ; ++f) {
+            const uint32_t byte = ((uint32_t)scl[wc * (BQ / 4) + h * (BQ / 8) + f * 16 + li] >> (8 * g)) & 0xffu;
+            scp = (int)(((uint32_t)scp & ~(0xffu << (8 * (h * FQ + f)))) | (byte << (8 * (h * FQ + f))));
+          }
       }
       if (t + 1 < n) issue(Y3{}, t + 1);
     } else if constexpr (j == 1) {
@@ -527,7 +536,7 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
         uint8_t* orow = a.oq + (size_t)m * a.N_out;
         *reinterpret_cast<uint32_t*>(orow + nb + 4 * g) = mx_pack4(v[0], v[1], v[2], v[3], inv);
         *reinterpret_cast<uint32_t*>(orow + nb + 16 + 4 * g) = mx_pack4(v[4], v[5], v[6], v[7], inv);
-        if (g == 0) a.oe[(size_t)m * (a.N_out >> 5) + (nb >> 5)] = (uint8_t)e;
+        if (g == 0) a.oe[mx_scale_off(m, nb >> 5, a.M)] = (uint8_t)e;
       }
     } else if constexpr (EPI == PG_SWIGLU) {
 #pragma unroll
@@ -709,8 +718,8 @@ extern "C" int k8s_pgemm_plan(int M, int N_out, int K, int epi, int fp8, int cfg
 }
 
 // out[M, N_out] = epi(x[M, K] . W^T).  fp8 = 1: x / W are e4m3 bytes with per-row scales xs / wsc; fp8 = 3: x is
-// MX e4m3 with its E8M0 block scales [M][K / 32] in xs (bytes), W e4m3 with row scales wsc.  SwiGLU: W holds
-// 2 * N_out rows ([gate; up]); oq / oe (fp8): the output as MX e4m3 [M][N_out] + E8M0 [M][N_out / 32] (out unused).
+// MX e4m3 with its E8M0 block scales in xs (bytes, mx_scale_off layout), W e4m3 with row scales wsc.  SwiGLU: W holds
+// 2 * N_out rows ([gate; up]); oq / oe (fp8): the output as MX e4m3 [M][N_out] + E8M0 (mx_scale_off layout) (out unused).
 // res: bf16 residual added in the bf16 epilogue (may alias out).  rms: bf16 RMS prologue (out scaled by 1 / rms(x
 // row); the norm gamma is folded into W).
 extern "C" int k8s_pgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs,
@@ -718,7 +727,7 @@ extern "C" int k8s_pgemm(void* out, float* ws, unsigned* tickets, const void* x,
                          int group_m, const void* res, int rms, float eps, void* oq, void* oe, hipStream_t stream) {
   if (fp8 < 0 || fp8 > 3 || fp8 == 2) return -1;
   const bool mx = fp8 == 3;
-  if (oq != nullptr && (oe == nullptr || !fp8 || epi != PG_SWIGLU || N_out % 32 != 0)) return -7;
+  if (oq != nullptr && (oe == nullptr || !fp8 || epi != PG_SWIGLU || N_out % 128 != 0)) return -7;
   fp8 = fp8 ? 1 : 0;
   int nwg, nt;
   long long nws;

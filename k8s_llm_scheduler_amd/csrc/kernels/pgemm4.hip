@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(256) pgemm_reduce_kernel(void* __restrict__ ou
     amax = fmaxf(amax, __shfl_xor(amax, 4, WAVE));
     const uint32_t e = mx_e8m0(amax);
     *reinterpret_cast<uint32_t*>(oq + (size_t)m * N_out + n0) = mx_pack4(v[0], v[1], v[2], v[3], mx_inv_scale(e));
-    if ((n0 & 31) == 0) oe[(size_t)m * (N_out >> 5) + (n0 >> 5)] = (uint8_t)e;
+    if ((n0 & 31) == 0) oe[mx_scale_off(m, n0 >> 5, M)] = (uint8_t)e;
   } else if (EPI == P4_F32) {
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + (size_t)m * N_out + n0) = f32x4{v[0], v[1], v[2], v[3]};
   } else {
@@ -431,7 +431,7 @@ extern "C" int k8s_pgemm_reduce(void* out, const void* res, const float* slab, i
   const bool fp8 = wsc != nullptr;   // (xs == nullptr with fp8: MX activations)
   if (rms && fp8) return -6;
   if (oq != nullptr) {
-    if (!fp8 || epi != P4_SWIGLU || oe == nullptr || N_out % 32) return -7;
+    if (!fp8 || epi != P4_SWIGLU || oe == nullptr || N_out % 128) return -7;
     return reduce_launch<P4_SWIGLU, false, true, true>(out, res, slab, splits, M, N_out, half, wrows, K, eps, xs, wsc,
                                                       oq, oe, s);
   }

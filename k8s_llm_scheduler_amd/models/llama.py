@@ -226,7 +226,7 @@ class LlamaModel:
                 o = ops.linear(a, w.wo)
                 self.tp.all_reduce_(o, residual=r)     # o = r + attention branch
                 r = o
-            g = ops.linear_rms(r, w.wgu, eps, ops.EPI_SWIGLU)
+            g = ops.linear_rms(r, w.wgu, eps, ops.EPI_SWIGLU, mx_consumer=w.wdown)   # fp8 GEMM rows: MX e4m3 (K16)
             if tp1:
                 r = ops.linear_residual(g, w.wdown, r)
             else:
@@ -443,11 +443,14 @@ class LlamaModel:
             return self._forward_decode_fused(tokens, context_lens, block_tables, max_context)
         kv = self.kv_cache
         fused_attn = self.device.type == "cuda" and self.fused_decode   # batched decode (B > 8)
+        # fp8 GEMM rows: the attention kernel writes the O projection's input as MX e4m3 (K16)
+        mx = fused_attn and ops.mx_rows(B, self.layers[0].wo)
 
-        def attn(l: int, qkv: torch.Tensor) -> torch.Tensor:
+        def attn(l: int, qkv: torch.Tensor):
             if fused_attn:
                 return ops.decode_attention_fused(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
-                                                  self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
+                                                  self.scale, self.block_size, max_context, self.nq, self.nkv, self.D,
+                                                  mx=mx)
             q = ops.rope_kv_write(qkv, self.cos_sin, kv[l, 0], kv[l, 1], self.nq, self.nkv, self.D,
                                   context_lens=context_lens, block_tables=block_tables, block_size=self.block_size)
             a = ops.paged_decode_attention(q, kv[l, 0], kv[l, 1], block_tables, context_lens, self.scale,

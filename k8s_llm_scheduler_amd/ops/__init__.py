@@ -184,8 +184,10 @@ def quantize_act_fp8(x: torch.Tensor, rms_eps: Optional[float] = None) -> Tuple[
 
 
 class MxAct:
-    """OCP MX e4m3 activations (K16 block-scaled; fp8.hip): ``q`` [M, K] uint8 e4m3 bit patterns, ``e`` [M, K / 32]
-    uint8 E8M0 exponents, x[m, k] ~= e4m3(q[m, k]) * 2^(e[m, k // 32] - 127).  The O and down projections of the fp8
+    """OCP MX e4m3 activations (K16 block-scaled; fp8.hip): ``q`` [M, K] uint8 e4m3 bit patterns, ``e`` the uint8
+    E8M0 exponents in the kernels' layout [K / 128, M, 4] (common.h mx_scale_off: a k-tile's scales of consecutive
+    rows are adjacent); :meth:`blocks` gives them as [M, K / 32], x[m, k] ~= e4m3(q[m, k]) * 2^(blocks[m, k // 32] -
+    127).  The O and down projections of the fp8
     GEMM rows take their input in this form: the SwiGLU epilogue (mgemm / pgemm ``mx_out``) and the attention
     output write it, and the GEMMs feed the E8M0 bytes to the block-scaled MFMA's scale operand (mgemm / pgemm MX
     mode) -- no per-token absmax pass, no quantize launch between a producer and its consumer."""
@@ -193,10 +195,19 @@ class MxAct:
     __slots__ = ("q", "e")
 
     def __init__(self, q: torch.Tensor, e: torch.Tensor):
-        if (q.dtype != torch.uint8 or e.dtype != torch.uint8 or q.dim() != 2 or q.shape[1] % 32
-                or e.shape != (q.shape[0], q.shape[1] // 32)):
-            raise ValueError("MxAct needs q [M, K] uint8 (K % 32 == 0) and e [M, K / 32] uint8")
+        if (q.dtype != torch.uint8 or e.dtype != torch.uint8 or q.dim() != 2 or q.shape[1] % 128
+                or e.shape != (q.shape[1] // 128, q.shape[0], 4)):
+            raise ValueError("MxAct needs q [M, K] uint8 (K % 128 == 0) and e [K / 128, M, 4] uint8")
         self.q, self.e = q, e
+
+    @staticmethod
+    def empty(M: int, K: int, device) -> "MxAct":
+        return MxAct(torch.empty(M, K, dtype=torch.uint8, device=device),
+                     torch.empty(K // 128, M, 4, dtype=torch.uint8, device=device))
+
+    def blocks(self) -> torch.Tensor:
+        """The E8M0 scales as [M, K / 32]."""
+        return ref.mx_scales_from_device_layout(self.e)
 
     @property
     def shape(self):
@@ -215,19 +226,24 @@ class MxAct:
 
 
 # K8S_MX=0: the fp8 O / down GEMM rows take per-token e4m3 activations (a quantize_act_fp8 launch each) instead of
-# the MX form their producers write.
+# the MX form their producers write.  MX is used where the consuming GEMM is mgemm (batched decode, short chunks):
+# measured there 1.1-1.5x faster than quantize + per-token GEMM (profiles/mgemm_mx_tune_r5.txt; fp8 batch-64 decode
+# 20.0 -> 19.6 ms/step, one TP = 4 rank's shapes 8.40 -> 8.17).  pgemm's MX mode is correct but ~10 % slower than its
+# per-token mode at prefill sizes (the MFMA-bound regime; profiles/mx_pgemm_bench_r5.txt), more than the quantize
+# launch it saves, so prefill-size consumers stay per-token unless K8S_MX_PGEMM=1.
 MX_ON = os.environ.get("K8S_MX", "1") != "0"
+MX_PGEMM = os.environ.get("K8S_MX_PGEMM", "0") == "1"
 
 
 def quantize_act_mx(x: torch.Tensor) -> MxAct:
-    """bf16 [M, K] -> MxAct (stand-alone form of what the fused producers write; K % 32 == 0)."""
+    """bf16 [M, K] -> MxAct (stand-alone form of what the fused producers write; K % 128 == 0)."""
     if not x.is_cuda:
-        return MxAct(*ref.quantize_mx(x))
+        q, e = ref.quantize_mx(x)
+        return MxAct(q, ref.mx_scales_to_device_layout(e))
     M, K = x.shape
-    q = torch.empty(M, K, dtype=torch.uint8, device=x.device)
-    e = torch.empty(M, K // 32, dtype=torch.uint8, device=x.device)
-    native().quantize_act_mx(q.data_ptr(), e.data_ptr(), _chk(x, BF16, "x"), M, K, -1)
-    return MxAct(q, e)
+    a = MxAct.empty(M, K, x.device)
+    native().quantize_act_mx(a.q.data_ptr(), a.e.data_ptr(), _chk(x, BF16, "x"), M, K, -1)
+    return a
 
 
 def _fp8_gemm(x: torch.Tensor, w: "Fp8Weight", out_dtype=None, act=None) -> torch.Tensor:
@@ -516,7 +532,7 @@ def mgemm_valid(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int
         return False
     if int(fp8) in (2, 3) and _mg_mode_lds(cfg, int(fp8)) < 0:
         return False
-    if mx_out and (epi != EPI_SWIGLU or int(fp8) not in (1, 3) or N % 32 or _mg_mode_lds(cfg, 4) < 0):
+    if mx_out and (epi != EPI_SWIGLU or int(fp8) not in (1, 3) or N % 128 or _mg_mode_lds(cfg, 4) < 0):
         return False
     kb = K * (1 if fp8 else 2)
     if kb % mgemm_configs()[cfg][5] or N % 4 or M <= 0:
@@ -572,15 +588,16 @@ def mgemm_w8_plan(M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]
 
 
 def mgemm_mx_plan(M: int, N: int, K: int, epi: int, act_mx: bool, mx_out: bool) -> Optional[Tuple[int, int]]:
-    """(cfg, grid) for fp8 weights with MX activations (``act_mx``) and / or MX SwiGLU output, or None: the tuned fp8
-    plan where that configuration runs the mode, else the fp8 heuristic's, else the first weight-streaming / MFMA-dense
-    configuration that does (same grid rule)."""
+    """(cfg, grid) for fp8 weights with MX activations (``act_mx``; table key fp8 = 3) or MX SwiGLU output (key 4),
+    or None: the tuned MX plan, else the tuned fp8 plan where that configuration runs the mode, else the fp8
+    heuristic's, else the first weight-streaming / MFMA-dense configuration that does (same grid rule)."""
     mode = 3 if act_mx else 1
     if K % 128:
         return None
-    pick = _mg_table_row(M, N, K, epi, 1)
-    if pick is not None and mgemm_valid(pick[1], M, N, K, epi, mode, pick[2], mx_out):
-        return pick[1], pick[2]
+    for key in (3 if act_mx else 4, 1):   # the tuned MX plan (tools/mgemm_tune.py --mx), then the fp8 one
+        pick = _mg_table_row(M, N, K, epi, key)
+        if pick is not None and mgemm_valid(pick[1], M, N, K, epi, mode, pick[2], mx_out):
+            return pick[1], pick[2]
     cfg, grid = mgemm_heuristic(M, N, K, epi, 1)
     if mgemm_valid(cfg, M, N, K, epi, mode, grid, mx_out):
         return cfg, grid
@@ -732,10 +749,9 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
         raise ValueError("mgemm: residual epilogue needs a bf16 [M, N] residual and the bf16 epilogue")
     mxo = None
     if mx_out:
-        if res is not None:
-            raise ValueError("mgemm: MX output is the SwiGLU epilogue's")
-        mxo = MxAct(torch.empty(M, N, dtype=torch.uint8, device=x.device),
-                    torch.empty(M, N // 32, dtype=torch.uint8, device=x.device))
+        if res is not None or N % 128:
+            raise ValueError("mgemm: MX output is the SwiGLU epilogue's (N % 128 == 0)")
+        mxo = MxAct.empty(M, N, x.device)
         out = mxo.q   # (not written as bf16)
     if out is None:
         out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
@@ -810,10 +826,9 @@ def pgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: int = 0, splits: int = 1
     nwg, n_ws, n_tk = native().pgemm_plan(M, N, K, epi, int(fp8), cfg, splits)
     mxo = None
     if mx_out:
-        if epi != EPI_SWIGLU or N % 32 or res is not None:
-            raise ValueError("pgemm: MX output is the SwiGLU epilogue's (N % 32 == 0)")
-        mxo = MxAct(torch.empty(M, N, dtype=torch.uint8, device=x.device),
-                    torch.empty(M, N // 32, dtype=torch.uint8, device=x.device))
+        if epi != EPI_SWIGLU or N % 128 or res is not None:
+            raise ValueError("pgemm: MX output is the SwiGLU epilogue's (N % 128 == 0)")
+        mxo = MxAct.empty(M, N, x.device)
         out = mxo.q   # (not written as bf16)
     if out is None:
         out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
@@ -983,12 +998,52 @@ def xgemm(x: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, res: Optional[t
     return out
 
 
+def mx_rows(M: int, w) -> bool:
+    """An fp8 GEMM of M rows against ``w`` (the consumer: O or down) takes its input as MX e4m3 (:class:`MxAct`):
+    above the GEMV / sgemv rows (bf16 activations there), outside W8 mode, K % 128 == 0, on mgemm (or pgemm with
+    K8S_MX_PGEMM=1)."""
+    if not (MX_ON and _is_fp8(w) and M > max(GEMV_MAX_M, SGEMV_MAX_M) and not w8_rows(M)
+            and GEMM_BACKEND != "library" and w.shape[1] % 128 == 0):
+        return False
+    return MX_PGEMM or gemm_route(M, w.shape[0], w.shape[1], EPI_BF16, True)[0] == "mgemm"
+
+
+def _gemm_mx(act: MxAct, w, epi: int, res: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """An MX-activation GEMM on the routed kernel (mgemm MX mode / pgemm MX mode)."""
+    M, K = act.shape
+    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+    kern, plan = gemm_route(M, N, K, epi, True)
+    if kern == "pgemm":
+        cfg, sp, gm = plan
+        return pgemm(act, w, epi, cfg=cfg, splits=sp, group_m=gm, res=res, out=out)
+    if kern == "library":   # K8S_GEMM=library (the A/B oracle): per-token e4m3 of the dequantized MX rows
+        y = _fp8_gemm(act.dequant(), w, F32 if epi == EPI_F32 else BF16) if epi != EPI_SWIGLU else \
+            silu_mul(_fp8_gemm(act.dequant(), w))
+        if res is not None:
+            res.add_(y)
+            return res
+        return y
+    return mgemm(act, w, epi, res=res, out=out)
+
+
 def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
-          out: Optional[torch.Tensor] = None, act=None) -> Optional[torch.Tensor]:
+          out: Optional[torch.Tensor] = None, act=None, mx_out: bool = False):
     """Routed hand-written GEMM of M > GEMV_MAX_M rows (None: the library route).  ``act``: the fp8 activations
-    (e4m3, per-token scales) when the caller quantized them already."""
+    (e4m3, per-token scales) when the caller quantized them already, or an :class:`MxAct`.  ``mx_out`` (fp8 SwiGLU):
+    the result as an :class:`MxAct` where the routed kernel's plan writes it (else bf16)."""
+    if isinstance(act, MxAct):
+        return _gemm_mx(act, w, epi, res=res, out=out)
     M, K = x2.shape
     fp8 = _is_fp8(w)
+    if mx_out and fp8 and act is not None:
+        N = w.shape[0] // 2
+        kern, plan = gemm_route(M, N, K, epi, True)
+        if kern == "pgemm" and N % 128 == 0:
+            cfg, sp, gm = plan
+            return pgemm(x2, w, epi, cfg=cfg, splits=sp, group_m=gm, act=act, mx_out=True)
+        if kern == "mgemm" and mgemm_mx_plan(M, N, K, epi, False, True) is not None and N % 128 == 0:
+            return mgemm(x2, w, epi, act=act, mx_out=True)
     if M <= SGEMV_MAX_M and act is None:
         y = _sgemv(x2, w, epi, res=res, rms_eps=rms_eps, out=out)
         if y is not None:
@@ -1023,11 +1078,15 @@ RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "64"))
 RMS_UNFUSED_MIN_N = int(os.environ.get("K8S_RMS_UNFUSED_MIN_N", "8192"))
 
 
-def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Tensor:
+def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16, mx_consumer=None):
     """epi(rmsnorm(r) @ w.T) for M > GEMV_MAX_M rows with the norm gamma folded into ``w`` (LlamaModel folds it at
     load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
-    copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM."""
+    copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM.  ``mx_consumer`` (SwiGLU, fp8
+    weights): the weight of the GEMM that consumes the result (down); where :func:`mx_rows` holds for it, the
+    epilogue writes the result as an :class:`MxAct`."""
     M, K = r.shape
+    mx_out = (mx_consumer is not None and epi == EPI_SWIGLU and _is_fp8(w) and mx_rows(M, mx_consumer)
+              and (w.shape[0] // 2) % 128 == 0)
     if _is_fp8(w) and w8_rows(M):
         # W8 rows: mgemm's RMS prologue on the un-normalised bf16 rows against the fp8 weights (no quantize launch)
         if _gpu(r):
@@ -1044,7 +1103,7 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
         # reads r once; no rmsnorm kernel, no normalised copy) -> the fp8 GEMM
         act = quantize_act_fp8(r.contiguous(), rms_eps=eps)
         if _gpu(r):
-            y = _gemm(r.contiguous(), w, epi, act=act)
+            y = _gemm(r.contiguous(), w, epi, act=act, mx_out=mx_out)
             if y is None:   # K8S_GEMM=library
                 _library_allowed("linear_rms", r, w)
                 y = _fp8_gemm(r, w, F32 if epi == EPI_F32 else BF16, act=act) if epi != EPI_SWIGLU else \
@@ -1052,7 +1111,8 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
             return y
         xa = ref.dequant_fp8(act[0], act[1], torch.float32)
         if epi == EPI_SWIGLU:
-            return ref.linear_swiglu(xa, w).to(BF16)
+            y = ref.linear_swiglu(xa, w).to(BF16)
+            return quantize_act_mx(y) if mx_out else y
         return ref.linear(xa, w, F32 if epi == EPI_F32 else BF16)
     n_out = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     xg = (XGEMM_ON and not _is_fp8(w) and M <= XGEMM_MAX_M and GEMM_BACKEND == "auto"
@@ -1071,10 +1131,19 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16) -> torch.Ten
     return linear(x, w, F32 if epi == EPI_F32 else None)
 
 
-def linear_residual(x: torch.Tensor, w, res: torch.Tensor) -> torch.Tensor:
+def linear_residual(x, w, res: torch.Tensor) -> torch.Tensor:
     """res + x @ w.T (bf16), written into ``res`` (the residual stream).  mgemm route: the add is the GEMM's
-    epilogue; otherwise GEMM + add."""
+    epilogue; otherwise GEMM + add.  ``x``: bf16, or an :class:`MxAct` (fp8 weights); bf16 rows of
+    :func:`mx_rows` are turned into MX first (the producers that write MX themselves pass an MxAct)."""
     M, K = x.shape
+    if not isinstance(x, MxAct) and mx_rows(M, w) and K % 128 == 0:
+        x = quantize_act_mx(x.contiguous())
+    if isinstance(x, MxAct):
+        if not x.is_cuda:
+            y = ref.linear(x.dequant(torch.float32), w).to(BF16)
+            res.copy_((res.float() + y.float()).to(res.dtype))
+            return res
+        return _gemm_mx(x, w, EPI_BF16, res=res, out=res)
     if _gpu(x) and M > GEMV_MAX_M:
         y = _gemm(x.contiguous(), w, EPI_BF16, res=res, out=res)
         if y is not None:
@@ -1106,6 +1175,10 @@ if GEMM_BACKEND not in ("mgemm", "pgemm", "library", "auto"):
 def linear(x: torch.Tensor, w: torch.Tensor, out_dtype=None) -> torch.Tensor:
     """y = x @ w.T with w [N, K] (bf16 or Fp8Weight).  M <= GEMV_MAX_M rows: hand-written HBM-streaming GEMV;
     more rows (batched decode, prefill): hand-written MFMA GEMM (mgemm.hip)."""
+    if isinstance(x, MxAct):   # MX rows (fp8 weights): the producer's quantized activations
+        if not x.is_cuda:
+            return ref.linear(x.dequant(torch.float32), w, out_dtype or BF16)
+        return _gemm_mx(x, w, EPI_F32 if out_dtype == F32 else EPI_BF16)
     if not _gpu(x, w):
         return ref.linear(_ref_act_quant(x, w), w, out_dtype)
     x2 = x.reshape(-1, x.shape[-1])
@@ -1170,9 +1243,16 @@ def linear_norm(x: torch.Tensor, w, norm_w: Optional[torch.Tensor], eps: float,
 
 def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                            block_tables: torch.Tensor, context_lens: torch.Tensor, scale: float, block_size: int,
-                           max_context: int, nq: int, nkv: int, D: int) -> torch.Tensor:
-    """RoPE + KV write of the new token + paged GQA attention, one kernel.  Returns [B, nq*D]."""
+                           max_context: int, nq: int, nkv: int, D: int, mx: bool = False):
+    """RoPE + KV write of the new token + paged GQA attention, one kernel.  Returns [B, nq*D] bf16, or with ``mx``
+    an :class:`MxAct` (the fp8 O projection's input: written as MX e4m3 by the one-workgroup kernel and its merge;
+    the other forms quantize their bf16 output)."""
     B = qkv.shape[0]
+    if mx:
+        if not _gpu(qkv, k_cache) or block_size != 16 or (B * nkv <= _split_pairs_limit(max_context)
+                                                          and max_context <= 64 * SPLIT_PARTITION):
+            return quantize_act_mx(decode_attention_fused(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens,
+                                                          scale, block_size, max_context, nq, nkv, D))
     if not _gpu(qkv, k_cache) or block_size != 16:
         if _gpu(qkv, k_cache):  # general block sizes: unfused kernels
             q = rope_kv_write(qkv, cos_sin, k_cache, v_cache, nq, nkv, D, context_lens=context_lens,
@@ -1188,7 +1268,8 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
                                        max_context, nq, nkv, D)
     part = fused_partition(B * nkv)
     pmax = max(1, math.ceil(max_context / part))
-    out = torch.empty(B, nq * D, dtype=BF16, device=qkv.device)
+    mxo = MxAct.empty(B, nq * D, qkv.device) if mx else None
+    out = mxo.q if mx else torch.empty(B, nq * D, dtype=BF16, device=qkv.device)
     if pmax > 1:
         pacc = torch.empty(B * nq * pmax * D, dtype=F32, device=qkv.device)
         pml = torch.empty(B * nq * pmax * 2, dtype=F32, device=qkv.device)
@@ -1198,8 +1279,9 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
     native().decode_attention_fused(out.data_ptr(), pa, pm, _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"),
                                     _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
                                     _chk(block_tables, I32, "block_tables"), _chk(context_lens, I32, "context_lens"),
-                                    float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], pmax, part, -1)
-    return out
+                                    float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], pmax, part, -1,
+                                    mxo.q.data_ptr() if mx else 0, mxo.e.data_ptr() if mx else 0)
+    return mxo if mx else out
 
 
 # Context tokens per workgroup of the one-workgroup-per-pair decode attention: 1024 (16 waves, one workgroup per CU

@@ -201,7 +201,22 @@ def quantize_mx(x: torch.Tensor):
     return q.view(torch.uint8).reshape(M, K), e.to(torch.uint8)
 
 
+def mx_scales_to_device_layout(e: torch.Tensor) -> torch.Tensor:
+    """[M, K / 32] E8M0 -> the kernels' layout [K / 128, M, 4] (csrc/kernels/common.h mx_scale_off)."""
+    M, KB = e.shape
+    return e.reshape(M, KB // 4, 4).permute(1, 0, 2).contiguous()
+
+
+def mx_scales_from_device_layout(e: torch.Tensor) -> torch.Tensor:
+    """[K / 128, M, 4] -> [M, K / 32]."""
+    KT, M, _ = e.shape
+    return e.permute(1, 0, 2).reshape(M, KT * 4)
+
+
 def dequant_mx(q: torch.Tensor, e: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    """``e``: [M, K / 32] (logical) or the kernels' [K / 128, M, 4]."""
+    if e.dim() == 3:
+        e = mx_scales_from_device_layout(e)
     M, K = q.shape
     s = torch.ldexp(torch.ones(e.shape, dtype=torch.float32, device=q.device), e.float() - 127)
     v = q.view(torch.float8_e4m3fn).float().reshape(M, K // MX_BLOCK, MX_BLOCK) * s[..., None]

@@ -108,3 +108,28 @@ def test_fp8_linear_rms_quantizes_the_unnormalised_rows():
     gu = ops.quantize_fp8((torch.randn(2 * 32, 256, generator=g) * 0.05).bfloat16())
     y = ops.linear_rms(r, gu, 1e-5, ops.EPI_SWIGLU)
     assert y.shape == (M, 32) and y.dtype == torch.bfloat16
+
+
+def test_mx_rows_route_o_and_down_inputs_through_mx_e4m3():
+    """K16 block-scaled: above the sgemv rows the fp8 SwiGLU output is produced as MX e4m3 (one E8M0 scale per 32
+    values) and the O / down projections consume MX rows; the CPU path rounds exactly as the GPU kernels do."""
+    g = torch.Generator().manual_seed(4)
+    M = max(ops.GEMV_MAX_M, ops.SGEMV_MAX_M) + 5
+    r = (torch.randn(M, 256, generator=g) * 3).bfloat16()
+    gu = ops.quantize_fp8((torch.randn(2 * 128, 256, generator=g) * 0.05).bfloat16())
+    wd = ops.quantize_fp8((torch.randn(256, 128, generator=g) * 0.05).bfloat16())
+    y = ops.linear_rms(r, gu, 1e-5, ops.EPI_SWIGLU, mx_consumer=wd)
+    if not ops.mx_rows(M, wd):
+        assert isinstance(y, torch.Tensor)
+        return
+    assert isinstance(y, ops.MxAct) and y.q.shape == (M, 128) and y.blocks().shape == (M, 4)
+    bf = ops.linear_rms(r, gu, 1e-5, ops.EPI_SWIGLU)
+    q, e = ref.quantize_mx(bf)
+    assert torch.equal(y.q, q) and torch.equal(y.blocks(), e)
+    res = torch.randn(M, 256, generator=g).bfloat16()
+    want = (res.float() + (ref.dequant_mx(q, e) @ wd.dequant(torch.float32).T).bfloat16().float()).bfloat16()
+    out = ops.linear_residual(y, wd, res.clone())
+    torch.testing.assert_close(out.float(), want.float())
+    # bf16 rows of the MX range are quantized to MX before the fp8 GEMM (the attention output's path)
+    out2 = ops.linear_residual(bf, wd, res.clone())
+    torch.testing.assert_close(out2.float(), want.float())

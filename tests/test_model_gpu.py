@@ -106,21 +106,25 @@ def test_long_prefill_on_big_tile_gemms_matches_cpu_reference(fp8):
     """A 600-token prefill: every projection has M = 600 >= PG_MIN_M rows, so gemm_route puts them on the big-tile
     kernels (pgemm / pgemm4, RMS prologue + residual epilogue fused) -- never the library -- vs the CPU model."""
     calls = []
-    real = ops._gemm
+    real, real_mx = ops._gemm, ops._gemm_mx
 
     def spy(x2, w, epi, **kw):
         calls.append(ops.gemm_route(x2.shape[0], w.shape[0] // (2 if epi == ops.EPI_SWIGLU else 1), x2.shape[1],
                                     epi, ops._is_fp8(w))[0])
         return real(x2, w, epi, **kw)
 
+    def spy_mx(act, w, epi, **kw):   # fp8: the O / down inputs arrive as MX e4m3
+        calls.append(ops.gemm_route(act.shape[0], w.shape[0], act.shape[1], epi, True)[0])
+        return real_mx(act, w, epi, **kw)
+
     g = LlamaModel(CFG, device="cuda", seed=4, max_model_len=2048, weight_dtype="fp8" if fp8 else "bf16")
     c = LlamaModel(CFG, device="cpu", seed=4, max_model_len=2048, weight_dtype="fp8" if fp8 else "bf16")
     ids = [(13 * p + 5) % 16000 for p in range(600)]
-    orig, ops._gemm = ops._gemm, spy
+    ops._gemm, ops._gemm_mx = spy, spy_mx
     try:
         lg_g, _ = _prefill(g, ids)
     finally:
-        ops._gemm = orig
+        ops._gemm, ops._gemm_mx = real, real_mx
     lg_c, _ = _prefill(c, ids)
     assert calls and all(k in ("pgemm", "pgemm4", "mgemm") for k in calls) and \
         sum(k.startswith("pgemm") for k in calls) >= 3 * CFG.num_layers, calls

@@ -29,12 +29,12 @@ def _weights(rows, K, seed):
     return ops.quantize_fp8(((torch.rand(rows, K, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16).to(DEV))
 
 
-@pytest.mark.parametrize("M,K", [(1, 32), (17, 256), (64, 8192), (130, 3584), (7, 28672)])
+@pytest.mark.parametrize("M,K", [(1, 128), (17, 256), (64, 8192), (130, 3584), (7, 28672)])
 def test_quantize_act_mx_matches_reference_bit_for_bit(M, K):
     x = _act(M, K, M + K)
     a = ops.quantize_act_mx(x.to(DEV))
     q, e = ref.quantize_mx(x)
-    assert torch.equal(a.e.cpu(), e)
+    assert torch.equal(a.blocks().cpu(), e)
     assert torch.equal(a.q.cpu(), q)
     back = a.dequant(torch.float32).cpu()
     blk = torch.ldexp(torch.ones(e.shape), e.float() - 127).repeat_interleave(32, 1)   # the block scales
@@ -104,7 +104,7 @@ def test_mgemm_swiglu_mx_output_is_the_quantized_bf16_output(act_mx):
                 y = ops.mgemm(x, w, ops.EPI_SWIGLU, cfg=cfg, grid=grid, act=act)
                 mx = ops.mgemm(x, w, ops.EPI_SWIGLU, cfg=cfg, grid=grid, act=act, mx_out=True)
                 q, e = ref.quantize_mx(y.cpu())
-                assert torch.equal(mx.e.cpu(), e), f"cfg {cfg} grid {grid} M {M}"
+                assert torch.equal(mx.blocks().cpu(), e), f"cfg {cfg} grid {grid} M {M}"
                 assert torch.equal(mx.q.cpu(), q), f"cfg {cfg} grid {grid} M {M}"
     assert n_cfg >= 2
 
@@ -152,7 +152,34 @@ def test_pgemm_swiglu_mx_output_is_the_quantized_bf16_output(act_mx):
                 y = ops.pgemm(x, w, ops.EPI_SWIGLU, cfg=cfg, splits=splits, act=act)
                 mx = ops.pgemm(x, w, ops.EPI_SWIGLU, cfg=cfg, splits=splits, act=act, mx_out=True)
                 q, e = ref.quantize_mx(y.cpu())
-                assert torch.equal(mx.e.cpu(), e), f"cfg {cfg} splits {splits}/{slabs}"
+                assert torch.equal(mx.blocks().cpu(), e), f"cfg {cfg} splits {splits}/{slabs}"
                 assert torch.equal(mx.q.cpu(), q), f"cfg {cfg} splits {splits}/{slabs}"
     finally:
         ops.native().pgemm_set_row_slabs(keep)
+
+
+@pytest.mark.parametrize("B,ctx,part", [(24, 300, 1024), (64, 1500, 1024), (40, 700, 512)])
+def test_decode_attention_mx_output_is_the_quantized_bf16_output(B, ctx, part, monkeypatch):
+    """The one-workgroup decode attention (and its partition merge, ctx > part) writes the O projection's input as
+    MX e4m3: bit for bit quantize_act_mx of its bf16 output."""
+    from k8s_llm_scheduler_amd.models.config import PRESETS
+    from k8s_llm_scheduler_amd.models.llama import LlamaModel
+    monkeypatch.setattr(ops, "FUSED_PART_ENV", part)
+    monkeypatch.setattr(ops, "SPLIT_MAX_PAIRS", 0)   # the one-workgroup kernel
+    m = LlamaModel(PRESETS["tiny"], device="cuda", seed=1, max_model_len=2048)
+    nb = (ctx + 15) // 16 + 1
+    m.allocate_kv(B * nb + 1, 16)
+    kc, vc = m.kv_cache[0, 0], m.kv_cache[0, 1]
+    kc.normal_()
+    vc.normal_()
+    g = torch.Generator(device="cpu").manual_seed(B)
+    qkv = (torch.randn(B, (m.nq + 2 * m.nkv) * m.D, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    ctxs = torch.tensor([max(1, ctx - 7 * i) for i in range(B)], dtype=torch.int32, device=DEV)
+    bt = torch.arange(B * nb, dtype=torch.int32, device=DEV).view(B, nb)
+    args = (qkv, m.cos_sin, kc, vc, bt, ctxs, m.scale, 16, ctx, m.nq, m.nkv, m.D)
+    y = ops.decode_attention_fused(*args)
+    mx = ops.decode_attention_fused(*args, mx=True)
+    assert isinstance(mx, ops.MxAct)
+    q, e = ref.quantize_mx(y.cpu())
+    assert torch.equal(mx.blocks().cpu(), e)
+    assert torch.equal(mx.q.cpu(), q)

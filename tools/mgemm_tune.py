@@ -11,6 +11,10 @@ copies of the weight to exceed the 256 MiB Infinity Cache (weights are cold in t
 --w8 tunes mgemm's W8 mode (fp8 weights, bf16 activations; table key fp8 = 2) against the per-token e4m3 path it
 replaces (quantize_act_fp8 + the tuned fp8 mgemm plan).
 
+--mx tunes the K16 MX modes (fp8 weights): O / down with MX e4m3 activations (table key fp8 = 3; compared with the
+per-token path they replace: quantize_act_fp8 + the tuned fp8 plan) and gate/up with the SwiGLU epilogue writing MX
+output (key fp8 = 4; compared with the same GEMM writing bf16, per-token activations quantized outside both).
+
 --write merges the winners into engine/assets/mgemm_gfx950.json (the table ops.mgemm_plan reads).
 """
 
@@ -31,6 +35,7 @@ from k8s_llm_scheduler_amd import ops  # noqa: E402
 from k8s_llm_scheduler_amd.engine import _load_gemm_table  # noqa: E402
 
 REPS = 12
+ACT = [None]   # MX tuning: the activations every candidate takes (MxAct, or the per-token pair for --mx gate/up)
 COLD_BYTES = 600 << 20
 
 
@@ -73,16 +78,18 @@ def time_graph(fn, copies: int) -> float:
 def candidates(M, N, K, epi, fp8):
     cfgs = ops.mgemm_configs()
     out = []
+    mx_out = fp8 == 4
+    mode = 1 if mx_out else fp8
     for c, (bm, bn, _th, _lds, _sw, rb) in enumerate(cfgs):
         steps = K * (1 if fp8 else 2) // rb
-        if fp8 == 2 and not ops.mgemm_valid(c, M, N, K, epi, 2):
+        if fp8 in (2, 3, 4) and not ops.mgemm_valid(c, M, N, K, epi, mode, 1, mx_out):
             continue
         if bm > max(16, 2 * M) or (M > 64 and bm < 64) or (M > 256 and bm < 128):
             continue
         tiles = ops._mg_tiles(c, M, N, epi)
         seen = set()
         for gr in ops.MG_GRIDS:
-            if not ops.mgemm_valid(c, M, N, K, epi, fp8, gr):
+            if not ops.mgemm_valid(c, M, N, K, epi, mode, gr, mx_out):
                 continue
             nwg = ops.mgemm_nwg(c, M, N, K, epi, fp8, gr)
             if nwg in seen or (gr > 1 and steps // gr < 4) or nwg > 4096:
@@ -95,8 +102,10 @@ def candidates(M, N, K, epi, fp8):
 def lib_fn(x, Ws, epi, fp8):
     def f(i):
         w = Ws[i]
-        if fp8 == 2:   # W8 tuning: the per-token e4m3 path it replaces
+        if fp8 in (2, 3):   # W8 / MX tuning: the per-token e4m3 path it replaces (quantize + the tuned fp8 plan)
             return ops.mgemm(x, w, epi)
+        if fp8 == 4:        # MX output tuning: the same GEMM writing bf16 (per-token activations given)
+            return ops.mgemm(x, w, epi, act=ACT[0])
         if fp8:
             y = ops._fp8_gemm(x, w)
             if epi == ops.EPI_F32:
@@ -119,6 +128,7 @@ def main() -> int:
     ap.add_argument("--only", nargs="*", default=None, help="projection names")
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--w8", action="store_true", help="tune the W8 mode (fp8 weights, bf16 activations)")
+    ap.add_argument("--mx", action="store_true", help="tune the MX modes (MX activations; MX SwiGLU output)")
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
@@ -140,6 +150,10 @@ def main() -> int:
         for name, N, K, epi in shapes(tp):
             if a.only and name not in a.only:
                 continue
+            if a.mx:
+                if name in ("qkv", "lm_head"):   # per-token (RMS-folded) inputs: nothing MX to tune
+                    continue
+                a.fp8 = 4 if epi == ops.EPI_SWIGLU else 3
             wrows = 2 * N if epi == ops.EPI_SWIGLU else N
             wbytes = wrows * K * (1 if a.fp8 else 2)
             copies = max(1, min(16, math.ceil(COLD_BYTES / wbytes)))
@@ -150,11 +164,16 @@ def main() -> int:
                 del w
             for M in a.m:
                 x = torch.empty(M, K, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1)
+                ACT[0] = (ops.quantize_act_mx(x) if a.fp8 == 3 else ops.quantize_act_fp8(x) if a.fp8 == 4
+                          else None)
                 lib_us = time_graph(lib_fn(x, Ws, epi, a.fp8), copies)
                 best = (float("inf"), None)
+
+                def run(i, c, gr):
+                    return ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr, w8=a.fp8 == 2, act=ACT[0], mx_out=a.fp8 == 4)
+
                 for c, gr in candidates(M, N, K, epi, a.fp8):
-                    us = time_graph(lambda i, c=c, gr=gr: ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr, w8=a.fp8 == 2),
-                                    copies)
+                    us = time_graph(lambda i, c=c, gr=gr: run(i, c, gr), copies)
                     if a.verbose:
                         bm, bn = ops.mgemm_configs()[c][:2]
                         print(f"    cand tp{tp} {name} M={M} cfg {c:2d} ({bm}x{bn}) grid {gr:5d} "
@@ -168,8 +187,9 @@ def main() -> int:
                     else:
                         gfn = lambda i: ops.linear(x, Ws[i], out_dtype=torch.float32 if epi == ops.EPI_F32 else None)
                     gemv_us = round(time_graph(gfn, copies), 2)
-                hc = ops.mgemm_heuristic(M, N, K, epi, a.fp8)
-                h_us = time_graph(lambda i: ops.mgemm(x, Ws[i], epi, cfg=hc[0], grid=hc[1], w8=a.fp8 == 2), copies)
+                hc = (ops.mgemm_heuristic(M, N, K, epi, a.fp8) if a.fp8 in (0, 1, 2) else
+                      ops.mgemm_mx_plan(M, N, K, epi, a.fp8 == 3, a.fp8 == 4))
+                h_us = time_graph(lambda i: run(i, hc[0], hc[1]), copies)
                 us, (c, ks) = best
                 plans[f"{ops._mg_bucket(M)},{N},{K},{epi},{int(a.fp8)}"] = [c, ks, round(us, 2), round(lib_us, 2)]
                 row = dict(tp=tp, proj=name, M=M, N=N, K=K, epi=epi, fp8=a.fp8, lib_us=round(lib_us, 2),
