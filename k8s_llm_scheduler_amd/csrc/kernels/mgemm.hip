@@ -51,6 +51,7 @@ enum { MG_BF16 = 0, MG_F32 = 1, MG_SWIGLU = 2 };
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(2))) float f2v;
 
 __device__ __forceinline__ float mg_silu(float g) { return g / (1.f + __expf(-g)); }
 
@@ -122,8 +123,9 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert(RB == 64 || RB == 128 || RB == 256 || RB == 512, "row bytes per k-step");
   static_assert(!(FP8 && W8), "W8: fp8 weights with bf16 activations");
   static_assert(!MX || FP8, "MX: e4m3 activations with E8M0 block scales");
-  static_assert(!MXO || (EPI == MG_SWIGLU && ((FN / 2) % 2 == 0 || (FN == 2 && WN % 2 == 0 && WK == 1))),
-                "MX output: SwiGLU, 32-feature spans per wave or per wave pair");
+  static_assert(!MXO || (EPI == MG_SWIGLU && ((FN / 2) % 2 == 0 || (FN == 2 && WN % 2 == 0 && WK == 1))) ||
+                    (EPI == MG_BF16 && FN % 2 == 0),
+                "MX output: SwiGLU with 32-feature spans per wave or wave pair, or the residual epilogue");
   constexpr int XRB = W8 ? 2 * RB : RB;              // x row bytes per k-step (W8: RB bf16 values)
   constexpr int CPR = RB / 16, XCPR = XRB / 16;      // 16-byte chunks per staged W / x row
   constexpr int KS = (FP8 || W8) ? RB / 32 : RB / 64;   // k32 MFMA steps per k-step (RB = 64: one)
@@ -140,9 +142,11 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert((S - 2) * LPS <= 63, "vmcnt range");
   static_assert(WK == 1 || (WK - 1) * FN * FM * 64 * 16 * WM * WN <= S * STAGE_B, "LDS reduction space");
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the launch stub (its lambdas use device builtins)
-  __shared__ __attribute__((aligned(16))) char lds[S * STAGE_B + 16 + WK * WN * BM * 4];
+  constexpr int XPAIR = (MXO && EPI == MG_SWIGLU && FN == 2) ? WN * BM : 0;   // wave-pair MX absmax exchange
+  __shared__ __attribute__((aligned(16))) char lds[S * STAGE_B + 16 + WK * WN * BM * 4 + XPAIR * 4];
   unsigned* flag = reinterpret_cast<unsigned*>(lds + S * STAGE_B);
   float* rss = reinterpret_cast<float*>(lds + S * STAGE_B + 16);   // [WK * WN][BM] row sums of squares
+  float* xpair = rss + WK * WN * BM;                                 // [WN][BM] (wave-pair MX output)
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wk = wid % WK, wt = wid / WK;           // k-share, output sub-tile
@@ -249,7 +253,10 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     float ss[FM];   // RMS prologue: this lane's share of sum(x^2) of its fragment rows
 #pragma unroll
     for (int j = 0; j < FM; ++j) ss[j] = 0.f;
-    const bool do_rms = !FP8 && a.rms != 0;
+    f32x4 accsq[MX ? FM : 1];   // MX RMS prologue: x . x^T per row fragment (diagonal = sums of squares)
+#pragma unroll
+    for (int j = 0; j < (MX ? FM : 1); ++j) accsq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool do_rms = (!FP8 || MX) && a.rms != 0;   // MX: the squares of the dequantized e4m3 values
     // 8 e4m3 weights -> the bf16x8 A operand (exact; the row scale is applied in the epilogue)
     auto w8_frag = [](long q) {
       const uint32_t lo = (uint32_t)q, hi = (uint32_t)((unsigned long)q >> 32);
@@ -323,6 +330,14 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
               const int r = brow0 + j * 16;
               bx[j] = frag32(xb + r * RB, r);
               sc[j] = sl[r * KS4 + kk4] >> (8 * g);   // this lane's block scale in byte 0 (op_sel 0)
+              // RMS prologue on MX rows: one more MFMA, x . x^T of the fragment with both scale operands = the
+              // block scales -- its diagonal is the rows' sums of squares of the dequantized values (the VALU
+              // form, 16 conversions + 32 FMAs per lane and subtile, was the bottleneck); wave wn = 0 of a row block.
+              // The condition must be a scalar branch: an MFMA ignores EXEC, so a lane-masked "if" would still
+              // accumulate in every wave (readfirstlane makes wn provably wave-uniform)
+              if (do_rms && __builtin_amdgcn_readfirstlane(wn) == 0)
+                accsq[j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bx[j], bx[j], accsq[j], 0, 0, 0, sc[j], 0,
+                                                                            sc[j]);
             }
 #pragma unroll
             for (int f = 0; f < FN; ++f)
@@ -394,6 +409,12 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     }
 
     // ---- RMS prologue: row sums of squares over this segment's k-steps -> rss[wk][row]
+    if constexpr (MX) {   // the diagonal of x . x^T: C[4 g + i][li] with 4 g + i == li
+      if (do_rms) {
+#pragma unroll
+        for (int j = 0; j < FM; ++j) ss[j] = (g == (li >> 2)) ? accsq[j][li & 3] : 0.f;
+      }
+    }
     if (do_rms) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
@@ -475,15 +496,16 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     if (do_rms) mg_barrier();   // row totals visible to every wave's epilogue
     if (wk != 0) continue;
 
-    if constexpr (MXO && FN == 2) {
+    if constexpr (MXO && EPI == MG_SWIGLU && FN == 2) {
       // MX output, 16 SwiGLU features per wave: a 32-feature block is waves wn and wn ^ 1 (same rows); each wave
-      // parks its rows' absmax in rss (free in fp8 modes), one barrier, then both take the pair's max
+      // parks its rows' absmax in LDS, one barrier, then both take the pair's max
       float v[FM][4], am[FM];
       const int n0 = nt * (BN / 2) + wn * 16 + 4 * g;
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int m = min(mt * BM + wm * (BM / WM) + j * 16 + li, a.M - 1);
-        const float sxx = MX ? 1.f : a.xs[m];
+        float sxx = MX ? 1.f : a.xs[m];
+        if (do_rms) sxx = rsqrtf(rss[wm * (BM / WM) + j * 16 + li] / (float)a.xkbytes + a.eps);
         am[j] = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -496,14 +518,14 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
         }
         am[j] = fmaxf(am[j], __shfl_xor(am[j], 16, WAVE));
         am[j] = fmaxf(am[j], __shfl_xor(am[j], 32, WAVE));
-        rss[wn * BM + wm * (BM / WM) + j * 16 + li] = am[j];
+        xpair[wn * BM + wm * (BM / WM) + j * 16 + li] = am[j];
       }
       mg_barrier();
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int m = mt * BM + wm * (BM / WM) + j * 16 + li;
         if (m >= a.M || n0 >= a.N_out) continue;   // N_out % 32 == 0: a wave pair is in or out together
-        const float amax = fmaxf(am[j], rss[(wn ^ 1) * BM + wm * (BM / WM) + j * 16 + li]);
+        const float amax = fmaxf(am[j], xpair[(wn ^ 1) * BM + wm * (BM / WM) + j * 16 + li]);
         const uint32_t e = mx_e8m0(amax);
         *reinterpret_cast<uint32_t*>(a.oq + (long long)m * a.N_out + n0) =
             mx_pack4(v[j][0], v[j][1], v[j][2], v[j][3], mx_inv_scale(e));
@@ -518,8 +540,8 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
       const int m = mt * BM + wm * (BM / WM) + j * 16 + li;
       if (m >= a.M) continue;
       float sx = (FP8 && !MX) ? a.xs[m] : 1.f;
-      if (do_rms) sx = rsqrtf(rss[wm * (BM / WM) + j * 16 + li] / (float)(a.xkbytes >> 1) + a.eps);
-      if constexpr (MXO && FN != 2) {   // 32-feature blocks = fragment pairs (2 b, 2 b + 1); the block's lanes share li
+      if (do_rms) sx = rsqrtf(rss[wm * (BM / WM) + j * 16 + li] / (float)(MX ? a.xkbytes : (a.xkbytes >> 1)) + a.eps);
+      if constexpr (MXO && EPI == MG_SWIGLU && FN != 2) {   // 32-feature blocks = fragment pairs (2 b, 2 b + 1)
 #pragma unroll
         for (int b = 0; b < FN / 4; ++b) {
           const int nb = nt * (BN / 2) + wn * (BN / 2 / WN) + b * 32;   // first feature of the block
@@ -533,6 +555,44 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
               float gt = acc[f][j][i] * sx * a.wsc[n0 + i], up = acc[f + FN / 2][j][i] * sx * a.wsc[a.half_rows + n0 + i];
               v[4 * h + i] = bf_round(mg_silu(gt) * up);
             }
+          }
+          float amax = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+          amax = fmaxf(amax, __shfl_xor(amax, 16, WAVE));
+          amax = fmaxf(amax, __shfl_xor(amax, 32, WAVE));
+          const uint32_t e = mx_e8m0(amax);
+          const float inv = mx_inv_scale(e);
+          uint8_t* orow = a.oq + (long long)m * a.N_out;
+          *reinterpret_cast<uint32_t*>(orow + nb + 4 * g) = mx_pack4(v[0], v[1], v[2], v[3], inv);
+          *reinterpret_cast<uint32_t*>(orow + nb + 16 + 4 * g) = mx_pack4(v[4], v[5], v[6], v[7], inv);
+          if (g == 0) a.oe[mx_scale_off(m, nb >> 5, a.M)] = (uint8_t)e;
+        }
+      } else if constexpr (MXO && EPI == MG_BF16) {
+        // residual epilogue + its MX copy: out = acc + res (bf16, the residual stream) and the same values as MX
+        // e4m3 -- the next pre-norm projection's input (its RMS statistics are that GEMM's prologue)
+#pragma unroll
+        for (int b = 0; b < FN / 2; ++b) {
+          const int nb = nt * BN + wn * (BN / WN) + b * 32;
+          if (nb >= a.N_out) continue;   // N_out % 128 == 0: whole blocks
+          float v[8];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int f = 2 * b + h, n0 = nb + 16 * h + 4 * g;
+            const u32x2 rr = *reinterpret_cast<const u32x2*>(a.res + (long long)m * a.N_out + n0);
+            float t[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) t[i] = acc[f][j][i] * sx * a.wsc[n0 + i];
+            t[0] += lo_bf(rr[0]);
+            t[1] += hi_bf(rr[0]);
+            t[2] += lo_bf(rr[1]);
+            t[3] += hi_bf(rr[1]);
+            const u32x2 o = {pack_bf2(t[0], t[1]), pack_bf2(t[2], t[3])};
+            *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.out) + (long long)m * a.N_out + n0) = o;
+            v[4 * h] = lo_bf(o[0]);
+            v[4 * h + 1] = hi_bf(o[0]);
+            v[4 * h + 2] = lo_bf(o[1]);
+            v[4 * h + 3] = hi_bf(o[1]);
           }
           float amax = 0.f;
 #pragma unroll
@@ -665,11 +725,15 @@ constexpr bool mg_mxo_cfg(int c) {
          (kMgCfgs[c].bn / (kMgCfgs[c].wn * 16) == 2 && kMgCfgs[c].wn % 2 == 0 && kMgCfgs[c].wk == 1);
 }
 
+// residual epilogue with MX output: fragment pairs per wave
+constexpr bool mg_mxr_cfg(int c) { return (kMgCfgs[c].bn / (kMgCfgs[c].wn * 16)) % 2 == 0; }
+
 template <int C, int EPI, bool FP8, bool W8, bool MX, bool MXO>
 int mg_launch(const MgArgs& a, int grid, hipStream_t s) {
   constexpr bool ok = (EPI != MG_SWIGLU || (kMgCfgs[C].bn / (kMgCfgs[C].wn * 16)) % 2 == 0) &&
                       (!W8 || (mg_w8_cfg(C) && mg_lds_bytes(kMgCfgs[C], 2) <= 160 * 1024)) &&
-                      (!MX || mg_mx_cfg(C)) && (!MXO || (EPI == MG_SWIGLU && mg_mxo_cfg(C)));
+                      (!MX || mg_mx_cfg(C)) &&
+                      (!MXO || (EPI == MG_SWIGLU && mg_mxo_cfg(C)) || (EPI == MG_BF16 && mg_mxr_cfg(C)));
   if constexpr (!ok) {
     return -2;
   } else {
@@ -682,8 +746,12 @@ int mg_launch(const MgArgs& a, int grid, hipStream_t s) {
 
 template <int C, bool FP8, bool W8, bool MX>
 int mg_epi(const MgArgs& a, int grid, int epi, bool mxo, hipStream_t s) {
-  if constexpr (FP8) {   // MX output: the SwiGLU epilogue of the fp8 and MX modes
-    if (mxo) return epi == MG_SWIGLU ? mg_launch<C, MG_SWIGLU, FP8, W8, MX, true>(a, grid, s) : -2;
+  if constexpr (FP8) {   // MX output: the SwiGLU / residual epilogues of the fp8 and MX modes
+    if (mxo) {
+      if (epi == MG_SWIGLU) return mg_launch<C, MG_SWIGLU, FP8, W8, MX, true>(a, grid, s);
+      if (epi == MG_BF16) return mg_launch<C, MG_BF16, FP8, W8, MX, true>(a, grid, s);
+      return -2;
+    }
   }
   switch (epi) {
     case MG_BF16: return mg_launch<C, MG_BF16, FP8, W8, MX, false>(a, grid, s);
@@ -719,13 +787,16 @@ bool mg_mxo_valid(int cfg) {
   if constexpr (C < kMgNumCfgs) return cfg == C ? mg_mxo_cfg(C) : mg_mxo_valid<C + 1>(cfg);
   else return false;
 }
+bool mg_mxr_valid(int cfg) { return cfg >= 0 && cfg < kMgNumCfgs && (kMgCfgs[cfg].bn / (kMgCfgs[cfg].wn * 16)) % 2 == 0; }
 }  // namespace
 
 // LDS bytes of a config in a mode (0 bf16, 1 fp8, 2 W8, 3 MX activations); -1: the config is not built for that
-// mode.  Mode 4: 0 if the config's SwiGLU epilogue can write MX output, else -1.
+// mode.  Mode 4: 0 if the config's SwiGLU epilogue can write MX output, else -1; mode 5: the same for the residual
+// epilogue.
 extern "C" int k8s_mgemm_lds_bytes(int cfg, int mode) {
-  if (cfg < 0 || cfg >= kMgNumCfgs || mode < 0 || mode > 4) return -1;
+  if (cfg < 0 || cfg >= kMgNumCfgs || mode < 0 || mode > 5) return -1;
   if (mode == 4) return mg_mxo_valid(cfg) ? 0 : -1;
+  if (mode == 5) return mg_mxr_valid(cfg) ? 0 : -1;
   const int b = mg_lds_bytes(kMgCfgs[cfg], mode);
   if (mode == 2 && (!mg_w8_cfg(cfg) || b > 160 * 1024)) return -1;
   if (mode == 3 && !mg_mx_valid(cfg)) return -1;
@@ -791,7 +862,8 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   if (N_out % 4 != 0) return -1;
   if (fp8 < 0 || fp8 > 3) return -1;
   const bool w8 = fp8 == 2, mx = fp8 == 3, mxo = oq != nullptr;
-  if (mxo && (oe == nullptr || epi != MG_SWIGLU || (fp8 != 1 && fp8 != 3) || N_out % 128 != 0 || !mg_mxo_valid(cfg)))
+  if (mxo && (oe == nullptr || (fp8 != 1 && fp8 != 3) || N_out % 128 != 0 ||
+              !(epi == MG_SWIGLU ? mg_mxo_valid(cfg) : (epi == MG_BF16 && res != nullptr && mg_mxr_valid(cfg)))))
     return -7;
   if (mx && (K % 128 != 0 || !mg_mx_valid(cfg))) return -7;
   const long long kbytes = (long long)K * (fp8 ? 1 : 2), xkbytes = (long long)K * ((fp8 == 1 || fp8 == 3) ? 1 : 2);
@@ -805,7 +877,7 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   if ((fp8 == 1 || fp8 == 3) && (xs == nullptr || wsc == nullptr)) return -3;
   if (w8 && wsc == nullptr) return -3;
   if (res != nullptr && epi != MG_BF16) return -6;   // residual epilogue: bf16 output only
-  if (rms && (fp8 == 1 || fp8 == 3)) return -6;      // fp8 activations are quantized before the GEMM
+  if (rms && fp8 == 1) return -6;   // per-token e4m3 activations carry 1 / rms in their scales (MX rows: prologue)
   MgArgs a;
   a.res = static_cast<const bf16_t*>(res);
   a.rms = rms;

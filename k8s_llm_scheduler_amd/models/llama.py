@@ -217,18 +217,23 @@ class LlamaModel:
         eps = self.cfg.rms_eps
         r = h.clone()
         tp1 = self.tp.world == 1 or self.tp.simulate
+        r_mx = None   # fp8 GEMM rows at TP = 1: the MX copy of r written by the residual epilogue (K16)
+        L = len(self.layers)
         for l, w in enumerate(self.layers):
-            qkv = ops.linear_rms(r, w.wqkv, eps)
+            qkv = ops.linear_rms(r, w.wqkv, eps, x_mx=r_mx)
             a = attn(l, qkv)
             if tp1:
-                r = ops.linear_residual(a, w.wo, r)
+                r, r_mx = ops.linear_residual(a, w.wo, r, mx_next=w.wgu)
             else:
                 o = ops.linear(a, w.wo)
                 self.tp.all_reduce_(o, residual=r)     # o = r + attention branch
                 r = o
-            g = ops.linear_rms(r, w.wgu, eps, ops.EPI_SWIGLU, mx_consumer=w.wdown)   # fp8 GEMM rows: MX e4m3 (K16)
+            g = ops.linear_rms(r, w.wgu, eps, ops.EPI_SWIGLU, mx_consumer=w.wdown, x_mx=r_mx)   # fp8: MX e4m3
             if tp1:
-                r = ops.linear_residual(g, w.wdown, r)
+                if l + 1 < L:
+                    r, r_mx = ops.linear_residual(g, w.wdown, r, mx_next=self.layers[l + 1].wqkv)
+                else:
+                    r = ops.linear_residual(g, w.wdown, r)
             else:
                 d = ops.linear(g, w.wdown)
                 self.tp.all_reduce_(d, residual=r)     # d = r + MLP branch

@@ -532,7 +532,8 @@ def mgemm_valid(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int
         return False
     if int(fp8) in (2, 3) and _mg_mode_lds(cfg, int(fp8)) < 0:
         return False
-    if mx_out and (epi != EPI_SWIGLU or int(fp8) not in (1, 3) or N % 128 or _mg_mode_lds(cfg, 4) < 0):
+    if mx_out and (int(fp8) not in (1, 3) or N % 128 or
+                   (_mg_mode_lds(cfg, 4) < 0 if epi == EPI_SWIGLU else (epi != EPI_BF16 or _mg_mode_lds(cfg, 5) < 0))):
         return False
     kb = K * (1 if fp8 else 2)
     if kb % mgemm_configs()[cfg][5] or N % 4 or M <= 0:
@@ -594,7 +595,7 @@ def mgemm_mx_plan(M: int, N: int, K: int, epi: int, act_mx: bool, mx_out: bool) 
     mode = 3 if act_mx else 1
     if K % 128:
         return None
-    for key in (3 if act_mx else 4, 1):   # the tuned MX plan (tools/mgemm_tune.py --mx), then the fp8 one
+    for key in ((4 if epi == EPI_SWIGLU and mx_out else 3) if act_mx else 4, 3, 1):   # tuned MX plans, then fp8
         pick = _mg_table_row(M, N, K, epi, key)
         if pick is not None and mgemm_valid(pick[1], M, N, K, epi, mode, pick[2], mx_out):
             return pick[1], pick[2]
@@ -744,15 +745,16 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
     nwg = mgemm_nwg(cfg, M, N, K, epi, fp8, grid)
     tiles, cmax, n_ws = _mg_plan_info(M, N, K, epi, mode, cfg, nwg)
     if mode == 1 and rms_eps is not None:
-        raise ValueError("mgemm: the RMS prologue needs bf16 activations")
+        raise ValueError("mgemm: the RMS prologue needs bf16 or MX activations")
     if res is not None and (epi != EPI_BF16 or res.shape != (M, N)):
         raise ValueError("mgemm: residual epilogue needs a bf16 [M, N] residual and the bf16 epilogue")
     mxo = None
     if mx_out:
-        if res is not None or N % 128:
-            raise ValueError("mgemm: MX output is the SwiGLU epilogue's (N % 128 == 0)")
+        if N % 128 or (epi == EPI_SWIGLU) == (res is not None):
+            raise ValueError("mgemm: MX output is the SwiGLU or the residual epilogue's (N % 128 == 0)")
         mxo = MxAct.empty(M, N, x.device)
-        out = mxo.q   # (not written as bf16)
+        if res is None:
+            out = mxo.q   # SwiGLU: not written as bf16
     if out is None:
         out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
     ws = torch.empty(n_ws, dtype=F32, device=x.device) if n_ws > 0 else None
@@ -764,7 +766,7 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
         if act.shape != (M, K) or not act.q.is_cuda:
             raise ValueError(f"mgemm: MX activations {tuple(act.shape)} for x {(M, K)}")
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, act.q.data_ptr(), w.q.data_ptr(),
-                       act.e.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 3, cfg, nwg, cmax, rp, 0, 0.0, -1, oq, oe)
+                       act.e.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 3, cfg, nwg, cmax, rp, rms, eps, -1, oq, oe)
     elif mode == 2:
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"), w.q.data_ptr(),
                        0, w.scale.data_ptr(), M, N, K, epi, 2, cfg, nwg, cmax, rp, rms, eps, -1)
@@ -776,7 +778,9 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"),
                        _chk(w, BF16, "w"), 0, 0, M, N, K, epi, 0, cfg, nwg, cmax, rp, rms, eps, -1)
     del ws
-    return mxo if mxo is not None else out
+    if mxo is not None:
+        return (out, mxo) if res is not None else mxo
+    return out
 
 
 # ----------------------------------------------------------------------------- big-tile MFMA GEMM (prefill rows)
@@ -1009,11 +1013,16 @@ def mx_rows(M: int, w) -> bool:
 
 
 def _gemm_mx(act: MxAct, w, epi: int, res: Optional[torch.Tensor] = None,
-             out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """An MX-activation GEMM on the routed kernel (mgemm MX mode / pgemm MX mode)."""
+             out: Optional[torch.Tensor] = None, mx_res: bool = False):
+    """An MX-activation GEMM on the routed kernel (mgemm MX mode / pgemm MX mode).  ``mx_res`` (residual
+    epilogue on mgemm): returns (res, MxAct of the new residual stream), or (res, None) where no plan writes it."""
     M, K = act.shape
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     kern, plan = gemm_route(M, N, K, epi, True)
+    if mx_res:
+        if kern == "mgemm" and mgemm_mx_plan(M, N, K, epi, True, True) is not None:
+            return mgemm(act, w, epi, res=res, out=out, mx_out=True)
+        return _gemm_mx(act, w, epi, res=res, out=out), None
     if kern == "pgemm":
         cfg, sp, gm = plan
         return pgemm(act, w, epi, cfg=cfg, splits=sp, group_m=gm, res=res, out=out)
@@ -1078,15 +1087,28 @@ RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "64"))
 RMS_UNFUSED_MIN_N = int(os.environ.get("K8S_RMS_UNFUSED_MIN_N", "8192"))
 
 
-def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16, mx_consumer=None):
+def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16, mx_consumer=None, x_mx: Optional[MxAct] = None):
     """epi(rmsnorm(r) @ w.T) for M > GEMV_MAX_M rows with the norm gamma folded into ``w`` (LlamaModel folds it at
     load time): on the mgemm route the RMS statistics are the GEMM's prologue (no norm kernel, no normalised
     copy of the activations); otherwise a plain RMSNorm (unit gamma) + the routed GEMM.  ``mx_consumer`` (SwiGLU, fp8
     weights): the weight of the GEMM that consumes the result (down); where :func:`mx_rows` holds for it, the
-    epilogue writes the result as an :class:`MxAct`."""
+    epilogue writes the result as an :class:`MxAct`.  ``x_mx``: the MX copy of ``r`` its producer wrote (residual
+    epilogue): the GEMM runs on it, the RMS statistics taken from the dequantized MX values in its prologue."""
     M, K = r.shape
     mx_out = (mx_consumer is not None and epi == EPI_SWIGLU and _is_fp8(w) and mx_rows(M, mx_consumer)
               and (w.shape[0] // 2) % 128 == 0)
+    if x_mx is not None and _is_fp8(w):
+        if not x_mx.is_cuda:
+            xa = x_mx.dequant(torch.float32)
+            xa = xa * torch.rsqrt(xa.pow(2).mean(-1, keepdim=True) + eps)
+            if epi == EPI_SWIGLU:
+                y = ref.linear_swiglu(xa, w).to(BF16)
+                return quantize_act_mx(y) if mx_out else y
+            return ref.linear(xa, w, F32 if epi == EPI_F32 else BF16)
+        n_out = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
+        if gemm_route(M, n_out, K, epi, True)[0] == "mgemm" and \
+                mgemm_mx_plan(M, n_out, K, epi, True, mx_out) is not None:
+            return mgemm(x_mx, w, epi, rms_eps=eps, mx_out=mx_out)
     if _is_fp8(w) and w8_rows(M):
         # W8 rows: mgemm's RMS prologue on the un-normalised bf16 rows against the fp8 weights (no quantize launch)
         if _gpu(r):
@@ -1131,19 +1153,29 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16, mx_consumer=
     return linear(x, w, F32 if epi == EPI_F32 else None)
 
 
-def linear_residual(x, w, res: torch.Tensor) -> torch.Tensor:
+def linear_residual(x, w, res: torch.Tensor, mx_next=None):
     """res + x @ w.T (bf16), written into ``res`` (the residual stream).  mgemm route: the add is the GEMM's
     epilogue; otherwise GEMM + add.  ``x``: bf16, or an :class:`MxAct` (fp8 weights); bf16 rows of
-    :func:`mx_rows` are turned into MX first (the producers that write MX themselves pass an MxAct)."""
+    :func:`mx_rows` are turned into MX first (the producers that write MX themselves pass an MxAct).
+    ``mx_next``: the weight of the pre-norm projection that reads the new residual stream next; then returns
+    (res, MxAct or None) -- the residual epilogue writes the stream's MX copy where :func:`mx_rows` holds for it."""
     M, K = x.shape
+    want_mx = mx_next is not None and mx_rows(M, mx_next) and res.shape[1] % 128 == 0
     if not isinstance(x, MxAct) and mx_rows(M, w) and K % 128 == 0:
         x = quantize_act_mx(x.contiguous())
     if isinstance(x, MxAct):
         if not x.is_cuda:
             y = ref.linear(x.dequant(torch.float32), w).to(BF16)
             res.copy_((res.float() + y.float()).to(res.dtype))
+            if mx_next is not None:
+                return res, (quantize_act_mx(res) if want_mx else None)
             return res
+        if mx_next is not None:
+            return _gemm_mx(x, w, EPI_BF16, res=res, out=res, mx_res=want_mx) if want_mx else \
+                (_gemm_mx(x, w, EPI_BF16, res=res, out=res), None)
         return _gemm_mx(x, w, EPI_BF16, res=res, out=res)
+    if mx_next is not None:
+        return linear_residual(x, w, res), None
     if _gpu(x) and M > GEMV_MAX_M:
         y = _gemm(x.contiguous(), w, EPI_BF16, res=res, out=res)
         if y is not None:

@@ -183,3 +183,55 @@ def test_decode_attention_mx_output_is_the_quantized_bf16_output(B, ctx, part, m
     q, e = ref.quantize_mx(y.cpu())
     assert torch.equal(mx.blocks().cpu(), e)
     assert torch.equal(mx.q.cpu(), q)
+
+
+def test_mgemm_residual_mx_copy_and_mx_rms_prologue():
+    """The residual epilogue's MX copy equals quantize_act_mx of the bf16 residual stream it wrote (bit for bit),
+    and an MX-mode GEMM with the RMS prologue matches the oracle on the dequantized rows (RMS of the dequantized
+    values), with bf16 and SwiGLU (+ MX output) epilogues."""
+    K, N, eps = 1024, 256, 1e-5
+    wo = _weights(N, K, 21)
+    n_cfg = 0
+    for cfg in range(len(ops.mgemm_configs())):
+        if not ops.mgemm_valid(cfg, 64, N, K, ops.EPI_BF16, 3, 1, mx_out=True):
+            continue
+        n_cfg += 1
+        for M in (19, 64):
+            act = ops.quantize_act_mx(_act(M, K, cfg + 3 * M, spread=False).to(DEV))
+            for grid in (1, 4, -256):
+                if not ops.mgemm_valid(cfg, M, N, K, ops.EPI_BF16, 3, grid, mx_out=True):
+                    continue
+                res = ((torch.rand(M, N, device=DEV) * 2 - 1) * 8).to(torch.bfloat16)
+                want = ops.mgemm(act, wo, ops.EPI_BF16, cfg=cfg, grid=grid, res=res.clone(), out=None)
+                out, mx = ops.mgemm(act, wo, ops.EPI_BF16, cfg=cfg, grid=grid, res=res.clone(), out=None,
+                                    mx_out=True)
+                # (the two epilogues may contract acc * scale + res differently: 1 bf16 ulp at most)
+                torch.testing.assert_close(out.float(), want.float(), rtol=2 ** -7, atol=1e-6)
+                q, e = ref.quantize_mx(out.cpu())
+                assert torch.equal(mx.blocks().cpu(), e) and torch.equal(mx.q.cpu(), q), f"cfg {cfg} grid {grid}"
+    assert n_cfg >= 4
+    # MX rows + RMS prologue
+    M = 48
+    x = (_act(M, K, 5, spread=False).float() * 3).to(torch.bfloat16).to(DEV)
+    act = ops.quantize_act_mx(x)
+    xa = ref.dequant_mx(act.q.cpu(), act.e.cpu())
+    inv = torch.rsqrt(xa.pow(2).mean(-1, keepdim=True) + eps)
+    wq = _weights(N, K, 23)
+    gu = _weights(2 * N, K, 24)
+    n_cfg = 0
+    for cfg in range(len(ops.mgemm_configs())):
+        if not ops.mgemm_valid(cfg, M, N, K, ops.EPI_BF16, 3):
+            continue
+        n_cfg += 1
+        y = ops.mgemm(act, wq, ops.EPI_BF16, cfg=cfg, grid=1, rms_eps=eps).float().cpu()
+        exp = (xa * inv) @ ref.dequant_fp8(wq.q.cpu(), wq.scale.cpu()).t()
+        assert (y - exp).abs().max().item() <= 1e-2 * exp.abs().max().item(), f"rms cfg {cfg}"
+        if ops.mgemm_valid(cfg, M, N, K, ops.EPI_SWIGLU, 3, 1, mx_out=True):
+            ys = ops.mgemm(act, gu, ops.EPI_SWIGLU, cfg=cfg, grid=1, rms_eps=eps)
+            mx = ops.mgemm(act, gu, ops.EPI_SWIGLU, cfg=cfg, grid=1, rms_eps=eps, mx_out=True)
+            q, e = ref.quantize_mx(ys.cpu())
+            assert torch.equal(mx.blocks().cpu(), e) and torch.equal(mx.q.cpu(), q), f"rms swiglu cfg {cfg}"
+            expg = (xa * inv) @ ref.dequant_fp8(gu.q.cpu(), gu.scale.cpu()).t()
+            expg = torch.nn.functional.silu(expg[:, :N]) * expg[:, N:]
+            assert (ys.float().cpu() - expg).abs().max().item() <= 1e-2 * expg.abs().max().item(), f"swiglu {cfg}"
+    assert n_cfg >= 6
