@@ -93,7 +93,8 @@ int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, cons
                int stop_eos_tok, int* stop_done, hipStream_t s);
 long long k8s_sample_scratch_bytes(int B);
 long long k8s_sample_nucleus_bytes(int B, int shards);
-int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab, hipStream_t s);
+int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab, void* oq, void* oe,
+                  hipStream_t s);
 int k8s_silu_mul(void* out, const void* gu, int T, int I, hipStream_t s);
 int k8s_prefetch(const void* p, long long bytes, int blocks, void* sink, hipStream_t s);
 int k8s_hash_init(void* out, int rows, int cols, long long gcols, long long row0, long long col0, uint32_t seed,
@@ -338,9 +339,11 @@ PYBIND11_MODULE(K8S_MODULE_NAME, m) {
   m.def("host_mapped_free", [](uintptr_t p) { (void)hipHostFree(reinterpret_cast<void*>(p)); });
   m.def("sample_scratch_bytes", [](int B) { return k8s_sample_scratch_bytes(B); });
   m.def("sample_nucleus_bytes", [](int B, int shards) { return k8s_sample_nucleus_bytes(B, shards); });
-  m.def("embedding", [](uintptr_t out, uintptr_t ids, uintptr_t table, int T, int H, int vocab, int64_t s) {
-    check(k8s_embedding(P(out), P<int>(ids), P(table), T, H, vocab, S(s)), "embedding");
-  });
+  m.def("embedding", [](uintptr_t out, uintptr_t ids, uintptr_t table, int T, int H, int vocab, int64_t s,
+                        uintptr_t oq, uintptr_t oe) {
+    check(k8s_embedding(P(out), P<int>(ids), P(table), T, H, vocab, P(oq), P(oe), S(s)), "embedding");
+  }, py::arg("out"), py::arg("ids"), py::arg("table"), py::arg("T"), py::arg("H"), py::arg("vocab"), py::arg("s"),
+     py::arg("oq") = 0, py::arg("oe") = 0);
   m.def("prefetch", [](uintptr_t p, long long bytes, int blocks, uintptr_t sink, int64_t s) {
     check(k8s_prefetch(P(p), bytes, blocks, P(sink), S(s)), "prefetch");
   });

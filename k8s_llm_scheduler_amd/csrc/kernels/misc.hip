@@ -5,16 +5,38 @@
 #define K8S_CHK_THIS_UNIT 1
 namespace k8sllm {
 
-// out[t, :] = table[ids[t], :]   (rows of H bf16, H % 8 == 0)
+// out[t, :] = table[ids[t], :]   (rows of H bf16, H % 8 == 0).  oq / oe (H % 128 == 0): also the rows as MX e4m3
+// (K16; the first pre-norm fp8 projection's input): 4 adjacent threads hold one 32-value block.
 __global__ void embedding_kernel(bf16_t* __restrict__ out, const int* __restrict__ ids,
-                                 const bf16_t* __restrict__ table, int H, int vocab) {
+                                 const bf16_t* __restrict__ table, int H, int vocab, uint8_t* __restrict__ oq,
+                                 uint8_t* __restrict__ oe) {
   const int t = blockIdx.x;
   int id = ids[t];
   K8S_CHECK_RANGE(id, 0, K8S_CHK_TOKEN, 0);
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
   const u32x4* src = reinterpret_cast<const u32x4*>(table + (size_t)id * H);
   u32x4* dst = reinterpret_cast<u32x4*>(out + (size_t)t * H);
-  for (int i = threadIdx.x; i < H / 8; i += blockDim.x) dst[i] = src[i];
+  for (int i = threadIdx.x; i < H / 8; i += blockDim.x) {
+    const u32x4 v = src[i];
+    dst[i] = v;
+    if (oq != nullptr) {   // (uniform branch; H / 8 and blockDim are multiples of 4: a block's threads stay together)
+      float f[8], amax = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[2 * j] = lo_bf(v[j]);
+        f[2 * j + 1] = hi_bf(v[j]);
+        amax = fmaxf(amax, fmaxf(fabsf(f[2 * j]), fabsf(f[2 * j + 1])));
+      }
+      amax = fmaxf(amax, __shfl_xor(amax, 1, WAVE));
+      amax = fmaxf(amax, __shfl_xor(amax, 2, WAVE));
+      const uint32_t e = mx_e8m0(amax);
+      const float inv = mx_inv_scale(e);
+      uint32_t* q = reinterpret_cast<uint32_t*>(oq + (size_t)t * H + (size_t)i * 8);
+      q[0] = mx_pack4(f[0], f[1], f[2], f[3], inv);
+      q[1] = mx_pack4(f[4], f[5], f[6], f[7], inv);
+      if ((i & 3) == 0) oe[mx_scale_off(t, i >> 2, gridDim.x)] = (uint8_t)e;
+    }
+  }
 }
 
 // out[t, j] = silu(gu[t, j]) * gu[t, I + j]
@@ -77,11 +99,12 @@ extern "C" int k8s_prefetch(const void* p, long long bytes, int blocks, void* si
   return (int)hipGetLastError();
 }
 
-extern "C" int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab,
-                             hipStream_t stream) {
+extern "C" int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab, void* oq,
+                             void* oe, hipStream_t stream) {
   if (T <= 0) return 0;
-  if (H % 8) return -1;
-  embedding_kernel<<<T, 256, 0, stream>>>((bf16_t*)out, ids, (const bf16_t*)table, H, vocab);
+  if (H % 8 || (oq != nullptr && (H % 128 || oe == nullptr))) return -1;
+  embedding_kernel<<<T, 256, 0, stream>>>((bf16_t*)out, ids, (const bf16_t*)table, H, vocab, (uint8_t*)oq,
+                                          (uint8_t*)oe);
   return (int)hipGetLastError();
 }
 

@@ -208,16 +208,18 @@ class LlamaModel:
         return self.cfg.num_layers * 2 * block_size * self.nkv * self.D * torch.finfo(self.dtype).bits // 8
 
     # ------------------------------------------------------------------ forward
-    def _layers_folded(self, h: torch.Tensor, attn) -> torch.Tensor:
+    def _layers_folded(self, h, attn) -> torch.Tensor:
         """All decoder layers with the norm gammas folded into the weights (the default).  The residual stream
         ``r`` feeds the pre-norm projections directly: their RMS statistics are the GEMM's prologue
         (ops.linear_rms), and the row-parallel projections add their output into ``r`` in the GEMM epilogue
         (TP=1, ops.linear_residual) or in the all-reduce (TP>1, the xGMI kernels fuse it) -- no RMSNorm or
         residual-add kernels between the GEMMs.  Returns the final residual stream."""
         eps = self.cfg.rms_eps
+        r_mx = None   # fp8 GEMM rows at TP = 1: the MX copy of r written by its producer (K16)
+        if isinstance(h, tuple):   # (embedding rows, their MX copy)
+            h, r_mx = h
         r = h.clone()
         tp1 = self.tp.world == 1 or self.tp.simulate
-        r_mx = None   # fp8 GEMM rows at TP = 1: the MX copy of r written by the residual epilogue (K16)
         L = len(self.layers)
         for l, w in enumerate(self.layers):
             qkv = ops.linear_rms(r, w.wqkv, eps, x_mx=r_mx)
@@ -463,7 +465,8 @@ class LlamaModel:
             return a.view(B, self.nq * self.D)
 
         if self.norm_folded:
-            return self._logits_folded(self._layers_folded(ops.embedding(tokens, self.embed), attn))
+            mx0 = (self.tp.world == 1 or self.tp.simulate) and ops.mx_rows(B, self.layers[0].wqkv)
+            return self._logits_folded(self._layers_folded(ops.embedding(tokens, self.embed, mx=mx0), attn))
         h, res = self._layers(ops.embedding(tokens, self.embed), attn)
         return self._logits(h, res)
 

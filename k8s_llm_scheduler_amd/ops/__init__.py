@@ -1429,14 +1429,18 @@ def silu_mul(gu: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+def embedding(ids: torch.Tensor, table: torch.Tensor, mx: bool = False):
+    """table[ids] (bf16).  ``mx``: returns (rows, their MX e4m3 copy) -- the first fp8 pre-norm projection's input,
+    written by the gather itself (K16)."""
     if not _gpu(ids, table):
-        return ref.embedding(ids, table)
+        out = ref.embedding(ids, table)
+        return (out, quantize_act_mx(out)) if mx else out
     T = ids.numel()
     out = torch.empty(T, table.shape[1], dtype=table.dtype, device=table.device)
+    mxo = MxAct.empty(T, table.shape[1], table.device) if mx else None
     native().embedding(out.data_ptr(), _chk(ids, I32, "ids"), _chk(table, BF16, "table"), T, table.shape[1],
-                       table.shape[0], -1)
-    return out
+                       table.shape[0], -1, mxo.q.data_ptr() if mx else 0, mxo.e.data_ptr() if mx else 0)
+    return (out, mxo) if mx else out
 
 
 # ----------------------------------------------------------------------------- sampling

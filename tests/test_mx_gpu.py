@@ -235,3 +235,13 @@ def test_mgemm_residual_mx_copy_and_mx_rms_prologue():
             expg = torch.nn.functional.silu(expg[:, :N]) * expg[:, N:]
             assert (ys.float().cpu() - expg).abs().max().item() <= 1e-2 * expg.abs().max().item(), f"swiglu {cfg}"
     assert n_cfg >= 6
+
+
+def test_embedding_mx_copy_is_the_quantized_rows():
+    g = torch.Generator(device="cpu").manual_seed(9)
+    table = (torch.randn(1000, 1024, generator=g) * 0.3).to(torch.bfloat16).to(DEV)
+    ids = torch.randint(0, 1000, (37,), generator=g, dtype=torch.int32).to(DEV)
+    out, mx = ops.embedding(ids, table, mx=True)
+    assert torch.equal(out, ops.embedding(ids, table))
+    q, e = ref.quantize_mx(out.cpu())
+    assert torch.equal(mx.blocks().cpu(), e) and torch.equal(mx.q.cpu(), q)

@@ -11,9 +11,10 @@ copies of the weight to exceed the 256 MiB Infinity Cache (weights are cold in t
 --w8 tunes mgemm's W8 mode (fp8 weights, bf16 activations; table key fp8 = 2) against the per-token e4m3 path it
 replaces (quantize_act_fp8 + the tuned fp8 mgemm plan).
 
---mx tunes the K16 MX modes (fp8 weights): O / down with MX e4m3 activations (table key fp8 = 3; compared with the
-per-token path they replace: quantize_act_fp8 + the tuned fp8 plan) and gate/up with the SwiGLU epilogue writing MX
-output (key fp8 = 4; compared with the same GEMM writing bf16, per-token activations quantized outside both).
+--mx tunes the K16 MX modes (fp8 weights) as the decode layer runs them: QKV with MX activations and the RMS
+prologue, O / down with MX activations and the residual epilogue writing the stream's MX copy (table key fp8 = 3),
+gate/up with MX activations, the RMS prologue and MX SwiGLU output (key fp8 = 4); each compared with the per-token
+path it replaces (quantize_act_fp8 + the tuned fp8 plan).
 
 --write merges the winners into engine/assets/mgemm_gfx950.json (the table ops.mgemm_plan reads).
 """
@@ -75,11 +76,11 @@ def time_graph(fn, copies: int) -> float:
     return best
 
 
-def candidates(M, N, K, epi, fp8):
+def candidates(M, N, K, epi, fp8, mx_out=False):
     cfgs = ops.mgemm_configs()
     out = []
-    mx_out = fp8 == 4
-    mode = 1 if mx_out else fp8
+    mx_out = mx_out or fp8 == 4
+    mode = 3 if fp8 == 4 else fp8
     for c, (bm, bn, _th, _lds, _sw, rb) in enumerate(cfgs):
         steps = K * (1 if fp8 else 2) // rb
         if fp8 in (2, 3, 4) and not ops.mgemm_valid(c, M, N, K, epi, mode, 1, mx_out):
@@ -102,10 +103,8 @@ def candidates(M, N, K, epi, fp8):
 def lib_fn(x, Ws, epi, fp8):
     def f(i):
         w = Ws[i]
-        if fp8 in (2, 3):   # W8 / MX tuning: the per-token e4m3 path it replaces (quantize + the tuned fp8 plan)
+        if fp8 in (2, 3, 4):   # W8 / MX tuning: the per-token e4m3 path it replaces (quantize + the tuned fp8 plan)
             return ops.mgemm(x, w, epi)
-        if fp8 == 4:        # MX output tuning: the same GEMM writing bf16 (per-token activations given)
-            return ops.mgemm(x, w, epi, act=ACT[0])
         if fp8:
             y = ops._fp8_gemm(x, w)
             if epi == ops.EPI_F32:
@@ -151,7 +150,7 @@ def main() -> int:
             if a.only and name not in a.only:
                 continue
             if a.mx:
-                if name in ("qkv", "lm_head"):   # per-token (RMS-folded) inputs: nothing MX to tune
+                if name == "lm_head":   # bf16 residual stream + the final norm: no MX input
                     continue
                 a.fp8 = 4 if epi == ops.EPI_SWIGLU else 3
             wrows = 2 * N if epi == ops.EPI_SWIGLU else N
@@ -164,15 +163,18 @@ def main() -> int:
                 del w
             for M in a.m:
                 x = torch.empty(M, K, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1)
-                ACT[0] = (ops.quantize_act_mx(x) if a.fp8 == 3 else ops.quantize_act_fp8(x) if a.fp8 == 4
-                          else None)
+                ACT[0] = ops.quantize_act_mx(x) if a.fp8 in (3, 4) else None
+                res_mx = a.mx and name in ("o_proj", "down")   # residual epilogue + the stream's MX copy
+                rms_mx = a.mx and name in ("qkv", "gate_up")   # MX rows + the RMS prologue
+                RES = torch.empty(M, N, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1) if res_mx else None
                 lib_us = time_graph(lib_fn(x, Ws, epi, a.fp8), copies)
                 best = (float("inf"), None)
 
                 def run(i, c, gr):
-                    return ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr, w8=a.fp8 == 2, act=ACT[0], mx_out=a.fp8 == 4)
+                    return ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr, w8=a.fp8 == 2, act=ACT[0],
+                                     mx_out=a.fp8 == 4 or res_mx, res=RES, rms_eps=1e-5 if rms_mx else None)
 
-                for c, gr in candidates(M, N, K, epi, a.fp8):
+                for c, gr in candidates(M, N, K, epi, a.fp8, res_mx):
                     us = time_graph(lambda i, c=c, gr=gr: run(i, c, gr), copies)
                     if a.verbose:
                         bm, bn = ops.mgemm_configs()[c][:2]
@@ -188,7 +190,7 @@ def main() -> int:
                         gfn = lambda i: ops.linear(x, Ws[i], out_dtype=torch.float32 if epi == ops.EPI_F32 else None)
                     gemv_us = round(time_graph(gfn, copies), 2)
                 hc = (ops.mgemm_heuristic(M, N, K, epi, a.fp8) if a.fp8 in (0, 1, 2) else
-                      ops.mgemm_mx_plan(M, N, K, epi, a.fp8 == 3, a.fp8 == 4))
+                      ops.mgemm_mx_plan(M, N, K, epi, True, a.fp8 == 4 or res_mx))
                 h_us = time_graph(lambda i: run(i, hc[0], hc[1]), copies)
                 us, (c, ks) = best
                 plans[f"{ops._mg_bucket(M)},{N},{K},{epi},{int(a.fp8)}"] = [c, ks, round(us, 2), round(lib_us, 2)]
