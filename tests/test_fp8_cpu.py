@@ -133,3 +133,52 @@ def test_mx_rows_route_o_and_down_inputs_through_mx_e4m3():
     # bf16 rows of the MX range are quantized to MX before the fp8 GEMM (the attention output's path)
     out2 = ops.linear_residual(bf, wd, res.clone())
     torch.testing.assert_close(out2.float(), want.float())
+
+
+def _fp8_tp_worker(rank, world, port, q, ids):
+    import os
+
+    import torch.distributed as dist
+
+    from k8s_llm_scheduler_amd.parallel import TPGroup
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tp = TPGroup(rank, world, dist.group.WORLD, "gloo")
+        m = LlamaModel(PRESETS["tiny"], tp, device="cpu", seed=3, max_model_len=256, weight_dtype="fp8")
+        lg, _ = _prefill(m, ids)
+        if rank == 0:
+            q.put(lg.float().flatten())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fp8_mx_rows_under_tensor_parallel_track_tp1():
+    """A 24-token fp8 prefill (GEMM rows: the O / down inputs travel as MX e4m3, the SwiGLU output is produced in MX)
+    on TP = 2 gloo ranks tracks TP = 1: the 32-value blocks never straddle a shard boundary, so each rank's MX rows
+    are the TP = 1 rows' own slices."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    ids = [(37 * i + 11) % 16000 for i in range(24)]
+    m1 = LlamaModel(PRESETS["tiny"], device="cpu", seed=3, max_model_len=256, weight_dtype="fp8")
+    assert ops.mx_rows(24, m1.layers[0].wo) == ops.MX_ON
+    lg1, _ = _prefill(m1, ids)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fp8_tp_worker, args=(r, 2, port, q, ids)) for r in range(2)]
+    for p in procs:
+        p.start()
+    lg2 = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    cos = torch.nn.functional.cosine_similarity(lg1.float().flatten(), lg2, dim=0)
+    assert float(cos) > 0.995, float(cos)
