@@ -67,7 +67,9 @@ class GraphCaptureMixin:
 
     def _capture_graphs(self, buckets: Optional[Sequence[int]], nucleus: bool) -> None:
         assert not self.running and not self.prefilling, "capture needs an idle engine"
-        buckets = buckets or [b for b in BUCKETS if b <= self.max_batch]
+        # (a max_batch that is not a bucket is its own top bucket: _bucket returns it for the rows above the last
+        # bucket below it, which otherwise decoded eagerly)
+        buckets = buckets or sorted({b for b in BUCKETS if b <= self.max_batch} | {self.max_batch})
         stream = torch.cuda.Stream(self.device)
         for B in sorted(set(buckets)):
             for mc in self._ctx_classes():

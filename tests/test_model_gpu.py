@@ -101,6 +101,47 @@ def test_batched_decode_matches_cpu_reference(models, gemm, monkeypatch):
     torch.testing.assert_close(outs["cuda"].cpu(), outs["cpu"], atol=6e-2, rtol=5e-2)
 
 
+def test_batched_fp8_decode_on_mx_rows_matches_cpu_reference():
+    """B = 24 fp8 rows: every projection input travels as MX e4m3 written by its producer (embedding, attention,
+    SwiGLU and residual epilogues; the RMS statistics from the extra MFMA) -- vs the CPU model, which rounds the
+    activations the same way."""
+    g = LlamaModel(CFG, device="cuda", seed=6, max_model_len=2048, weight_dtype="fp8")
+    c = LlamaModel(CFG, device="cpu", seed=6, max_model_len=2048, weight_dtype="fp8")
+    B, bs, per = 24, 16, 24
+    assert ops.mx_rows(B, g.layers[0].wo) == ops.MX_ON
+    lens = [5 + 13 * i for i in range(B)]
+    outs = {}
+    for m in (g, c):
+        dev = m.device
+        m.allocate_kv(B * per + 8, bs)
+        bt = torch.zeros(B, 32, dtype=torch.int32)
+        t = lambda x: torch.tensor(x, dtype=torch.int32, device=dev)
+        for i, T in enumerate(lens):
+            blocks = list(range(i * per, (i + 1) * per))
+            bt[i, :per] = torch.tensor(blocks)
+            ids = [(37 * i + 11 * p) % 16000 for p in range(T)]
+            slots = [blocks[p // bs] * bs + p % bs for p in range(T)]
+            m.forward_prefill(t(ids), t(list(range(T))), t(slots), t([0, T]), t([T]), bt[i:i + 1].to(dev), T,
+                              t([T - 1]))
+        ctx = t([T + 1 for T in lens])
+        outs[dev.type] = m.forward_decode(t([(7 * i) % 16000 for i in range(B)]), ctx, bt.to(dev), 2048)
+    torch.testing.assert_close(outs["cuda"].cpu(), outs["cpu"], atol=1.5e-1, rtol=5e-2)
+
+
+def test_engine_fp8_batched_decode_graph_equals_eager():
+    """An fp8 engine decoding 20 sequences (MX rows) gives the same tokens from the captured decode graphs as from
+    eager steps."""
+    eng = build_engine("tiny", device="cuda:0", max_batch=24, num_blocks=1024, max_model_len=1024, seed=5,
+                       weight_dtype="fp8")
+    p = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    prompts = [f"schedule pod {i} onto the least loaded node" for i in range(20)]
+    graphed = eng.generate(prompts, p)
+    assert eng.stats["graph_replays"] > 0
+    eng.use_graphs = False
+    eager = eng.generate(prompts, p)
+    assert [o.token_ids for o in graphed] == [o.token_ids for o in eager]
+
+
 @pytest.mark.parametrize("fp8", [False, True])
 def test_long_prefill_on_big_tile_gemms_matches_cpu_reference(fp8):
     """A 600-token prefill: every projection has M = 600 >= PG_MIN_M rows, so gemm_route puts them on the big-tile
