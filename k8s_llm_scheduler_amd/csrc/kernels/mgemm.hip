@@ -41,6 +41,8 @@
 //    span is a multiple of 32), or of one fragment in each of two neighbouring waves (16 features per wave: the
 //    row absmax goes through LDS, one barrier): a shuffle max gives the block's E8M0 scale and every lane stores
 //    its e4m3 bytes -- the down projection's input is produced already quantized.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace k8sllm {
@@ -99,6 +101,7 @@ struct MgArgs {
   const bf16_t* res;     // optional residual (bf16 [M][N_out], may alias out): out = acc + res  (bf16 epilogue)
   int rms;               // 1: RMSNorm prologue -- out scaled by 1 / rms(x row) (the gamma is folded into W)
   float eps;
+  int rms_mfma;          // bf16 / W8 rows: the row sums of squares from x . x^T on the MFMA (1) or v_dot2 (0)
 };
 
 // Wave layout: WM x WN waves own (BM / WM) x (BN / WN) output sub-tiles; WK waves share each
@@ -253,9 +256,10 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     float ss[FM];   // RMS prologue: this lane's share of sum(x^2) of its fragment rows
 #pragma unroll
     for (int j = 0; j < FM; ++j) ss[j] = 0.f;
-    f32x4 accsq[MX ? FM : 1];   // MX RMS prologue: x . x^T per row fragment (diagonal = sums of squares)
+    f32x4 accsq[FM];   // RMS prologue on the MFMA: x . x^T per row fragment (diagonal = sums of squares)
 #pragma unroll
-    for (int j = 0; j < (MX ? FM : 1); ++j) accsq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FM; ++j) accsq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool rms_mfma = MX || a.rms_mfma != 0;
     const bool do_rms = (!FP8 || MX) && a.rms != 0;   // MX: the squares of the dequantized e4m3 values
     // 8 e4m3 weights -> the bf16x8 A operand (exact; the row scale is applied in the epilogue)
     auto w8_frag = [](long q) {
@@ -297,7 +301,16 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
 #pragma unroll
             for (int j = 0; j < FM; ++j)
               acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], bfr[j], acc[f][j], 0, 0, 0);
-          if (do_rms) {   // the WN waves of a row block hold the same x fragments: each squares 1/WN of them
+          if (do_rms && rms_mfma) {
+            // one more MFMA per x fragment, x . x^T (diagonal = the rows' sums of squares), in wave wn = 0 of a row
+            // block; a scalar branch (readfirstlane), since an MFMA ignores EXEC.  In the weight-streaming regime the
+            // MFMA pipe is idle enough that this costs less than v_dot2 squares in every k-step (or a norm launch)
+            if (__builtin_amdgcn_readfirstlane(wn) == 0) {
+#pragma unroll
+              for (int j = 0; j < FM; ++j)
+                accsq[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], bfr[j], accsq[j], 0, 0, 0);
+            }
+          } else if (do_rms) {   // the WN waves of a row block hold the same x fragments: each squares 1/WN of them
 #pragma unroll
             for (int j = 0; j < FM; ++j)
 #pragma unroll
@@ -409,11 +422,9 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     }
 
     // ---- RMS prologue: row sums of squares over this segment's k-steps -> rss[wk][row]
-    if constexpr (MX) {   // the diagonal of x . x^T: C[4 g + i][li] with 4 g + i == li
-      if (do_rms) {
+    if (do_rms && rms_mfma) {   // the diagonal of x . x^T: C[4 g + i][li] with 4 g + i == li
 #pragma unroll
-        for (int j = 0; j < FM; ++j) ss[j] = (g == (li >> 2)) ? accsq[j][li & 3] : 0.f;
-      }
+      for (int j = 0; j < FM; ++j) ss[j] = (g == (li >> 2)) ? accsq[j][li & 3] : 0.f;
     }
     if (do_rms) {
 #pragma unroll
@@ -882,6 +893,12 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.res = static_cast<const bf16_t*>(res);
   a.rms = rms;
   a.eps = eps;
+  // RMS prologue on the MFMA for the wide projections (>= 8192 output features: the 70B TP = 1 / 2 QKV, gate/up),
+  // v_dot2 squares for the narrow ones, where the extra MFMA is as large as the tile's own work (one TP = 8 rank:
+  // batch-64 decode 7.66 ms/step with v_dot2, 7.78 with the MFMA; TP = 1: 31.98 -> 30.72, profiles/rms_mfma_ab_r5.txt).
+  // K8S_RMS_MFMA = 0 / 1 forces one form.
+  static const int rms_mfma_env = [] { const char* e = getenv("K8S_RMS_MFMA"); return e ? atoi(e) : -1; }();
+  a.rms_mfma = rms_mfma_env >= 0 ? rms_mfma_env : (N_out >= 8192 ? 1 : 0);
   a.out = out;
   a.ws = ws;
   a.cnt = tickets;

@@ -1078,12 +1078,12 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
 
 
 # bf16 rows in (SGEMV_MAX_M, RMS_PROLOGUE_MAX_UNFUSED] with at least RMS_UNFUSED_MIN_N output features take a
-# separate RMSNorm + plain GEMM instead of mgemm's RMS prologue (K8S_RMS_UNFUSED_MAX_M, default 64; 0 = always the
-# prologue).  Measured (profiles/bench_r4_rms_prologue_ab.txt): the TP = 1 projections (QKV 10240, gate/up 28672
-# features) are faster that way -- batch 64 decode 31.54-31.63 -> 31.02-31.04 ms/step, batch 32 28.28 -> 28.10 --
-# while one TP = 8 rank's (1280 / 3584 features) is slower (batch 64 7.56-7.62 -> 8.23-8.26 ms/step: the norm launch
-# costs more than those small GEMMs' prologue); a 245-row prefill was unchanged, so the prologue keeps > 64 rows.
-RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "64"))
+# separate RMSNorm + plain GEMM instead of mgemm's RMS prologue (K8S_RMS_UNFUSED_MAX_M; 0 = always the prologue, the
+# default since round 5).  Round 4 (profiles/bench_r4_rms_prologue_ab.txt) measured the separate norm faster for the
+# TP = 1 projections (QKV 10240, gate/up 28672 features) while their prologue squared x with v_dot2 in every k-step;
+# with the sums of squares taken from one extra MFMA (x . x^T diagonal, mgemm.hip) the prologue wins there too:
+# batch 64 30.85 -> 30.72 ms/step, batch 32 28.18 -> 27.52 (profiles/rms_mfma_ab_r5.txt).
+RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "0"))
 RMS_UNFUSED_MIN_N = int(os.environ.get("K8S_RMS_UNFUSED_MIN_N", "8192"))
 
 

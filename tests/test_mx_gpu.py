@@ -245,3 +245,24 @@ def test_embedding_mx_copy_is_the_quantized_rows():
     assert torch.equal(out, ops.embedding(ids, table))
     q, e = ref.quantize_mx(out.cpu())
     assert torch.equal(mx.blocks().cpu(), e) and torch.equal(mx.q.cpu(), q)
+
+
+@pytest.mark.parametrize("N", [4096, 8192])
+def test_mgemm_bf16_rms_prologue_both_forms(N):
+    """The bf16 RMS prologue: v_dot2 squares below 8192 output features, the x . x^T MFMA diagonal from 8192 on
+    (mgemm.hip rms_mfma) -- every configuration against the fp32 oracle."""
+    K, eps = 1024, 1e-5
+    g = torch.Generator(device="cpu").manual_seed(N)
+    w = ((torch.rand(N, K, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16).to(DEV)
+    n_cfg = 0
+    for cfg in range(len(ops.mgemm_configs())):
+        if not ops.mgemm_valid(cfg, 64, N, K, ops.EPI_BF16, 0):
+            continue
+        n_cfg += 1
+        for M in (24, 64):
+            r = (torch.randn(M, K, generator=g) * 3).to(torch.bfloat16).to(DEV)
+            y = ops.mgemm(r, w, ops.EPI_BF16, cfg=cfg, grid=1, rms_eps=eps).float().cpu()
+            rf = r.float().cpu()
+            exp = (rf * torch.rsqrt(rf.pow(2).mean(-1, keepdim=True) + eps)) @ w.float().cpu().t()
+            assert (y - exp).abs().max().item() <= 1e-2 * exp.abs().max().item(), f"cfg {cfg} M {M}"
+    assert n_cfg >= 6
