@@ -1078,12 +1078,15 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
 
 
 # bf16 rows in (SGEMV_MAX_M, RMS_PROLOGUE_MAX_UNFUSED] with at least RMS_UNFUSED_MIN_N output features take a
-# separate RMSNorm + plain GEMM instead of mgemm's RMS prologue (K8S_RMS_UNFUSED_MAX_M; 0 = always the prologue, the
-# default since round 5).  Round 4 (profiles/bench_r4_rms_prologue_ab.txt) measured the separate norm faster for the
-# TP = 1 projections (QKV 10240, gate/up 28672 features) while their prologue squared x with v_dot2 in every k-step;
-# with the sums of squares taken from one extra MFMA (x . x^T diagonal, mgemm.hip) the prologue wins there too:
-# batch 64 30.85 -> 30.72 ms/step, batch 32 28.18 -> 27.52 (profiles/rms_mfma_ab_r5.txt).
-RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "0"))
+# separate RMSNorm + plain GEMM instead of mgemm's RMS prologue (K8S_RMS_UNFUSED_MAX_M; 0 = always the prologue).
+# Round 4 (profiles/bench_r4_rms_prologue_ab.txt) measured the separate norm faster for the TP = 1 projections while
+# the prologue squared x with v_dot2 in every k-step.  Round 5 takes the sums of squares from one extra MFMA (x . x^T
+# diagonal, mgemm.hip) on the wide projections, which makes gate/up's prologue the faster form, while the QKV GEMM
+# stays faster plain (batch 64: QKV separate + gate/up prologue 30.48-30.52 ms/step, both prologue 30.69-30.79, both
+# separate 30.72-30.83; batch 32: 27.71 / 27.63 / 28.13 -- profiles/rms_policy_ab_r5.txt).
+RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "64"))
+# ... except gate/up (SwiGLU): its prologue always (K8S_RMS_PROLOGUE_SWIGLU=0: the round-4 rule for it too)
+RMS_PROLOGUE_SWIGLU = os.environ.get("K8S_RMS_PROLOGUE_SWIGLU", "1") != "0"
 RMS_UNFUSED_MIN_N = int(os.environ.get("K8S_RMS_UNFUSED_MIN_N", "8192"))
 
 
@@ -1140,7 +1143,8 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16, mx_consumer=
     xg = (XGEMM_ON and not _is_fp8(w) and M <= XGEMM_MAX_M and GEMM_BACKEND == "auto"
           and native().xgemm_plan(M, n_out, K, epi, 1)[0] == 0) if _gpu(r) else False
     if _gpu(r) and M > GEMV_MAX_M and (M <= SGEMV_MAX_M or M > RMS_PROLOGUE_MAX_UNFUSED or _is_fp8(w)
-                                       or n_out < RMS_UNFUSED_MIN_N or xg):
+                                       or n_out < RMS_UNFUSED_MIN_N or xg
+                                       or (epi == EPI_SWIGLU and RMS_PROLOGUE_SWIGLU)):
         y = _gemm(r.contiguous(), w, epi, rms_eps=eps)
         if y is not None:
             return y
