@@ -302,14 +302,14 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
             for (int j = 0; j < FM; ++j)
               acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], bfr[j], acc[f][j], 0, 0, 0);
           if (do_rms && rms_mfma) {
-            // one more MFMA per x fragment, x . x^T (diagonal = the rows' sums of squares), in wave wn = 0 of a row
-            // block; a scalar branch (readfirstlane), since an MFMA ignores EXEC.  In the weight-streaming regime the
-            // MFMA pipe is idle enough that this costs less than v_dot2 squares in every k-step (or a norm launch)
-            if (__builtin_amdgcn_readfirstlane(wn) == 0) {
+            // one more MFMA per x fragment, x . x^T (diagonal = the rows' sums of squares); a scalar branch
+            // (readfirstlane), since an MFMA ignores EXEC.  In the weight-streaming regime the MFMA pipe is idle
+            // enough that this costs less than v_dot2 squares in every k-step (or a norm launch).  Fragment j in
+            // wave wn = j % WN of the row block: the extra MFMAs spread over the waves that share x
+            const int wn_u = __builtin_amdgcn_readfirstlane(wn);
 #pragma unroll
-              for (int j = 0; j < FM; ++j)
-                accsq[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], bfr[j], accsq[j], 0, 0, 0);
-            }
+            for (int j = 0; j < FM; ++j)
+              if (j % WN == wn_u) accsq[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], bfr[j], accsq[j], 0, 0, 0);
           } else if (do_rms) {   // the WN waves of a row block hold the same x fragments: each squares 1/WN of them
 #pragma unroll
             for (int j = 0; j < FM; ++j)

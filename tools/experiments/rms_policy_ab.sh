@@ -9,7 +9,7 @@ run() {  # run <label> <seconds> <env> <bench args...>
   env $e timeout -k 10 "$t" python -u bench.py "$@" > "$O/$label.json" 2> "$O/$label.err" || { echo "$label FAILED"; tail -5 "$O/$label.err"; exit 1; }
   echo "$label $(tail -1 $O/$label.json | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["decode_ms_per_step"], d.get("prefill_ms_per_decision"))')"
 }
-for rep in 1 2; do
+for rep in 1; do
 run b64_qkvsep_gufused_$rep 600 "" --batch 64 --steps 3 --warmup 1
 run b64_allfused_$rep 600 K8S_RMS_UNFUSED_MAX_M=0 --batch 64 --steps 3 --warmup 1
 run b64_allsep_$rep 600 K8S_RMS_PROLOGUE_SWIGLU=0 --batch 64 --steps 3 --warmup 1
