@@ -19,9 +19,12 @@
 //    logical range), with the k-slices of one tile adjacent, then the m-tiles of one n-tile:
 //    the weights a tile streams are re-read by its neighbours from the same L2.
 //  * split-K for small grids (TP = 8 shapes: N = 1280, K = 8192): every slice writes an fp32 slab
-//    in fragment order, publishes it (agent release + arrival ticket), and the last arriving slice
-//    of a tile reduces all slabs and applies the epilogue in the same launch (no memset, no
-//    second kernel; the ticket is reset by the reducer).
+//    in fragment order with write-through (sc1) 16-byte buffer stores, waits for them, and counts its
+//    arrival with one relaxed device-scope ticket add; the last arriving slice of a tile reads all
+//    slabs back with sc1 loads (fixed order), reduces them and applies the epilogue in the same launch
+//    (no memset, no second kernel, no cache-wide fence; the ticket is reset by the reducer) -- opt-in,
+//    K8S_MGEMM_FENCED=0; the default keeps plain slab stores with agent-scope release / acquire fences
+//    (measured no slower at this grid size, tools/experiments/mgemm_fence_ab.sh).
 //  * fp8: activations are quantized per token (fp8.hip), weights per row; the epilogue applies
 //    sx[m] * sw[n].  Non-scaled fp8 MFMA runs at the bf16 rate but halves the staged bytes.
 //  * fp8 weights x bf16 activations (W8, host mode fp8 = 2; the batched-decode regime): no activation
@@ -102,6 +105,7 @@ struct MgArgs {
   int rms;               // 1: RMSNorm prologue -- out scaled by 1 / rms(x row) (the gamma is folded into W)
   float eps;
   int rms_mfma;          // bf16 / W8 rows: the row sums of squares from x . x^T on the MFMA (1) or v_dot2 (0)
+  int fenced;            // split tiles: 1 = plain slab stores + agent-scope release / acquire fences (round-4 form)
 };
 
 // Wave layout: WM x WN waves own (BM / WM) x (BN / WN) output sub-tiles; WK waves share each
@@ -451,7 +455,59 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     const int w_last = (int)(((i_first + T) * a.nwg - 1) / a.total);
     const int nc = w_last - w_first + 1;
     constexpr int SLAB = BM * BN + BM;   // partial tile + row sums of squares
-    if (nc > 1) {
+    if (nc > 1 && !a.fenced) {
+      // the sgemv.hip protocol, no cache-wide fences (an agent-scope release / acquire costs an L2 write-back /
+      // invalidate per arriving workgroup on this chip): device-coherent slab stores, every wave waits for its own
+      // stores, one relaxed device-scope ticket add per workgroup, device-coherent slab loads by the last arriver
+      float* base = a.ws + (long long)tile * a.cmax * SLAB;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+      const int sbase = (lid - w_first) * SLAB * 4;   // this workgroup's slab, bytes from base
+      constexpr int MG_SC1 = 16;                       // buffer-op cache policy sc1: write-through, coherent at L2
+      if (do_rms && threadIdx.x < BM)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, rss[threadIdx.x]), rs,
+                                              sbase + (BM * BN + threadIdx.x) * 4, 0, MG_SC1);
+      if (wk == 0) {
+#pragma unroll
+        for (int f = 0; f < FN; ++f)
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[f][j]), rs,
+                                                   sbase + ((((wt * FN + f) * FM + j) * 64 + lane) * 4) * 4, 0, MG_SC1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab stores have landed
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned last = old == (unsigned)(nc - 1);
+        if (last) __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+        *flag = last;
+      }
+      __syncthreads();
+      if (*flag == 0u) continue;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // (compiler ordering: the loads stay below the add)
+      if (wk == 0) {   // fixed summation order over ALL slabs (own included)
+#pragma unroll
+        for (int f = 0; f < FN; ++f)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s2 = 0; s2 < nc; ++s2) {
+#pragma unroll
+          for (int f = 0; f < FN; ++f)
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+              acc[f][j] += __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                             rs, (s2 * SLAB + (((wt * FN + f) * FM + j) * 64 + lane) * 4) * 4, 0, MG_SC1));
+        }
+      }
+      if (do_rms && threadIdx.x < BM) {
+        float t = 0.f;
+        for (int s2 = 0; s2 < nc; ++s2)
+          t += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             rs, (s2 * SLAB + BM * BN + threadIdx.x) * 4, 0, MG_SC1));
+        rss[threadIdx.x] = t;
+      }
+    } else if (nc > 1) {
       float* base = a.ws + (long long)tile * a.cmax * SLAB;
       float* slab = base + (long long)(lid - w_first) * SLAB;
       if (do_rms && threadIdx.x < BM) slab[BM * BN + threadIdx.x] = rss[threadIdx.x];
@@ -899,6 +955,8 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   // K8S_RMS_MFMA = 0 / 1 forces one form.
   static const int rms_mfma_env = [] { const char* e = getenv("K8S_RMS_MFMA"); return e ? atoi(e) : -1; }();
   a.rms_mfma = rms_mfma_env >= 0 ? rms_mfma_env : (N_out >= 8192 ? 1 : 0);
+  static const int fenced = [] { const char* e = getenv("K8S_MGEMM_FENCED"); return e ? atoi(e) : 1; }();
+  a.fenced = fenced;
   a.out = out;
   a.ws = ws;
   a.cnt = tickets;
