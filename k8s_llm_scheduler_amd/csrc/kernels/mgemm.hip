@@ -22,9 +22,9 @@
 //    in fragment order with write-through (sc1) 16-byte buffer stores, waits for them, and counts its
 //    arrival with one relaxed device-scope ticket add; the last arriving slice of a tile reads all
 //    slabs back with sc1 loads (fixed order), reduces them and applies the epilogue in the same launch
-//    (no memset, no second kernel, no cache-wide fence; the ticket is reset by the reducer) -- opt-in,
-//    K8S_MGEMM_FENCED=0; the default keeps plain slab stores with agent-scope release / acquire fences
-//    (measured no slower at this grid size, tools/experiments/mgemm_fence_ab.sh).
+//    (no memset, no second kernel, no cache-wide fence; the ticket is reset by the reducer).  Measured
+//    against the round-4 form (plain stores + agent-scope release / acquire fences, K8S_MGEMM_FENCED=1):
+//    batch-64 decode 30.68 -> 30.46 ms/step bf16, 18.73 -> 18.30 fp8 (profiles/mgemm_fence_ab_r5.txt).
 //  * fp8: activations are quantized per token (fp8.hip), weights per row; the epilogue applies
 //    sx[m] * sw[n].  Non-scaled fp8 MFMA runs at the bf16 rate but halves the staged bytes.
 //  * fp8 weights x bf16 activations (W8, host mode fp8 = 2; the batched-decode regime): no activation
@@ -955,7 +955,7 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   // K8S_RMS_MFMA = 0 / 1 forces one form.
   static const int rms_mfma_env = [] { const char* e = getenv("K8S_RMS_MFMA"); return e ? atoi(e) : -1; }();
   a.rms_mfma = rms_mfma_env >= 0 ? rms_mfma_env : (N_out >= 8192 ? 1 : 0);
-  static const int fenced = [] { const char* e = getenv("K8S_MGEMM_FENCED"); return e ? atoi(e) : 1; }();
+  static const int fenced = [] { const char* e = getenv("K8S_MGEMM_FENCED"); return e ? atoi(e) : 0; }();
   a.fenced = fenced;
   a.out = out;
   a.ws = ws;
