@@ -56,7 +56,6 @@ enum { MG_BF16 = 0, MG_F32 = 1, MG_SWIGLU = 2 };
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(4))) int i32x4;
-typedef __attribute__((ext_vector_type(2))) float f2v;
 
 __device__ __forceinline__ float mg_silu(float g) { return g / (1.f + __expf(-g)); }
 
