@@ -128,6 +128,9 @@ def main() -> int:
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--w8", action="store_true", help="tune the W8 mode (fp8 weights, bf16 activations)")
     ap.add_argument("--mx", action="store_true", help="tune the MX modes (MX activations; MX SwiGLU output)")
+    ap.add_argument("--insitu", action="store_true",
+                    help="bf16: time O / down with the residual epilogue and gate/up with the RMS prologue, as the "
+                         "17-64-row decode layer runs them (QKV stays plain: norm + GEMM)")
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
@@ -164,17 +167,18 @@ def main() -> int:
             for M in a.m:
                 x = torch.empty(M, K, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1)
                 ACT[0] = ops.quantize_act_mx(x) if a.fp8 in (3, 4) else None
-                res_mx = a.mx and name in ("o_proj", "down")   # residual epilogue + the stream's MX copy
-                rms_mx = a.mx and name in ("qkv", "gate_up")   # MX rows + the RMS prologue
+                res_mx = (a.mx or a.insitu) and name in ("o_proj", "down")   # residual epilogue (+ MX copy)
+                rms_mx = (a.mx and name in ("qkv", "gate_up")) or (a.insitu and name == "gate_up")   # RMS prologue
                 RES = torch.empty(M, N, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1) if res_mx else None
                 lib_us = time_graph(lib_fn(x, Ws, epi, a.fp8), copies)
                 best = (float("inf"), None)
 
                 def run(i, c, gr):
                     return ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr, w8=a.fp8 == 2, act=ACT[0],
-                                     mx_out=a.fp8 == 4 or res_mx, res=RES, rms_eps=1e-5 if rms_mx else None)
+                                     mx_out=a.fp8 == 4 or (res_mx and a.mx), res=RES,
+                                     rms_eps=1e-5 if rms_mx else None)
 
-                for c, gr in candidates(M, N, K, epi, a.fp8, res_mx):
+                for c, gr in candidates(M, N, K, epi, a.fp8, res_mx and a.mx):
                     us = time_graph(lambda i, c=c, gr=gr: run(i, c, gr), copies)
                     if a.verbose:
                         bm, bn = ops.mgemm_configs()[c][:2]
