@@ -130,3 +130,24 @@ def test_library_route_only_under_k8s_gemm_library(monkeypatch):
     monkeypatch.setattr(ops, "_lib_linear", lambda x, w: called.append("lib") or (x.float() @ w.float().t()).to(x.dtype))
     y = ops.linear(torch.randn(300, 256, dtype=torch.bfloat16), torch.randn(128, 256, dtype=torch.bfloat16))
     assert called == ["lib"] and y.shape == (300, 128)
+
+
+def _llama70b_decode_shapes(tp):
+    hidden, inter, nq, nkv, d = 8192, 28672, 64, 8, 128
+    return [((nq + 2 * nkv) * d // tp, hidden, ops.EPI_BF16), (hidden, nq * d // tp, ops.EPI_BF16),
+            (inter // tp, hidden, ops.EPI_SWIGLU), (hidden, inter // tp, ops.EPI_BF16)]
+
+
+@pytest.mark.parametrize("tp", [1, 2, 4, 8])
+def test_every_batched_decode_shape_has_a_valid_tuned_plan(tp):
+    """The 17-128-row bf16 plans (re-tuned in situ) and the MX plans (keys 3 / 4) cover every projection of a Llama-70B
+    decode layer at TP = 1 / 2 / 4 / 8, and each tuned plan is valid for every row count of its bucket -- a shape that
+    fell off the table would silently run the heuristic plan."""
+    for i, (N, K, epi) in enumerate(_llama70b_decode_shapes(tp)):
+        for M in (17, 24, 32, 33, 48, 64, 65, 100, 128):
+            row = ops._mg_table_row(M, N, K, epi, False)
+            assert row is not None, (tp, M, N, K, epi)
+            assert ops.mgemm_valid(row[1], M, N, K, epi, 0, row[2]), (tp, M, N, K, epi, row)
+            if K % 128 == 0:
+                mx_out = i > 0   # O / down: the residual epilogue's MX copy; gate/up: MX SwiGLU output
+                assert ops.mgemm_mx_plan(M, N, K, epi, True, mx_out) is not None, (tp, M, N, K, epi)
