@@ -1078,13 +1078,13 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
 
 
 # bf16 rows in (SGEMV_MAX_M, RMS_PROLOGUE_MAX_UNFUSED] with at least RMS_UNFUSED_MIN_N output features take a
-# separate RMSNorm + plain GEMM instead of mgemm's RMS prologue (K8S_RMS_UNFUSED_MAX_M; 0 = always the prologue).
-# Round 4 (profiles/bench_r4_rms_prologue_ab.txt) measured the separate norm faster for the TP = 1 projections while
-# the prologue squared x with v_dot2 in every k-step.  Round 5 takes the sums of squares from one extra MFMA (x . x^T
-# diagonal, mgemm.hip) on the wide projections, which makes gate/up's prologue the faster form, while the QKV GEMM
-# stays faster plain (batch 64: QKV separate + gate/up prologue 30.48-30.52 ms/step, both prologue 30.69-30.79, both
-# separate 30.72-30.83; batch 32: 27.71 / 27.63 / 28.13 -- profiles/rms_policy_ab_r5.txt).
-RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "64"))
+# separate RMSNorm + plain GEMM instead of mgemm's RMS prologue (K8S_RMS_UNFUSED_MAX_M; 0, the default = always the
+# prologue).  Round 4 (profiles/bench_r4_rms_prologue_ab.txt) measured the separate norm faster for the TP = 1
+# projections while the prologue squared x with v_dot2 in every k-step.  Round 5 takes the sums of squares from one
+# extra MFMA (x . x^T diagonal, mgemm.hip) on the wide projections, which made gate/up's prologue the faster form
+# (profiles/rms_policy_ab_r5.txt); with the QKV plans re-tuned for the prologue in situ the TP = 1 QKV's prologue wins
+# too (batch 64 29.49 -> 29.09 ms/step, batch 32 26.63 -> 26.21 -- profiles/qkv_rms_ab_r5.txt).
+RMS_PROLOGUE_MAX_UNFUSED = int(os.environ.get("K8S_RMS_UNFUSED_MAX_M", "0"))
 # ... except gate/up (SwiGLU): its prologue always (K8S_RMS_PROLOGUE_SWIGLU=0: the round-4 rule for it too)
 RMS_PROLOGUE_SWIGLU = os.environ.get("K8S_RMS_PROLOGUE_SWIGLU", "1") != "0"
 RMS_UNFUSED_MIN_N = int(os.environ.get("K8S_RMS_UNFUSED_MIN_N", "8192"))

@@ -131,6 +131,7 @@ def main() -> int:
     ap.add_argument("--insitu", action="store_true",
                     help="bf16: time O / down with the residual epilogue and gate/up with the RMS prologue, as the "
                          "17-64-row decode layer runs them (QKV stays plain: norm + GEMM)")
+    ap.add_argument("--qkv-rms", action="store_true", help="--insitu: time QKV with the RMS prologue too")
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
@@ -168,7 +169,7 @@ def main() -> int:
                 x = torch.empty(M, K, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1)
                 ACT[0] = ops.quantize_act_mx(x) if a.fp8 in (3, 4) else None
                 res_mx = (a.mx or a.insitu) and name in ("o_proj", "down")   # residual epilogue (+ MX copy)
-                rms_mx = (a.mx and name in ("qkv", "gate_up")) or (a.insitu and name == "gate_up")   # RMS prologue
+                rms_mx = (a.mx and name in ("qkv", "gate_up")) or (a.insitu and (name == "gate_up" or (a.qkv_rms and name == "qkv")))   # RMS prologue
                 RES = torch.empty(M, N, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1) if res_mx else None
                 lib_us = time_graph(lib_fn(x, Ws, epi, a.fp8), copies)
                 best = (float("inf"), None)
