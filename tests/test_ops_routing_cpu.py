@@ -151,3 +151,13 @@ def test_every_batched_decode_shape_has_a_valid_tuned_plan(tp):
             if K % 128 == 0:
                 mx_out = i > 0   # O / down: the residual epilogue's MX copy; gate/up: MX SwiGLU output
                 assert ops.mgemm_mx_plan(M, N, K, epi, True, mx_out) is not None, (tp, M, N, K, epi)
+
+
+def test_mx_plans_are_tuned_for_every_tp_shard():
+    """fp8 batched decode at TP = 1 / 2 / 4 / 8: every projection has TUNED MX plans (table keys 3 / 4) for 32-256 rows,
+    not only a heuristic one."""
+    table = ops._mg_load_table()
+    for tp in (1, 2, 4, 8):
+        for N, K, epi in _llama70b_decode_shapes(tp):
+            key = (N, K, epi, 4 if epi == ops.EPI_SWIGLU else 3)
+            assert sorted(r[0] for r in table.get(key, [])) == [32, 64, 128, 256], (tp, key)
