@@ -273,7 +273,9 @@ def main() -> int:
         "metric": "scheduling_decisions_per_sec",
         "value": round(value, 4),
         "unit": "decisions/s",
-        "n_gpus": tp.world * dp if not tp.simulate else tp.world,
+        # --simulate-tp: ONE GPU ran one TP rank's shapes (collectives skipped) -- n_gpus stays the GPUs used
+        "n_gpus": tp.world * dp if not tp.simulate else 1,
+        "simulated_tp": tp.world if tp.simulate else None,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000 * elapsed / args.steps, 3),

@@ -66,22 +66,6 @@ int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const v
                                float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax, int part,
                                void* oq, void* oe, hipStream_t s);
 long long k8s_decode_split_workspace(int B, int nq, int nkv, int pmax);
-int k8s_decode_persist_plan(int M, int H, int nq, int nkv, int I, int pmax, int* gl, int* grid);
-int k8s_decode_persist(const void* layers, int L, const void* x0, void* xout, int M, int H, int nq, int nkv, int I,
-                       float eps, float scale, const float* cos_sin, const int* block_tables, const int* context_lens,
-                       int max_blocks, int pmax, void* gran, void* part, uint32_t* counters, uint32_t* sync,
-                       void* trace, long long timeout_ticks, hipStream_t s);
-int k8s_decode_persist_layer_bytes();
-int k8s_xgemm_plan(int M, int N, int K, int epi, int rms, int* nslab, int* gps, long long* ws_floats,
-                   long long* rss_floats);
-int k8s_xgemm(void* out, void* ws, void* rss, const void* x, const void* W, const void* res, int M, int N, int K,
-              int epi, int rms, float eps, hipStream_t s);
-int k8s_decode_persist_trace_points();
-int k8s_decode_attention_split_oproj(void* attn, void* part, uint32_t* counters, const void* qkv, const float* cos_sin,
-                                     void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
-                                     float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks,
-                                     int pmax, const void* wo, void* o_out, int N, uint32_t* sync, int delay,
-                                     int poll_sleep, hipStream_t s);
 int k8s_decode_attention_split(void* out, void* part, uint32_t* counters, const void* qkv, const float* cos_sin,
                                void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
                                float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax,
@@ -90,7 +74,16 @@ int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, cons
                const float* top_p, const uint32_t* seeds, const int* counter, int* ctx_inc, int* hist, int hist_stride,
                int* steps, void* scratch, void* nuc_scratch, const int* slots, const int* stop_cls, int* stop_json,
                const int* stop_cfg, const int* stop_forced, const int* stop_forced_len, int stop_fstride,
-               int stop_eos_tok, int* stop_done, hipStream_t s);
+               int stop_eos_tok, int* stop_done, int id_base, void* keys_out, int nuc_passes, hipStream_t s);
+int k8s_sample_nuc_local(int level, const float* logits, int B, int Vs, const float* temperature, const float* top_p,
+                         const int* ctx_inc, const int* slots, void* nuc_scratch, void* out, hipStream_t s);
+int k8s_sample_nuc_combine(int level, const void* g, int ld, int ranks, int B, const float* temperature,
+                           const float* top_p, const int* ctx_inc, const int* slots, void* nuc_scratch, void* mine,
+                           hipStream_t s);
+int k8s_sample_merge(int* tokens, const void* g, int ld, int ranks, int B, int* ctx_inc, int* hist, int hist_stride,
+                     int* steps, const int* slots, const int* stop_cls, int* stop_json, const int* stop_cfg,
+                     const int* stop_forced, const int* stop_forced_len, int stop_fstride, int stop_eos_tok,
+                     int* stop_done, hipStream_t s);
 long long k8s_sample_scratch_bytes(int B);
 long long k8s_sample_nucleus_bytes(int B, int shards);
 int k8s_embedding(void* out, const int* ids, const void* table, int T, int H, int vocab, void* oq, void* oe,
@@ -106,7 +99,7 @@ int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, int cfg, int 
                         long long* ws_elems);
 int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs, const float* wsc,
               int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax, const void* res, int rms,
-              float eps, void* oq, void* oe, hipStream_t s);
+              float eps, void* oq, void* oe, int fenced, hipStream_t s);
 int k8s_pgemm4_num_configs();
 int k8s_pgemm4_config(int cfg, int* bp, int* bq, int* lds_bytes);
 int k8s_pgemm4_plan(int M, int N_out, int K, int epi, int cfg, int splits, int* nwg, long long* slab_elems);
@@ -264,47 +257,8 @@ PYBIND11_MODULE(K8S_MODULE_NAME, m) {
      py::arg("vc"), py::arg("bt"), py::arg("ctx"), py::arg("scale"), py::arg("B"), py::arg("nq"), py::arg("nkv"),
      py::arg("D"), py::arg("bs"), py::arg("max_blocks"), py::arg("pmax"), py::arg("part"), py::arg("s"),
      py::arg("oq") = 0, py::arg("oe") = 0);
-  // layer-persistent decode (decode_persist.hip): plan -> (rc, granules per (layer, row), grid); rc < 0: not taken
-  m.def("decode_persist_plan", [](int M, int H, int nq, int nkv, int I, int pmax) {
-    int gl = 0, grid = 0;
-    const int rc = k8s_decode_persist_plan(M, H, nq, nkv, I, pmax, &gl, &grid);
-    return py::make_tuple(rc, gl, grid);
-  });
-  m.def("decode_persist_layer_bytes", []() { return k8s_decode_persist_layer_bytes(); });
-  // activation-resident GEMM for 17-64 decode rows (xgemm.hip): plan -> (rc, slabs, groups, ws floats, rss floats)
-  m.def("xgemm_plan", [](int M, int N, int K, int epi, int rms) {
-    int ns = 0, g = 0;
-    long long wf = 0, rf = 0;
-    const int rc = k8s_xgemm_plan(M, N, K, epi, rms, &ns, &g, &wf, &rf);
-    return py::make_tuple(rc, ns, g, wf, rf);
-  });
-  m.def("xgemm", [](uintptr_t out, uintptr_t ws, uintptr_t rss, uintptr_t x, uintptr_t W, uintptr_t res, int M, int N,
-                    int K, int epi, int rms, float eps, int64_t s) {
-    check(k8s_xgemm(P(out), P(ws), P(rss), P(x), P(W), P(res), M, N, K, epi, rms, eps, S(s)), "xgemm");
-  });
-  m.def("decode_persist_trace_points", []() { return k8s_decode_persist_trace_points(); });
-  m.def("decode_persist", [](uintptr_t layers, int L, uintptr_t x0, uintptr_t xout, int M, int H, int nq, int nkv,
-                             int I, float eps, float scale, uintptr_t cos_sin, uintptr_t bt, uintptr_t ctx,
-                             int max_blocks, int pmax, uintptr_t gran, uintptr_t part, uintptr_t counters,
-                             uintptr_t sync, uintptr_t trace, long long timeout_ticks, int64_t s) {
-    check(k8s_decode_persist(P(layers), L, P(x0), P(xout), M, H, nq, nkv, I, eps, scale, P<float>(cos_sin),
-                             P<int>(bt), P<int>(ctx), max_blocks, pmax, P(gran), P(part), P<uint32_t>(counters),
-                             P<uint32_t>(sync), P(trace), timeout_ticks, S(s)),
-          "decode_persist");
-  });
   m.def("decode_split_workspace", [](int B, int nq, int nkv, int pmax) {
     return k8s_decode_split_workspace(B, nq, nkv, pmax);
-  });
-  m.def("decode_attention_split_oproj", [](uintptr_t attn, uintptr_t part, uintptr_t counters, uintptr_t qkv,
-                                           uintptr_t cos_sin, uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx,
-                                           float scale, int B, int nq, int nkv, int D, int bs, int max_blocks,
-                                           int pmax, uintptr_t wo, uintptr_t o_out, int N, uintptr_t sync,
-                                           int delay, int poll_sleep, int64_t s) {
-    check(k8s_decode_attention_split_oproj(P(attn), P(part), P<uint32_t>(counters), P(qkv), P<float>(cos_sin),
-                                           P(kc), P(vc), P<int>(bt), P<int>(ctx), scale, B, nq, nkv, D, bs,
-                                           max_blocks, pmax, P(wo), P(o_out), N, P<uint32_t>(sync), delay,
-                                           poll_sleep, S(s)),
-          "decode_attention_split_oproj");
   });
   m.def("decode_attention_split", [](uintptr_t out, uintptr_t part, uintptr_t counters, uintptr_t qkv,
                                      uintptr_t cos_sin, uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx,
@@ -318,12 +272,39 @@ PYBIND11_MODULE(K8S_MODULE_NAME, m) {
                      uintptr_t seeds, uintptr_t counter, uintptr_t ctx_inc, uintptr_t hist, int hist_stride,
                      uintptr_t steps, uintptr_t scratch, uintptr_t nuc_scratch, uintptr_t slots, uintptr_t cls,
                      uintptr_t json, uintptr_t cfg, uintptr_t forced, uintptr_t forced_len, int fstride, int eos_tok,
-                     uintptr_t done, int64_t s) {
+                     uintptr_t done, int64_t s, int id_base, uintptr_t keys_out, int nuc_passes) {
     check(k8s_sample(P<int>(tokens), P<float>(logits), B, Vs, shards, P<float>(temp), P<float>(top_p),
                      P<uint32_t>(seeds), P<int>(counter), P<int>(ctx_inc), P<int>(hist), hist_stride, P<int>(steps),
                      P(scratch), P(nuc_scratch), P<int>(slots), P<int>(cls), P<int>(json), P<int>(cfg), P<int>(forced),
-                     P<int>(forced_len), fstride, eos_tok, P<int>(done), S(s)),
+                     P<int>(forced_len), fstride, eos_tok, P<int>(done), id_base, P(keys_out), nuc_passes, S(s)),
           "sample");
+  }, py::arg("tokens"), py::arg("logits"), py::arg("B"), py::arg("Vs"), py::arg("shards"), py::arg("temp"),
+     py::arg("top_p"), py::arg("seeds"), py::arg("counter"), py::arg("ctx_inc"), py::arg("hist"),
+     py::arg("hist_stride"), py::arg("steps"), py::arg("scratch"), py::arg("nuc_scratch"), py::arg("slots"),
+     py::arg("cls"), py::arg("json"), py::arg("cfg"), py::arg("forced"), py::arg("forced_len"), py::arg("fstride"),
+     py::arg("eos_tok"), py::arg("done"), py::arg("stream"), py::arg("id_base") = 0, py::arg("keys_out") = 0,
+     py::arg("nuc_passes") = 1);
+  // vocab-parallel sampling stages (sampler.hip): the TP ranks exchange row maxima / bin totals / best keys
+  m.def("sample_nuc_local", [](int level, uintptr_t logits, int B, int Vs, uintptr_t temp, uintptr_t top_p,
+                               uintptr_t ctx_inc, uintptr_t slots, uintptr_t nuc_scratch, uintptr_t out, int64_t s) {
+    check(k8s_sample_nuc_local(level, P<float>(logits), B, Vs, P<float>(temp), P<float>(top_p), P<int>(ctx_inc),
+                               P<int>(slots), P(nuc_scratch), P(out), S(s)),
+          "sample_nuc_local");
+  });
+  m.def("sample_nuc_combine", [](int level, uintptr_t g, int ld, int ranks, int B, uintptr_t temp, uintptr_t top_p,
+                                 uintptr_t ctx_inc, uintptr_t slots, uintptr_t nuc_scratch, uintptr_t mine, int64_t s) {
+    check(k8s_sample_nuc_combine(level, P(g), ld, ranks, B, P<float>(temp), P<float>(top_p), P<int>(ctx_inc),
+                                 P<int>(slots), P(nuc_scratch), P(mine), S(s)),
+          "sample_nuc_combine");
+  });
+  m.def("sample_merge", [](uintptr_t tokens, uintptr_t g, int ld, int ranks, int B, uintptr_t ctx_inc, uintptr_t hist,
+                           int hist_stride, uintptr_t steps, uintptr_t slots, uintptr_t cls, uintptr_t json,
+                           uintptr_t cfg, uintptr_t forced, uintptr_t forced_len, int fstride, int eos_tok,
+                           uintptr_t done, int64_t s) {
+    check(k8s_sample_merge(P<int>(tokens), P(g), ld, ranks, B, P<int>(ctx_inc), P<int>(hist), hist_stride,
+                           P<int>(steps), P<int>(slots), P<int>(cls), P<int>(json), P<int>(cfg), P<int>(forced),
+                           P<int>(forced_len), fstride, eos_tok, P<int>(done), S(s)),
+          "sample_merge");
   });
   // Host memory the GPU can write (fine-grained, coherent): the decode graphs' done flags, polled by the host
   // between replays without a device synchronisation.
@@ -374,14 +355,14 @@ PYBIND11_MODULE(K8S_MODULE_NAME, m) {
   });
   m.def("mgemm", [](uintptr_t out, uintptr_t ws, uintptr_t tickets, uintptr_t x, uintptr_t W, uintptr_t xs,
                     uintptr_t wsc, int M, int N, int K, int epi, int fp8, int cfg, int nwg, int cmax, uintptr_t res,
-                    int rms, float eps, int64_t s, uintptr_t oq, uintptr_t oe) {
+                    int rms, float eps, int64_t s, uintptr_t oq, uintptr_t oe, int fenced) {
     check(k8s_mgemm(P(out), P<float>(ws), P<unsigned>(tickets), P(x), P(W), P<float>(xs), P<float>(wsc), M, N, K,
-                    epi, fp8, cfg, nwg, cmax, P(res), rms, eps, P(oq), P(oe), S(s)),
+                    epi, fp8, cfg, nwg, cmax, P(res), rms, eps, P(oq), P(oe), fenced, S(s)),
           "mgemm");
   }, py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("x"), py::arg("W"), py::arg("xs"), py::arg("wsc"),
      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("fp8"), py::arg("cfg"), py::arg("nwg"),
      py::arg("cmax"), py::arg("res"), py::arg("rms"), py::arg("eps"), py::arg("s"), py::arg("oq") = 0,
-     py::arg("oe") = 0);
+     py::arg("oe") = 0, py::arg("fenced") = 0);
 
   m.def("pgemm4_configs", []() {
     py::list out;

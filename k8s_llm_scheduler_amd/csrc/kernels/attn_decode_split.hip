@@ -66,27 +66,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t split_rsrc(const void* p) {
 
 }  // namespace
 
-// Publish a finished (sequence, kv head) output to the workgroups of the fused O projection:
-// 4-byte write-through (sc1) stores of bf16 pairs, every store drained, then one arrival.
-__device__ __forceinline__ void store_pair_sc1(bf16_t* p, float a, float b) {
-  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), pack_bf2(a, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-constexpr int OP_REPL = 8, OP_LINE = 32;   // published-pairs counter: 8 replicas, one 128-byte line each
-__device__ __forceinline__ void signal_done(uint32_t* done, int lane) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // one wave: every lane's output stores have landed
-  if (lane < OP_REPL)   // one add per replica, so each poller reads a line only 1/8 of them share
-    __hip_atomic_fetch_add(done + lane * OP_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The split-attention work of workgroup (chunk c, kv head kvh, sequence b).  SIGNAL: the workgroup
-// that writes a pair's final output publishes it (store_pair_sc1 + signal_done on `done`), for the
-// O-projection workgroups of decode_split_oproj_kernel.
-template <int G, bool SIGNAL>
+// The split-attention work of workgroup (chunk c, kv head kvh, sequence b).
+template <int G>
 __device__ __forceinline__ void split_body(
     bf16_t* __restrict__ out, float* __restrict__ part, uint32_t* __restrict__ counters,
     const bf16_t* __restrict__ qkv, const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache,
     bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
-    float scale, int max_blocks, int nkv, int pmax, int c, int kvh, int b, uint32_t* __restrict__ done) {
+    float scale, int max_blocks, int nkv, int pmax, int c, int kvh, int b) {
   constexpr int D = 128, HALF = D / 2, CH = SPLIT_CH;
   constexpr int PSTRIDE = G * D + 2 * G;  // floats per (b, kvh, chunk) partial record
   static_assert(G >= 1 && G <= 16, "GQA group of 1..16 heads");
@@ -122,10 +108,7 @@ __device__ __forceinline__ void split_body(
   }
   const bf16_t ka = row[(size_t)(nq + kvh) * D + lane], kb = row[(size_t)(nq + kvh) * D + HALF + lane];
   const bf16_t va = row[(size_t)(nq + nkv + kvh) * D + lane], vb2 = row[(size_t)(nq + nkv + kvh) * D + HALF + lane];
-  if (ctx <= 0 || start >= ctx) {
-    if (SIGNAL && ctx <= 0 && c == 0) signal_done(done, lane);   // padded row: nothing to wait for
-    return;
-  }
+  if (ctx <= 0 || start >= ctx) return;
   K8S_CHECK_MAX(ctx, max_blocks * 16, K8S_CHK_CTX);
 #pragma unroll
   for (int t = 0; t < 4; ++t) K8S_CHECK_RANGE(tblk[t], 0, K8S_CHK_BLOCK, 0);
@@ -302,16 +285,10 @@ __device__ __forceinline__ void split_body(
         const float inv = 1.f / lh[i];
 #pragma unroll
         for (int nn = 0; nn < D / 16; ++nn) {
-          if constexpr (SIGNAL) {   // lane li and li + 1 hold adjacent columns: even lanes store the pair
-            const float v = o[nn][i] * inv, nb = __shfl_down(v, 1, 16);
-            if ((li & 1) == 0) store_pair_sc1(op + 16 * nn + li, v, nb);
-          } else {
-            op[16 * nn + li] = f2bf(o[nn][i] * inv);
-          }
+          op[16 * nn + li] = f2bf(o[nn][i] * inv);
         }
       }
     }
-    if constexpr (SIGNAL) signal_done(done, lane);
     TR(7);
     return;
   }
@@ -411,14 +388,8 @@ __device__ __forceinline__ void split_body(
   TR(9);
   bf16_t* op = out + ((size_t)b * nq + kvh * G + h) * D + d0;
   const float inv = 1.f / den;
-  if constexpr (SIGNAL) {
 #pragma unroll
-    for (int j = 0; j < DPL; j += 2) store_pair_sc1(op + j, num[j] * inv, num[j + 1] * inv);
-    signal_done(done, lane);
-  } else {
-#pragma unroll
-    for (int j = 0; j < DPL; ++j) op[j] = f2bf(num[j] * inv);
-  }
+  for (int j = 0; j < DPL; ++j) op[j] = f2bf(num[j] * inv);
   TR(7);
 }
 
@@ -428,98 +399,8 @@ __global__ void __launch_bounds__(64) decode_split_kernel(
     const bf16_t* __restrict__ qkv, const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache,
     bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
     float scale, int max_blocks, int nkv, int pmax) {
-  split_body<G, false>(out, part, counters, qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale,
-                       max_blocks, nkv, pmax, blockIdx.x, blockIdx.y, blockIdx.z, nullptr);
-}
-
-// Split attention + the O projection in ONE launch (TP >= 4 decode, <= 2 sequences: o_proj has K = nq*D of
-// 1024 or 2048).  Blocks [0, n_attn) run the attention chunks above on their first wave; every other block
-// (4 waves, R rows of W_o per wave) loads its W_o rows into registers at launch -- the weight stream starts
-// while attention runs instead of after a kernel boundary -- then ONE lane polls one replica of the
-// published-pairs counter (relaxed, s_sleep, bounded), the block meets at a barrier, every wave reads the
-// attention rows with sc1 loads and writes o = a @ W_o.T.  The last block to acknowledge re-arms the sync
-// words for the next replay.  Attention blocks come first in dispatch order and never wait, so no wait
-// depends on residency.  sync (u32): replicas at [r * 32] (r < 8), acknowledgements at [256], timeout at [288].
-template <int G, int KPL, int R>
-__global__ void __launch_bounds__(256) decode_split_oproj_kernel(
-    bf16_t* __restrict__ attn, float* __restrict__ part, uint32_t* __restrict__ counters,
-    const bf16_t* __restrict__ qkv, const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache,
-    bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
-    float scale, int max_blocks, int nkv, int pmax, const bf16_t* __restrict__ wo, bf16_t* __restrict__ o_out,
-    int N, int B, uint32_t* __restrict__ sync, int delay, int poll_sleep) {
-  const int n_attn = pmax * nkv * B;
-  const int bid = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (bid < n_attn) {
-    if (wid != 0) return;   // one-wave attention work; ended waves do not hold the barriers below
-    split_body<G, true>(attn, part, counters, qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale,
-                        max_blocks, nkv, pmax, bid % pmax, (bid / pmax) % nkv, bid / (pmax * nkv), sync);
-    return;
-  }
-  constexpr int K = 64 * KPL, V8 = KPL / 8, ROWS = 4 * R;
-  const int ob = bid - n_attn;
-  const int row0 = ob * ROWS + wid * R;
-  const int n_ob = (N + ROWS - 1) / ROWS;
-  // keep the W_o burst off the attention chunks' first round trips: `delay` x ~1.7 us before loading
-  for (int i = 0; i < delay; ++i) __builtin_amdgcn_s_sleep(64);
-  // this wave's W_o rows, lane slice [lane * KPL, lane * KPL + KPL) of each
-  bf16x8 w[R][V8];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int row = min(row0 + r, N - 1);
-#pragma unroll
-    for (int v = 0; v < V8; ++v)
-      w[r][v] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wo + (size_t)row * K + lane * KPL) + v);
-  }
-  const uint32_t npairs = (uint32_t)(nkv * B);
-  if (threadIdx.x == 0) {
-    const uint32_t* rep = sync + (ob % OP_REPL) * OP_LINE;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < npairs) {
-      for (int i = 0; i < poll_sleep; ++i) __builtin_amdgcn_s_sleep(4);
-      if (++spins > (1u << 23)) {   // ~0.5 s: a producer never published -- report, do not hang
-        __hip_atomic_store(&sync[9 * OP_LINE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    // every block has passed its poll before the last acknowledgement re-arms the counters
-    const uint32_t prev = __hip_atomic_fetch_add(&sync[8 * OP_LINE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (uint32_t)n_ob - 1) {
-      for (int r = 0; r < OP_REPL; ++r)
-        __hip_atomic_store(&sync[r * OP_LINE], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sync[8 * OP_LINE], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // the loads below stay below the poll
-  const int nq = nkv * G;
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(attn, 0, 0x7fffffff, 0x00020000);
-  for (int b = 0; b < B; ++b) {
-    bf16x8 a[V8];
-#pragma unroll
-    for (int v = 0; v < V8; ++v)
-      a[v] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rs, (b * nq * 128 + lane * KPL + 8 * v) * 2, 0, 16 /* sc1 */));
-    float acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float s = 0.f;
-#pragma unroll
-      for (int v = 0; v < V8; ++v) {
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          const bf16x2 wa{w[r][v][e], w[r][v][e + 1]}, xa{a[v][e], a[v][e + 1]};
-          s = __builtin_amdgcn_fdot2_f32_bf16(wa, xa, s, false);
-        }
-      }
-      acc[r] = wave_sum(s);
-    }
-    if (lane < R && row0 + lane < N) {
-      float v = acc[0];
-#pragma unroll
-      for (int r = 1; r < R; ++r) v = lane == r ? acc[r] : v;
-      o_out[(size_t)b * N + row0 + lane] = f2bf(v);
-    }
-  }
+  split_body<G>(out, part, counters, qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, max_blocks,
+                nkv, pmax, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 }  // namespace k8sllm
@@ -533,48 +414,6 @@ extern "C" int k8s_attn_trace_set(unsigned long long* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_trace), &p, sizeof(p));
 }
 #endif
-
-// attn: [B, nq * D] bf16 scratch (the attention output); wo [N, nq * D] bf16; o_out [B, N] bf16;
-// sync: 1280 zeroed bytes, left zero by every launch (u32 [288] turns 1 if a wait ever timed out).
-extern "C" int k8s_decode_attention_split_oproj(void* attn, void* part, uint32_t* counters, const void* qkv,
-                                                const float* cos_sin, void* k_cache, void* v_cache,
-                                                const int* block_tables, const int* context_lens, float scale, int B,
-                                                int nq, int nkv, int D, int block_size, int max_blocks, int pmax,
-                                                const void* wo, void* o_out, int N, uint32_t* sync, int delay,
-                                                int poll_sleep, hipStream_t stream) {
-  if (B <= 0) return 0;
-  if (D != 128 || nkv <= 0 || nq % nkv != 0 || B > 2) return -1;
-  if (block_size != 16) return -4;
-  if (pmax < 1 || pmax > 64 || (pmax > 1 && (part == nullptr || counters == nullptr)) || sync == nullptr) return -3;
-  const long long G = nq / nkv;
-  if ((long long)pmax * (G * 128 + 2 * G) * 4 > 0x7fffffffLL) return -5;
-  const int K = nq * D;
-  const int n_attn = pmax * nkv * B;
-#define LO(GG, KP, RR)                                                                                        \
-  decode_split_oproj_kernel<GG, KP, RR><<<n_attn + (N + 4 * RR - 1) / (4 * RR), 256, 0, stream>>>(              \
-      (bf16_t*)attn, (float*)part, counters, (const bf16_t*)qkv, cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache,   \
-      block_tables, context_lens, scale, max_blocks, nkv, pmax, (const bf16_t*)wo, (bf16_t*)o_out, N, B, sync, \
-      delay, poll_sleep)
-#define LG(KP, RR)                   \
-  switch (G) {                       \
-    case 1: LO(1, KP, RR); break;    \
-    case 2: LO(2, KP, RR); break;    \
-    case 4: LO(4, KP, RR); break;    \
-    case 8: LO(8, KP, RR); break;    \
-    case 16: LO(16, KP, RR); break;  \
-    default: return -2;              \
-  }
-  if (K == 1024) {
-    LG(16, 8)
-  } else if (K == 2048) {
-    LG(32, 8)
-  } else {
-    return -6;   // o_proj K must be 1024 or 2048 (TP = 8 / 4 shards of Llama-3.3-70B)
-  }
-#undef LG
-#undef LO
-  return (int)hipGetLastError();
-}
 
 extern "C" long long k8s_decode_split_workspace(int B, int nq, int nkv, int pmax) {
   if (nkv <= 0 || nq % nkv != 0) return -1;

@@ -27,12 +27,6 @@
 //    batch-64 decode 30.68 -> 30.46 ms/step bf16, 18.73 -> 18.30 fp8 (profiles/mgemm_fence_ab_r5.txt).
 //  * fp8: activations are quantized per token (fp8.hip), weights per row; the epilogue applies
 //    sx[m] * sw[n].  Non-scaled fp8 MFMA runs at the bf16 rate but halves the staged bytes.
-//  * fp8 weights x bf16 activations (W8, host mode fp8 = 2; the batched-decode regime): no activation
-//    quantization at all -- x is staged as bf16 (twice the row bytes of the weight k-step), every lane turns
-//    its 8 e4m3 weights of a k32 step into bf16 with v_cvt_scalef32_pk_bf16_fp8 (exact) and the MFMA is the
-//    bf16 one, the same rate as the non-scaled fp8 MFMA.  The weight bytes streamed are the fp8 ones; the RMS
-//    prologue works as for bf16 (the un-normalised residual is the x operand), so the fp8 QKV / gate-up / O /
-//    down projections of a 17-128-row decode step launch no quantize kernel.
 //  * MX activations (host mode fp8 = 3): x is OCP MX e4m3 -- one E8M0 scale per 32 values of a row (fp8.hip), as
 //    the SwiGLU epilogue below and the attention kernels write it -- and the MFMA is the block-scaled
 //    v_mfma_scale_f32_16x16x128_f8f6f4: lane (li, g) holds k 16 g.. and 64 + 16 g.. of its row and passes the scale
@@ -94,7 +88,7 @@ struct MgArgs {
   const uint8_t* xe;     // MX activations: E8M0 block scales, [K / 128][M] dwords (mx_scale_off)
   uint8_t* oq;           // MX output (SwiGLU): e4m3 [M][N_out] ...
   uint8_t* oe;           // ... and its E8M0 block scales, mx_scale_off layout (bf16 out not written)
-  long long kbytes;      // bytes per row of W (and of x, except W8: x rows are bf16, xkbytes)
+  long long kbytes;      // bytes per row of W (and of x)
   long long xkbytes;     // bytes per row of x
   long long total;       // tiles * T work items (one item = one tile x one 128-byte k-step)
   int M, N_out, half_rows;
@@ -103,7 +97,7 @@ struct MgArgs {
   const bf16_t* res;     // optional residual (bf16 [M][N_out], may alias out): out = acc + res  (bf16 epilogue)
   int rms;               // 1: RMSNorm prologue -- out scaled by 1 / rms(x row) (the gamma is folded into W)
   float eps;
-  int rms_mfma;          // bf16 / W8 rows: the row sums of squares from x . x^T on the MFMA (1) or v_dot2 (0)
+  int rms_mfma;          // bf16 rows: the row sums of squares from x . x^T on the MFMA (1) or v_dot2 (0)
   int fenced;            // split tiles: 1 = plain slab stores + agent-scope release / acquire fences (round-4 form)
 };
 
@@ -117,8 +111,7 @@ __device__ __forceinline__ int mg_swz_rb(int r) {
   return RB == 64 ? ((r >> 2) & 3) : RB == 128 ? ((r >> 1) & 7) : (r & 15);
 }
 
-template <int BM, int BN, int WM, int WN, int WK, int RB, int S, int EPI, bool FP8, bool W8 = false, bool MX = false,
-          bool MXO = false>
+template <int BM, int BN, int WM, int WN, int WK, int RB, int S, int EPI, bool FP8, bool MX = false, bool MXO = false>
 __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   constexpr int NW = WM * WN * WK;
   constexpr int FM = BM / (WM * 16), FN = BN / (WN * 16);
@@ -127,14 +120,13 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
   static_assert(S >= 2 && S <= 8, "ring depth");
   static_assert(WN == 1 || WN == 2 || WN == 4, "the RMS prologue splits a fragment's 4 dot2 over WN waves");
   static_assert(RB == 64 || RB == 128 || RB == 256 || RB == 512, "row bytes per k-step");
-  static_assert(!(FP8 && W8), "W8: fp8 weights with bf16 activations");
   static_assert(!MX || FP8, "MX: e4m3 activations with E8M0 block scales");
   static_assert(!MXO || (EPI == MG_SWIGLU && ((FN / 2) % 2 == 0 || (FN == 2 && WN % 2 == 0 && WK == 1))) ||
                     (EPI == MG_BF16 && FN % 2 == 0),
                 "MX output: SwiGLU with 32-feature spans per wave or wave pair, or the residual epilogue");
-  constexpr int XRB = W8 ? 2 * RB : RB;              // x row bytes per k-step (W8: RB bf16 values)
+  constexpr int XRB = RB;                            // x row bytes per k-step
   constexpr int CPR = RB / 16, XCPR = XRB / 16;      // 16-byte chunks per staged W / x row
-  constexpr int KS = (FP8 || W8) ? RB / 32 : RB / 64;   // k32 MFMA steps per k-step (RB = 64: one)
+  constexpr int KS = FP8 ? RB / 32 : RB / 64;        // k32 MFMA steps per k-step (RB = 64: one)
   static_assert(KS % WK == 0, "k32 steps split evenly over WK waves");
   constexpr int KS4 = RB / 128;                      // MX: 128-value subtiles per k-step, one scaled MFMA each
   static_assert(!MX || (KS4 >= 1 && KS4 % WK == 0), "MX: subtiles split evenly over WK waves");
@@ -264,15 +256,6 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
     for (int j = 0; j < FM; ++j) accsq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const bool rms_mfma = MX || a.rms_mfma != 0;
     const bool do_rms = (!FP8 || MX) && a.rms != 0;   // MX: the squares of the dequantized e4m3 values
-    // 8 e4m3 weights -> the bf16x8 A operand (exact; the row scale is applied in the epilogue)
-    auto w8_frag = [](long q) {
-      const uint32_t lo = (uint32_t)q, hi = (uint32_t)((unsigned long)q >> 32);
-      const bf16x2 p0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, false);
-      const bf16x2 p1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, true);
-      const bf16x2 p2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, false);
-      const bf16x2 p3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, true);
-      return bf16x8{p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
-    };
 
     auto compute = [&](int stage) {
       const char* wb = lds + stage * STAGE_B;
@@ -283,17 +266,9 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
         if constexpr (!FP8) {
           const int c = kk * 4 + g;
           bf16x8 af[FN], bfr[FM];
-          if constexpr (W8) {   // lane: 8 e4m3 of k = 32 kk + 8 g .. +8 (8 bytes of chunk 2 kk + g / 2)
-            const int cw = kk * 2 + (g >> 1), hb = (g & 1) * 8;
 #pragma unroll
-            for (int f = 0; f < FN; ++f)
-              af[f] = w8_frag(
-                  *reinterpret_cast<const long*>(wb + arow[f] * RB + ((cw ^ mg_swz_rb<RB>(arow[f])) << 4) + hb));
-          } else {
-#pragma unroll
-            for (int f = 0; f < FN; ++f)
-              af[f] = *reinterpret_cast<const bf16x8*>(wb + arow[f] * RB + ((c ^ mg_swz_rb<RB>(arow[f])) << 4));
-          }
+          for (int f = 0; f < FN; ++f)
+            af[f] = *reinterpret_cast<const bf16x8*>(wb + arow[f] * RB + ((c ^ mg_swz_rb<RB>(arow[f])) << 4));
 #pragma unroll
           for (int j = 0; j < FM; ++j) {
             const int r = brow0 + j * 16;
@@ -681,7 +656,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float gt = acc[f][j][i] * sx, up = acc[f + FN / 2][j][i] * sx;
-            if (FP8 || W8) { gt *= a.wsc[n0 + i]; up *= a.wsc[a.half_rows + n0 + i]; }
+            if (FP8) { gt *= a.wsc[n0 + i]; up *= a.wsc[a.half_rows + n0 + i]; }
             v[i] = mg_silu(gt) * up;
           }
           u32x2 o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
@@ -694,7 +669,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) mgemm_kernel(MgArgs a) {
           if (n0 >= a.N_out) continue;
           float v[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = acc[f][j][i] * sx * ((FP8 || W8) ? a.wsc[n0 + i] : 1.f);
+          for (int i = 0; i < 4; ++i) v[i] = acc[f][j][i] * sx * (FP8 ? a.wsc[n0 + i] : 1.f);
           if constexpr (EPI == MG_F32) {
             *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + (long long)m * a.N_out + n0) =
                 f32x4{v[0], v[1], v[2], v[3]};
@@ -758,7 +733,7 @@ constexpr MgCfg kMgCfgs[] = {
     {256, 128, 2, 2, 1, 64, 5},   // 25
     {128, 256, 2, 4, 1, 64, 6},   // 26  8 waves
     {256, 128, 2, 4, 1, 64, 5},   // 27  8 waves
-    // --- 64-row weight-streaming tiles whose W8 image (x staged as bf16) fits: 4-deep rings of 128-byte k-steps
+    // --- 64-row weight-streaming tiles: 4-deep rings of 128-byte k-steps
     {64, 32, 2, 1, 2, 128, 4},    // 28
     {64, 64, 2, 2, 1, 128, 4},    // 29
     {64, 128, 1, 4, 1, 128, 4},   // 30
@@ -772,13 +747,10 @@ constexpr MgCfg kMgCfgs[] = {
 };
 constexpr int kMgNumCfgs = sizeof(kMgCfgs) / sizeof(kMgCfgs[0]);
 
-// LDS bytes of config c in mode (0 bf16, 1 fp8 x and W, 2 W8: fp8 W, bf16 x, 3 MX: fp8 W, MX x)
+// LDS bytes of config c in mode (0 bf16, 1 fp8 x and W, 3 MX: fp8 W, MX x)
 constexpr int mg_lds_bytes(const MgCfg c, int mode) {
-  return c.s * (c.bn * c.rb + c.bm * c.rb * (mode == 2 ? 2 : 1) + (mode == 3 ? c.bm * (c.rb / 32) : 0)) + 16 +
-         c.wk * c.wn * c.bm * 4;
+  return c.s * (c.bn * c.rb + c.bm * c.rb + (mode == 3 ? c.bm * (c.rb / 32) : 0)) + 16 + c.wk * c.wn * c.bm * 4;
 }
-// W8 is built for the weight-streaming configurations (batched decode) only
-constexpr bool mg_w8_cfg(int c) { return c <= 14 || (c >= 28 && c <= 31); }
 // MX activations: 128-value subtiles split evenly over the k-sharing waves, scale dwords evenly over all waves
 constexpr bool mg_mx_cfg(int c) {
   return kMgCfgs[c].rb >= 128 && (kMgCfgs[c].rb / 128) % kMgCfgs[c].wk == 0 &&
@@ -794,44 +766,43 @@ constexpr bool mg_mxo_cfg(int c) {
 // residual epilogue with MX output: fragment pairs per wave
 constexpr bool mg_mxr_cfg(int c) { return (kMgCfgs[c].bn / (kMgCfgs[c].wn * 16)) % 2 == 0; }
 
-template <int C, int EPI, bool FP8, bool W8, bool MX, bool MXO>
+template <int C, int EPI, bool FP8, bool MX, bool MXO>
 int mg_launch(const MgArgs& a, int grid, hipStream_t s) {
   constexpr bool ok = (EPI != MG_SWIGLU || (kMgCfgs[C].bn / (kMgCfgs[C].wn * 16)) % 2 == 0) &&
-                      (!W8 || (mg_w8_cfg(C) && mg_lds_bytes(kMgCfgs[C], 2) <= 160 * 1024)) &&
                       (!MX || mg_mx_cfg(C)) &&
                       (!MXO || (EPI == MG_SWIGLU && mg_mxo_cfg(C)) || (EPI == MG_BF16 && mg_mxr_cfg(C)));
   if constexpr (!ok) {
     return -2;
   } else {
     hipLaunchKernelGGL((mgemm_kernel<kMgCfgs[C].bm, kMgCfgs[C].bn, kMgCfgs[C].wm, kMgCfgs[C].wn, kMgCfgs[C].wk,
-                                      kMgCfgs[C].rb, kMgCfgs[C].s, EPI, FP8, W8, MX, MXO>),
+                                      kMgCfgs[C].rb, kMgCfgs[C].s, EPI, FP8, MX, MXO>),
                        dim3(grid), dim3(64 * kMgCfgs[C].wm * kMgCfgs[C].wn * kMgCfgs[C].wk), 0, s, a);
     return (int)hipGetLastError();
   }
 }
 
-template <int C, bool FP8, bool W8, bool MX>
+template <int C, bool FP8, bool MX>
 int mg_epi(const MgArgs& a, int grid, int epi, bool mxo, hipStream_t s) {
   if constexpr (FP8) {   // MX output: the SwiGLU / residual epilogues of the fp8 and MX modes
     if (mxo) {
-      if (epi == MG_SWIGLU) return mg_launch<C, MG_SWIGLU, FP8, W8, MX, true>(a, grid, s);
-      if (epi == MG_BF16) return mg_launch<C, MG_BF16, FP8, W8, MX, true>(a, grid, s);
+      if (epi == MG_SWIGLU) return mg_launch<C, MG_SWIGLU, FP8, MX, true>(a, grid, s);
+      if (epi == MG_BF16) return mg_launch<C, MG_BF16, FP8, MX, true>(a, grid, s);
       return -2;
     }
   }
   switch (epi) {
-    case MG_BF16: return mg_launch<C, MG_BF16, FP8, W8, MX, false>(a, grid, s);
-    case MG_F32: return mg_launch<C, MG_F32, FP8, W8, MX, false>(a, grid, s);
-    case MG_SWIGLU: return mg_launch<C, MG_SWIGLU, FP8, W8, MX, false>(a, grid, s);
+    case MG_BF16: return mg_launch<C, MG_BF16, FP8, MX, false>(a, grid, s);
+    case MG_F32: return mg_launch<C, MG_F32, FP8, MX, false>(a, grid, s);
+    case MG_SWIGLU: return mg_launch<C, MG_SWIGLU, FP8, MX, false>(a, grid, s);
   }
   return -2;
 }
 
-template <bool FP8, bool W8, bool MX, int C = 0>
+template <bool FP8, bool MX, int C = 0>
 int mg_cfg(const MgArgs& a, int grid, int cfg, int epi, bool mxo, hipStream_t s) {
   if constexpr (C < kMgNumCfgs) {
-    if (cfg == C) return mg_epi<C, FP8, W8, MX>(a, grid, epi, mxo, s);
-    return mg_cfg<FP8, W8, MX, C + 1>(a, grid, cfg, epi, mxo, s);
+    if (cfg == C) return mg_epi<C, FP8, MX>(a, grid, epi, mxo, s);
+    return mg_cfg<FP8, MX, C + 1>(a, grid, cfg, epi, mxo, s);
   } else {
     return -4;
   }
@@ -856,15 +827,14 @@ bool mg_mxo_valid(int cfg) {
 bool mg_mxr_valid(int cfg) { return cfg >= 0 && cfg < kMgNumCfgs && (kMgCfgs[cfg].bn / (kMgCfgs[cfg].wn * 16)) % 2 == 0; }
 }  // namespace
 
-// LDS bytes of a config in a mode (0 bf16, 1 fp8, 2 W8, 3 MX activations); -1: the config is not built for that
-// mode.  Mode 4: 0 if the config's SwiGLU epilogue can write MX output, else -1; mode 5: the same for the residual
+// LDS bytes of a config in a mode (0 bf16, 1 fp8, 3 MX activations; 2 is not a mode); -1: the config is not built for
+// that mode.  Mode 4: 0 if the config's SwiGLU epilogue can write MX output, else -1; mode 5: the same for the residual
 // epilogue.
 extern "C" int k8s_mgemm_lds_bytes(int cfg, int mode) {
-  if (cfg < 0 || cfg >= kMgNumCfgs || mode < 0 || mode > 5) return -1;
+  if (cfg < 0 || cfg >= kMgNumCfgs || mode < 0 || mode > 5 || mode == 2) return -1;
   if (mode == 4) return mg_mxo_valid(cfg) ? 0 : -1;
   if (mode == 5) return mg_mxr_valid(cfg) ? 0 : -1;
   const int b = mg_lds_bytes(kMgCfgs[cfg], mode);
-  if (mode == 2 && (!mg_w8_cfg(cfg) || b > 160 * 1024)) return -1;
   if (mode == 3 && !mg_mx_valid(cfg)) return -1;
   return b;
 }
@@ -916,32 +886,29 @@ extern "C" int k8s_mgemm_plan_info(int M, int N_out, int K, int epi, int fp8, in
 }
 
 // out[M, N_out] = epi(x[M, K] . W^T) with `nwg` workgroups streaming equal shares of the
-// (tile, k-step) items.  fp8 = 1: x / W are e4m3 bytes with per-row scales xs / wsc; fp8 = 2 (W8): W is e4m3
-// with row scales wsc, x is bf16 (no activation scales; the RMS prologue is allowed); fp8 = 3 (MX): W e4m3 with row
+// (tile, k-step) items.  fp8 = 1: x / W are e4m3 bytes with per-row scales xs / wsc; fp8 = 3 (MX): W e4m3 with row
 // scales wsc, x MX e4m3 with its E8M0 block scales in xs (bytes, mx_scale_off layout).  oq / oe (fp8 = 1 or 3, SwiGLU): the
 // output is written as MX e4m3 [M][N_out] + E8M0 (mx_scale_off layout) instead of bf16 (out unused).
 // SwiGLU: W holds 2 * N_out rows ([gate; up]); out has N_out columns.
 extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x, const void* W, const float* xs,
                          const float* wsc, int M, int N_out, int K, int epi, int fp8, int cfg, int nwg, int cmax,
-                         const void* res, int rms, float eps, void* oq, void* oe, hipStream_t stream) {
+                         const void* res, int rms, float eps, void* oq, void* oe, int fenced, hipStream_t stream) {
   if (cfg < 0 || cfg >= kMgNumCfgs || M <= 0 || N_out <= 0 || K <= 0 || nwg <= 0 || cmax < 1) return -1;
   if (N_out % 4 != 0) return -1;
-  if (fp8 < 0 || fp8 > 3) return -1;
-  const bool w8 = fp8 == 2, mx = fp8 == 3, mxo = oq != nullptr;
+  if (fp8 < 0 || fp8 > 3 || fp8 == 2) return -1;
+  const bool mx = fp8 == 3, mxo = oq != nullptr;
   if (mxo && (oe == nullptr || (fp8 != 1 && fp8 != 3) || N_out % 128 != 0 ||
               !(epi == MG_SWIGLU ? mg_mxo_valid(cfg) : (epi == MG_BF16 && res != nullptr && mg_mxr_valid(cfg)))))
     return -7;
   if (mx && (K % 128 != 0 || !mg_mx_valid(cfg))) return -7;
-  const long long kbytes = (long long)K * (fp8 ? 1 : 2), xkbytes = (long long)K * ((fp8 == 1 || fp8 == 3) ? 1 : 2);
+  const long long kbytes = (long long)K * (fp8 ? 1 : 2), xkbytes = kbytes;
   if (kbytes % kMgCfgs[cfg].rb != 0) return -1;
-  if (w8 && k8s_mgemm_lds_bytes(cfg, 2) < 0) return -4;
   const MgGeom g = mg_geom(M, N_out, K, epi, fp8, cfg);
   if (nwg > g.total) return -1;
   if (cmax > 1 && (ws == nullptr || tickets == nullptr)) return -3;
   const long long wrows = epi == MG_SWIGLU ? 2LL * N_out : (long long)N_out;
   if (wrows * kbytes >= (1LL << 32) || (long long)M * xkbytes >= (1LL << 32)) return -5;  // 32-bit DMA offsets
   if ((fp8 == 1 || fp8 == 3) && (xs == nullptr || wsc == nullptr)) return -3;
-  if (w8 && wsc == nullptr) return -3;
   if (res != nullptr && epi != MG_BF16) return -6;   // residual epilogue: bf16 output only
   if (rms && fp8 == 1) return -6;   // per-token e4m3 activations carry 1 / rms in their scales (MX rows: prologue)
   MgArgs a;
@@ -954,8 +921,7 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   // K8S_RMS_MFMA = 0 / 1 forces one form.
   static const int rms_mfma_env = [] { const char* e = getenv("K8S_RMS_MFMA"); return e ? atoi(e) : -1; }();
   a.rms_mfma = rms_mfma_env >= 0 ? rms_mfma_env : (N_out >= 8192 ? 1 : 0);
-  static const int fenced = [] { const char* e = getenv("K8S_MGEMM_FENCED"); return e ? atoi(e) : 0; }();
-  a.fenced = fenced;
+  a.fenced = fenced;   // (ops.mgemm: K8S_MGEMM_FENCED, or per call in the fenced-vs-fence-free test)
   a.out = out;
   a.ws = ws;
   a.cnt = tickets;
@@ -976,8 +942,6 @@ extern "C" int k8s_mgemm(void* out, float* ws, unsigned* tickets, const void* x,
   a.T = (int)g.T;
   a.nwg = nwg;
   a.cmax = cmax;
-  if (w8) return mg_cfg<false, true, false>(a, nwg, cfg, epi, false, stream);
-  if (mx) return mg_cfg<true, false, true>(a, nwg, cfg, epi, mxo, stream);
-  return fp8 ? mg_cfg<true, false, false>(a, nwg, cfg, epi, mxo, stream)
-             : mg_cfg<false, false, false>(a, nwg, cfg, epi, false, stream);
+  if (mx) return mg_cfg<true, true>(a, nwg, cfg, epi, mxo, stream);
+  return fp8 ? mg_cfg<true, false>(a, nwg, cfg, epi, mxo, stream) : mg_cfg<false, false>(a, nwg, cfg, epi, false, stream);
 }

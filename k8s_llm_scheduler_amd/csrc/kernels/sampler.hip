@@ -189,7 +189,8 @@ struct Slice {
   const float* base;
   int j0, j1, id0;
 };
-__device__ __forceinline__ Slice slice_of(const float* logits, int b, int B, int Vs, int shards) {
+// id_base: global id of this buffer's first token (vocab-parallel sampling: rank * Vs; 0 for a gathered buffer)
+__device__ __forceinline__ Slice slice_of(const float* logits, int b, int B, int Vs, int shards, int id_base) {
   const int per_shard = gridDim.x / shards;
   const int s = blockIdx.x / per_shard, q = blockIdx.x - s * per_shard;
   const int per = (Vs + per_shard - 1) / per_shard;
@@ -197,7 +198,7 @@ __device__ __forceinline__ Slice slice_of(const float* logits, int b, int B, int
   r.base = logits + ((size_t)s * B + b) * Vs;
   r.j0 = q * per;
   r.j1 = min(Vs, r.j0 + per);
-  r.id0 = s * Vs;
+  r.id0 = id_base + s * Vs;
   return r;
 }
 
@@ -207,15 +208,17 @@ __device__ __forceinline__ bool nuc_row(int b, const int* ctx_inc, const int* sl
          top_p[b] < 1.f;
 }
 
-// pass 1: row max of the logits (ordered-key atomicMax)
+// pass 1: row max of the logits (ordered-key atomicMax into maxkey[b * mstride]: the row state's maxkey, or -- vocab
+// parallel -- this rank's exported row maxima, combined over the ranks by nuc_import_max_kernel)
 __global__ void __launch_bounds__(ST) nuc_max_kernel(const float* __restrict__ logits, int B, int Vs, int shards,
                                                      const float* __restrict__ temperature,
                                                      const float* __restrict__ top_p, const int* __restrict__ ctx_inc,
-                                                     const int* __restrict__ slots, NucRow* __restrict__ st) {
+                                                     const int* __restrict__ slots, uint32_t* __restrict__ maxkey,
+                                                     int mstride) {
   __shared__ float red[ST / 64];
   const int b = blockIdx.y;
   if (!nuc_row(b, ctx_inc, slots, temperature, top_p)) return;
-  const Slice sl = slice_of(logits, b, B, Vs, shards);
+  const Slice sl = slice_of(logits, b, B, Vs, shards, 0);
   float m = -INFINITY;
   for (int j = sl.j0 + threadIdx.x; j < sl.j1; j += ST) m = fmaxf(m, sl.base[j]);
   m = wave_max(m);
@@ -223,18 +226,61 @@ __global__ void __launch_bounds__(ST) nuc_max_kernel(const float* __restrict__ l
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < ST / 64; ++w) m = fmaxf(m, red[w]);
-    __hip_atomic_fetch_max(&st[b].maxkey, ord_key(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(&maxkey[(size_t)b * mstride], ord_key(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Bin totals of one row (thread = bin; every thread of the workgroup calls this): inclusive scan, then the first bin
+// where the cumulative mass reaches the target.  LEVEL 0 stores target / mass above b* / b*, LEVEL 1 f* in the row
+// state.  sh_sel must be 256 on entry.
+template <int LEVEL>
+__device__ __forceinline__ void nuc_select(unsigned long long tot, int b, const float* __restrict__ top_p,
+                                           NucRow* __restrict__ st, unsigned long long (*scan)[256], int* sh_sel) {
+  const int tid = threadIdx.x;
+  int cur = 0;
+  scan[0][tid] = tot;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const unsigned long long v = scan[cur][tid] + (tid >= o ? scan[cur][tid - o] : 0ull);
+    scan[cur ^ 1][tid] = v;
+    cur ^= 1;
+    __syncthreads();
+  }
+  const unsigned long long incl = scan[cur][tid];
+  unsigned long long target, base;
+  if (LEVEL == 0) {
+    const unsigned long long Z = scan[cur][255];
+    target = (unsigned long long)((double)Z * (double)top_p[b]);
+    base = 0ull;
+  } else {
+    target = __hip_atomic_load(&st[b].target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base = __hip_atomic_load(&st[b].above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tot != 0ull && base + incl >= target) atomicMin(sh_sel, tid);
+  __syncthreads();
+  if (tid == (*sh_sel == 256 ? 255 : *sh_sel)) {
+    if (LEVEL == 0) {
+      __hip_atomic_store(&st[b].target, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&st[b].above, incl - tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&st[b].bstar, (uint32_t)tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint32_t bstar = __hip_atomic_load(&st[b].bstar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&st[b].fstar, (bstar << 8) | (uint32_t)tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
 // passes 2 (LEVEL 0: coarse bins f >> 8 over every token) and 3 (LEVEL 1: fine bins f & 255 of the
-// tokens in coarse bin b*).  ws: [B][gridDim.x][256] u64 partial histograms.
+// tokens in coarse bin b*).  ws: [B][gridDim.x][256] u64 partial histograms.  exp_out (vocab-parallel
+// sampling): the last arriver writes this rank's bin totals to exp_out[b][256] instead of selecting --
+// nuc_scan_kernel selects from the sum over the ranks (integer masses: the same totals as a gathered row).
 template <int LEVEL>
 __global__ void __launch_bounds__(ST) nuc_hist_kernel(const float* __restrict__ logits, int B, int Vs, int shards,
                                                       const float* __restrict__ temperature,
                                                       const float* __restrict__ top_p, const int* __restrict__ ctx_inc,
                                                       const int* __restrict__ slots, NucRow* __restrict__ st,
-                                                      unsigned long long* __restrict__ ws) {
+                                                      unsigned long long* __restrict__ ws,
+                                                      unsigned long long* __restrict__ exp_out) {
   __shared__ unsigned long long h[ST / 64][256];   // one histogram per wave: 4x fewer colliding atomics
   __shared__ unsigned long long scan[2][256];
   __shared__ uint32_t sh_prev;
@@ -248,7 +294,7 @@ __global__ void __launch_bounds__(ST) nuc_hist_kernel(const float* __restrict__ 
 #pragma unroll
   for (int w = 0; w < ST / 64; ++w) h[w][tid] = 0ull;
   __syncthreads();
-  const Slice sl = slice_of(logits, b, B, Vs, shards);
+  const Slice sl = slice_of(logits, b, B, Vs, shards, 0);
   for (int j = sl.j0 + tid; j < sl.j1; j += ST) {
     const float l = sl.base[j];
     const int f = nuc_fine(l, M, invT);
@@ -292,36 +338,45 @@ __global__ void __launch_bounds__(ST) nuc_hist_kernel(const float* __restrict__ 
       for (int k = 0; k < 16; ++k) tot += ((unsigned long long)v[k][1] << 32) | v[k][0];
     }
   }
-  int cur = 0;
-  scan[0][tid] = tot;
-  __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
-    const unsigned long long v = scan[cur][tid] + (tid >= o ? scan[cur][tid - o] : 0ull);
-    scan[cur ^ 1][tid] = v;
-    cur ^= 1;
-    __syncthreads();
+  if (exp_out != nullptr) {
+    exp_out[(size_t)b * 256 + tid] = tot;
+    return;
   }
-  const unsigned long long incl = scan[cur][tid];
-  unsigned long long target, base;
-  if (LEVEL == 0) {
-    const unsigned long long Z = scan[cur][255];
-    target = (unsigned long long)((double)Z * (double)top_p[b]);
-    base = 0ull;
-  } else {
-    target = __hip_atomic_load(&st[b].target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    base = __hip_atomic_load(&st[b].above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (tot != 0ull && base + incl >= target) atomicMin(&sh_sel, tid);
-  __syncthreads();
-  if (tid == (sh_sel == 256 ? 255 : sh_sel)) {
-    if (LEVEL == 0) {
-      __hip_atomic_store(&st[b].target, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&st[b].above, incl - tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&st[b].bstar, (uint32_t)tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(&st[b].fstar, (bstar << 8) | (uint32_t)tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  nuc_select<LEVEL>(tot, b, top_p, st, scan, &sh_sel);
+}
+
+// ---- vocab-parallel sampling: the combine steps after a (tiny) all-gather over the TP ranks
+// Row max: st[b].maxkey = max over the ranks' exported maxima g[r * ld + b]; this rank's export is re-armed to 0
+// (the all-gather that read it has run: stream order).  One thread per row.
+__global__ void __launch_bounds__(ST) nuc_import_max_kernel(const uint32_t* __restrict__ g, int ld, int ranks, int B,
+                                                            const float* __restrict__ temperature,
+                                                            const float* __restrict__ top_p,
+                                                            const int* __restrict__ ctx_inc,
+                                                            const int* __restrict__ slots, NucRow* __restrict__ st,
+                                                            uint32_t* __restrict__ mine) {
+  const int b = blockIdx.x * ST + threadIdx.x;
+  if (b >= B) return;
+  mine[b] = 0u;
+  if (!nuc_row(b, ctx_inc, slots, temperature, top_p)) return;
+  uint32_t m = 0u;
+  for (int r = 0; r < ranks; ++r) m = max(m, g[(size_t)r * ld + b]);
+  __hip_atomic_store(&st[b].maxkey, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Bin totals summed over the ranks' exports g[r][B][256] (grid B), then the selection of nuc_hist_kernel.
+template <int LEVEL>
+__global__ void __launch_bounds__(ST) nuc_scan_kernel(const unsigned long long* __restrict__ g, int ranks, int B,
+                                                      const float* __restrict__ temperature,
+                                                      const float* __restrict__ top_p, const int* __restrict__ ctx_inc,
+                                                      const int* __restrict__ slots, NucRow* __restrict__ st) {
+  __shared__ unsigned long long scan[2][256];
+  __shared__ int sh_sel;
+  const int b = blockIdx.x;
+  if (!nuc_row(b, ctx_inc, slots, temperature, top_p)) return;
+  unsigned long long tot = 0ull;
+  for (int r = 0; r < ranks; ++r) tot += g[((size_t)r * B + b) * 256 + threadIdx.x];
+  if (threadIdx.x == 0) sh_sel = 256;
+  nuc_select<LEVEL>(tot, b, top_p, st, scan, &sh_sel);
 }
 
 // grid (nbx, B); row_key [B] u64 and row_cnt [B] u32 must be zero before the first launch (the
@@ -333,7 +388,8 @@ __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, co
                                                     int* __restrict__ hist, int hist_stride, int* __restrict__ steps,
                                                     unsigned long long* __restrict__ row_key,
                                                     uint32_t* __restrict__ row_cnt, NucRow* __restrict__ nuc,
-                                                    const int* __restrict__ slots, StopArgs sa) {
+                                                    const int* __restrict__ slots, StopArgs sa, int id_base,
+                                                    unsigned long long* __restrict__ keys_out) {
   __shared__ float sv[ST / 64];
   __shared__ int si[ST / 64];
   const int b = blockIdx.y;
@@ -342,7 +398,7 @@ __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, co
   const float T = temperature[b];
   const uint32_t seed = seeds[b];
   const uint32_t ctr = counter ? (uint32_t)counter[b] : 0u;
-  const Slice sl = slice_of(logits, b, B, Vs, shards);
+  const Slice sl = slice_of(logits, b, B, Vs, shards, id_base);
   ArgMax best{-INFINITY, 0x7fffffff};
   if (T <= 0.f) {
     for (int j = sl.j0 + threadIdx.x; j < sl.j1; j += ST) best = better(best, ArgMax{sl.base[j], sl.id0 + j});
@@ -371,7 +427,6 @@ __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, co
     const uint32_t arrived = __hip_atomic_fetch_add(&row_cnt[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (arrived == gridDim.x - 1) {  // last arriver: every other workgroup's max is already folded in
       const unsigned long long k = __hip_atomic_load(&row_key[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int tok = (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull));
       __hip_atomic_store(&row_key[b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&row_cnt[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (nuc != nullptr && T > 0.f && top_p[b] < 1.f) {   // re-arm the nucleus row state (every
@@ -380,9 +435,31 @@ __global__ void __launch_bounds__(ST) sample_kernel(int* __restrict__ tokens, co
         __hip_atomic_store(&w->cnt0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&w->cnt1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      write_token(s, tok, tokens, ctx_inc, hist, hist_stride, steps, sa);
+      if (keys_out != nullptr) {   // vocab-parallel: this rank's best key; sample_merge_kernel picks over the ranks
+        keys_out[b] = k;
+      } else {
+        write_token(s, (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)), tokens, ctx_inc, hist, hist_stride, steps,
+                    sa);
+      }
     }
   }
+}
+
+// Vocab-parallel sampling, last step: the row's token is the best of the ranks' keys g[r * ld + b] (packed
+// score | ~global id: the same maximum as one pass over the gathered logits, ties to the lowest id), then the
+// decode-state update of sample_kernel.  Every rank runs it on the same gathered keys: the same token everywhere.
+__global__ void __launch_bounds__(64) sample_merge_kernel(int* __restrict__ tokens,
+                                                          const unsigned long long* __restrict__ g, int ld, int ranks,
+                                                          int B, int* __restrict__ ctx_inc, int* __restrict__ hist,
+                                                          int hist_stride, int* __restrict__ steps,
+                                                          const int* __restrict__ slots, StopArgs sa) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  const int s = slots != nullptr ? slots[b] : b;
+  if (ctx_inc != nullptr && ctx_inc[s] <= 0) return;
+  unsigned long long k = 0ull;
+  for (int r = 0; r < ranks; ++r) k = max(k, g[(size_t)r * ld + b]);
+  write_token(s, (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)), tokens, ctx_inc, hist, hist_stride, steps, sa);
 }
 
 __host__ __device__ inline int grid_x(int shards) { return shards * ((NB + shards - 1) / shards); }
@@ -399,6 +476,21 @@ using namespace k8sllm;
 //                the row states zero before the first call and left zero; the histograms are fully
 //                rewritten by every launch before they are read.
 constexpr int SAMPLE_ROW_CAP = 4096;
+
+static bool make_stop_args(StopArgs& sa, const int* cls, int* json, const int* cfg, const int* forced,
+                           const int* forced_len, int fstride, int eos_tok, int* done, const int* hist,
+                           const int* ctx_inc) {
+  sa.cls = reinterpret_cast<const int2*>(cls);
+  sa.json = json;
+  sa.cfg = cfg;
+  sa.forced = forced;
+  sa.forced_len = forced_len;
+  sa.fstride = fstride;
+  sa.eos_tok = eos_tok;
+  sa.done = done;
+  return !(sa.cls != nullptr && (sa.json == nullptr || sa.cfg == nullptr || hist == nullptr || ctx_inc == nullptr ||
+                                 (sa.forced != nullptr && sa.forced_len == nullptr)));
+}
 // slots (or null): decode-state slot of every row (tokens / ctx_inc / hist / steps / stop state are indexed by
 // slot; temperature / top_p / seeds / counter by row).  stop_*: device-side stop detection (null cls = off).
 extern "C" int k8s_sample(int* tokens, const float* logits, int B, int Vs, int shards, const float* temperature,
@@ -406,7 +498,7 @@ extern "C" int k8s_sample(int* tokens, const float* logits, int B, int Vs, int s
                           int hist_stride, int* steps, void* scratch, void* nuc_scratch, const int* slots,
                           const int* stop_cls, int* stop_json, const int* stop_cfg, const int* stop_forced,
                           const int* stop_forced_len, int stop_fstride, int stop_eos_tok, int* stop_done,
-                          hipStream_t stream) {
+                          int id_base, void* keys_out, int nuc_passes, hipStream_t stream) {
   if (B <= 0) return 0;
   if (B > SAMPLE_ROW_CAP) return -2;
   if (hist != nullptr && steps == nullptr) return -1;
@@ -419,24 +511,90 @@ extern "C" int k8s_sample(int* tokens, const float* logits, int B, int Vs, int s
   if (nuc_scratch != nullptr) {
     st = static_cast<NucRow*>(nuc_scratch);
     auto* ws = reinterpret_cast<unsigned long long*>(st + SAMPLE_ROW_CAP);
-    nuc_max_kernel<<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, slots, st);
-    nuc_hist_kernel<0><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, slots, st, ws);
-    nuc_hist_kernel<1><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, slots, st, ws);
+    if (nuc_passes) {   // (vocab-parallel sampling runs them itself, with its combine steps between)
+      nuc_max_kernel<<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, slots, &st->maxkey,
+                                              (int)(sizeof(NucRow) / sizeof(uint32_t)));
+      nuc_hist_kernel<0><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, slots, st, ws,
+                                                  nullptr);
+      nuc_hist_kernel<1><<<grid, ST, 0, stream>>>(logits, B, Vs, shards, temperature, top_p, ctx_inc, slots, st, ws,
+                                                  nullptr);
+    }
   }
   StopArgs sa;
-  sa.cls = reinterpret_cast<const int2*>(stop_cls);
-  sa.json = stop_json;
-  sa.cfg = stop_cfg;
-  sa.forced = stop_forced;
-  sa.forced_len = stop_forced_len;
-  sa.fstride = stop_fstride;
-  sa.eos_tok = stop_eos_tok;
-  sa.done = stop_done;
-  if (sa.cls != nullptr && (sa.json == nullptr || sa.cfg == nullptr || hist == nullptr || ctx_inc == nullptr ||
-                            (sa.forced != nullptr && sa.forced_len == nullptr)))
+  if (!make_stop_args(sa, stop_cls, stop_json, stop_cfg, stop_forced, stop_forced_len, stop_fstride, stop_eos_tok,
+                      stop_done, hist, ctx_inc))
     return -1;
   sample_kernel<<<grid, ST, 0, stream>>>(tokens, logits, B, Vs, shards, temperature, top_p, seeds, counter, ctx_inc,
-                                         hist, hist_stride, steps, key, cnt, st, slots, sa);
+                                         hist, hist_stride, steps, key, cnt, st, slots, sa, id_base,
+                                         static_cast<unsigned long long*>(keys_out));
+  return (int)hipGetLastError();
+}
+
+// Vocab-parallel sampling (each TP rank samples its own vocabulary shard; rows exchange a few bytes instead of
+// their logits).  Per call, on the local shard [B][Vs] (shards = 1, global ids from id_base):
+//   nucleus rows only:  local(-1) -> all-gather u32 [B] -> combine(-1)        (row max)
+//                       local(0)  -> all-gather u64 [B][256] -> combine(0)    (coarse bin b*)
+//                       local(1)  -> all-gather u64 [B][256] -> combine(1)    (fine bin f*)
+//   every row:          k8s_sample(keys_out, nuc_passes = 0) -> all-gather u64 [B] -> k8s_sample_merge
+// local: level -1 writes this rank's row maxima to out (u32 [B], zero before the call: combine(-1) re-arms it);
+// levels 0 / 1 this rank's bin totals to out (u64 [B][256]).
+extern "C" int k8s_sample_nuc_local(int level, const float* logits, int B, int Vs, const float* temperature,
+                                    const float* top_p, const int* ctx_inc, const int* slots, void* nuc_scratch,
+                                    void* out, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (B > SAMPLE_ROW_CAP || Vs < 1 || nuc_scratch == nullptr || out == nullptr) return -2;
+  auto* st = static_cast<NucRow*>(nuc_scratch);
+  auto* ws = reinterpret_cast<unsigned long long*>(st + SAMPLE_ROW_CAP);
+  const dim3 grid(grid_x(1), B);
+  auto* o64 = static_cast<unsigned long long*>(out);
+  if (level < 0)
+    nuc_max_kernel<<<grid, ST, 0, stream>>>(logits, B, Vs, 1, temperature, top_p, ctx_inc, slots,
+                                            static_cast<uint32_t*>(out), 1);
+  else if (level == 0)
+    nuc_hist_kernel<0><<<grid, ST, 0, stream>>>(logits, B, Vs, 1, temperature, top_p, ctx_inc, slots, st, ws, o64);
+  else
+    nuc_hist_kernel<1><<<grid, ST, 0, stream>>>(logits, B, Vs, 1, temperature, top_p, ctx_inc, slots, st, ws, o64);
+  return (int)hipGetLastError();
+}
+
+// combine: g = the all-gathered exports ([ranks][ld] u32 for level -1, with mine = this rank's export to re-arm;
+// [ranks][B][256] u64 for levels 0 / 1).
+extern "C" int k8s_sample_nuc_combine(int level, const void* g, int ld, int ranks, int B, const float* temperature,
+                                      const float* top_p, const int* ctx_inc, const int* slots, void* nuc_scratch,
+                                      void* mine, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (B > SAMPLE_ROW_CAP || ranks < 1 || nuc_scratch == nullptr || g == nullptr) return -2;
+  auto* st = static_cast<NucRow*>(nuc_scratch);
+  if (level < 0) {
+    if (mine == nullptr || ld < B) return -2;
+    nuc_import_max_kernel<<<(B + ST - 1) / ST, ST, 0, stream>>>(static_cast<const uint32_t*>(g), ld, ranks, B,
+                                                                temperature, top_p, ctx_inc, slots, st,
+                                                                static_cast<uint32_t*>(mine));
+  } else if (level == 0) {
+    nuc_scan_kernel<0><<<B, ST, 0, stream>>>(static_cast<const unsigned long long*>(g), ranks, B, temperature, top_p,
+                                             ctx_inc, slots, st);
+  } else {
+    nuc_scan_kernel<1><<<B, ST, 0, stream>>>(static_cast<const unsigned long long*>(g), ranks, B, temperature, top_p,
+                                             ctx_inc, slots, st);
+  }
+  return (int)hipGetLastError();
+}
+
+// merge: g = the all-gathered keys [ranks][ld] u64 (k8s_sample's keys_out of every rank); the decode-state update and
+// stop detection of k8s_sample.
+extern "C" int k8s_sample_merge(int* tokens, const void* g, int ld, int ranks, int B, int* ctx_inc, int* hist,
+                                int hist_stride, int* steps, const int* slots, const int* stop_cls, int* stop_json,
+                                const int* stop_cfg, const int* stop_forced, const int* stop_forced_len,
+                                int stop_fstride, int stop_eos_tok, int* stop_done, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (ld < B || ranks < 1 || g == nullptr) return -2;
+  if (hist != nullptr && steps == nullptr) return -1;
+  StopArgs sa;
+  if (!make_stop_args(sa, stop_cls, stop_json, stop_cfg, stop_forced, stop_forced_len, stop_fstride, stop_eos_tok,
+                      stop_done, hist, ctx_inc))
+    return -1;
+  sample_merge_kernel<<<(B + 63) / 64, 64, 0, stream>>>(tokens, static_cast<const unsigned long long*>(g), ld, ranks,
+                                                          B, ctx_inc, hist, hist_stride, steps, slots, sa);
   return (int)hipGetLastError();
 }
 

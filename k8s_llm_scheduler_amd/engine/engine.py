@@ -66,6 +66,11 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
                  watchdog_s: float = 60.0, on_unrecoverable: str = "stay", device_stop: bool = True,
                  mixed_steps: bool = True, mixed_step_rows: int = 256):
         self.model = model
+        # Vocab-parallel sampling at TP > 1: the model returns this rank's logits shard and the
+        # sampler exchanges a few bytes per row (ops.sample(tp=...)), so no step all-gathers rows x vocab x 4 B.
+        # K8S_VOCAB_PARALLEL=0: all-gather the logits and sample the full rows (same tokens).
+        self.vocab_parallel = model.tp.world > 1 and os.environ.get("K8S_VOCAB_PARALLEL", "1") != "0"
+        model.gather_logits = not self.vocab_parallel
         # Device-side stop detection: the decode graphs' sampler finishes rows itself (EOS,
         # closed JSON object, max_tokens) and raises a host-mapped flag; the host checks it after every replay
         # instead of after a whole decode_chunk.  Mixed steps (item 5): a prefill step also advances every
@@ -443,7 +448,7 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
                        self.s_seeds.index_select(0, d), ctx_d.clone(), shards=ld.shape[0], tokens_out=self.s_tokens,
                        ctx_inc=self.s_ctx, hist=self.s_hist, steps=self.s_steps,
                        nucleus=self._wants_nucleus(self.running[x] for x in dec), slots=d.to(torch.int32),
-                       stop=self._stop_args())
+                       stop=self._stop_args(), tp=self.model.tp)
             logits = logits[:, :len(chunk)]
             self.stats["mixed_steps"] += 1
             self.stats["mixed_decode_rows"] += len(dec)
@@ -481,7 +486,8 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
             if self._trace_steps:
                 self.recovery_trace.append((time.monotonic(), "prefill: staged"))
             ctr = self._dev([len(r.prompt_ids) for r in rs])
-            toks = ops.sample(sub, temp, top_p, seeds, ctr, shards=sub.shape[0], nucleus=self._wants_nucleus(rs))
+            toks = ops.sample(sub, temp, top_p, seeds, ctr, shards=sub.shape[0], nucleus=self._wants_nucleus(rs),
+                              tp=self.model.tp)
             if self._trace_steps:
                 self.recovery_trace.append((time.monotonic(), "prefill: sample enqueued"))
             slots_t = self._dev([r.slot for r in rs], torch.long)
@@ -639,12 +645,10 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
             ev_t[1].record()
         tp = self.model.tp
         tp.snapshot_health()             # rides on the bounded wait below
-        self.model.snapshot_decode_health()
         if tr is not None:
             tr.append((time.monotonic(), "decode: fetch"))
         hist, nsteps = self._fetch(self.s_hist[:B], self.s_steps[:B], what="decode")
         tp.check_health()                # a failed collective raises into the decision service
-        self.model.check_decode_health()
         self.stats["decode_time"] += (ev_t[0].elapsed_time(ev_t[1]) / 1e3) if ev_t is not None \
             else time.perf_counter() - t0
         finished = []

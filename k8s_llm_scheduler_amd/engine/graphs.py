@@ -15,6 +15,14 @@ from ..utils.tracing import trace
 from .common import BUCKETS, PREFILL_GRAPH_BUCKETS, _P_SPLIT, SPEC_GRAPH_T
 
 
+def logits_exchange_bytes(model, rows: int) -> int:
+    """Per-rank bytes of the largest collective the sampling of ``rows`` logits rows issues: the gathered fp32 logits,
+    or (vocab-parallel sampling) a top-p row's 256-bin u64 histogram."""
+    if getattr(model, "gather_logits", True):
+        return rows * model.lm_head.shape[0] * 4
+    return rows * 256 * 8
+
+
 class GraphCaptureMixin:
     """Decode / prefill / verify graph capture and the static state the graphs read."""
 
@@ -23,7 +31,8 @@ class GraphCaptureMixin:
                                            max_context or self.max_model_len)
         ops.sample(logits, self.s_temp[:B], self.s_top_p[:B], self.s_seeds[:B], self.s_ctx[:B],
                    shards=logits.shape[0], tokens_out=self.s_tokens[:B], ctx_inc=self.s_ctx[:B],
-                   hist=self.s_hist[:B], steps=self.s_steps[:B], nucleus=nucleus, stop=self._stop_args())
+                   hist=self.s_hist[:B], steps=self.s_steps[:B], nucleus=nucleus, stop=self._stop_args(),
+                   tp=self.model.tp)
 
     @staticmethod
     def _wants_nucleus(reqs) -> bool:
@@ -72,6 +81,8 @@ class GraphCaptureMixin:
         buckets = buckets or sorted({b for b in BUCKETS if b <= self.max_batch} | {self.max_batch})
         stream = torch.cuda.Stream(self.device)
         for B in sorted(set(buckets)):
+            if not self._decode_bucket_capturable(B):
+                continue    # decodes eagerly (its collectives do not all fit the graph-capturable transport)
             for mc in self._ctx_classes():
                 for nuc in ((False, True) if nucleus else (False,)):
                     if (B, mc, nuc) in self.graphs:
@@ -135,6 +146,19 @@ class GraphCaptureMixin:
         env = os.environ.get("K8S_PREFILL_GRAPHS", "")
         return env != "0" and self.use_graphs and PREFILL_GRAPH_BUCKETS[-1] <= self.max_prefill_tokens
 
+    def _decode_bucket_capturable(self, B: int) -> bool:
+        """TP > 1: every collective of a B-row decode step (the two residual all-reduces per layer, B x hidden bf16,
+        and the sampling exchange) fits the xGMI transports -- a gloo collective cannot be captured and RCCL stays out
+        of the graphs (the prefill buckets' rule, ``_prefill_bucket_capturable``).  A bucket that does not fit decodes
+        eagerly instead of capturing an RCCL / gloo call into its graph."""
+        tp = self.model.tp
+        if tp.world <= 1 or tp.simulate or os.environ.get("K8S_PREFILL_GRAPHS", "") == "1":
+            return True
+        if tp.xgmi is None:
+            return False
+        ar = B * self.model.cfg.hidden * 2
+        return ar <= tp.xgmi.max_allreduce_bytes and logits_exchange_bytes(self.model, B) <= tp.xgmi.slot_bytes
+
     def _prefill_bucket_capturable(self, Tb: int, logits_rows: int = 1) -> bool:
         """TP > 1: a chunk of Tb tokens all-reduces Tb x hidden bf16 twice per layer and all-gathers
         ``logits_rows`` rows of fp32 logits (one for a prefill chunk, every row for the speculative verify
@@ -150,9 +174,8 @@ class GraphCaptureMixin:
         if sp is not None and sp(Tb) and tp.rccl is not None:
             return False                   # the reduce-scatters run on RCCL: eager, like every RCCL chunk
         ar_bytes = Tb * self.model.cfg.hidden * 2
-        gather_bytes = logits_rows * self.model.lm_head.shape[0] * 4
         # captured with tp.capture_on_xgmi: every all-reduce that fits the capacity stays on xGMI
-        return ar_bytes <= tp.xgmi.max_allreduce_bytes and gather_bytes <= tp.xgmi.slot_bytes
+        return ar_bytes <= tp.xgmi.max_allreduce_bytes and logits_exchange_bytes(self.model, logits_rows) <= tp.xgmi.slot_bytes
 
     def _p_views(self, Tb: int):
         Tm = PREFILL_GRAPH_BUCKETS[-1]

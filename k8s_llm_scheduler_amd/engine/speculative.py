@@ -94,7 +94,8 @@ class SpeculativeMixin:
                                                     self._dev(bt), max(len(x[1]) for x in rows),
                                                     t(list(range(len(ids)))))
             toks = ops.sample(logits, t(temp, torch.float32), t(top_p, torch.float32), t(seeds), t(ctr),
-                              shards=logits.shape[0], nucleus=self._wants_nucleus(r for r, _, _ in rows))
+                              shards=logits.shape[0], nucleus=self._wants_nucleus(r for r, _, _ in rows),
+                              tp=self.model.tp)
             self.model.tp.snapshot_health()
             drawn = self._fetch(toks, what="speculative verify")[0].tolist()
             self.model.tp.check_health()

@@ -137,7 +137,23 @@ class RestKubeAPI:
                 if not line:
                     continue
                 ev = json.loads(line)
-                yield ev.get("type", ""), ev.get("object", {})
+                typ, obj = ev.get("type", ""), ev.get("object") or {}
+                if typ == "ERROR":
+                    # a Status object, not a pod.  410 Gone (the resourceVersion was compacted away): end the stream
+                    # at once -- the watch loop re-LISTs and watches from the new resourceVersion; any other error
+                    # goes through the loop's error back-off
+                    code = int(obj.get("code") or 0)
+                    if code == 410:
+                        return
+                    raise ApiError(code or 500, obj.get("reason", "") or "watch error", json.dumps(obj))
+                rv = (obj.get("metadata") or {}).get("resourceVersion")
+                if rv:
+                    self.last_resource_version = rv
+                if typ == "BOOKMARK":
+                    continue        # only advances the resourceVersion (allowWatchBookmarks): no pod in it
+                yield typ, obj
+
+    last_resource_version: str = ""   # of the last watch event or bookmark seen
 
     def create_binding(self, namespace: str, body: Obj) -> Obj:
         name = body["metadata"]["name"]

@@ -3,7 +3,7 @@
 from __future__ import annotations
 
 import json
-from dataclasses import asdict, dataclass, field
+from dataclasses import asdict, dataclass, field, replace
 from pathlib import Path
 from typing import Optional
 
@@ -68,6 +68,15 @@ PRESETS["llama-3.1-8b"] = LlamaConfig("llama-3.1-8b", 32, 4096, 32, 8, 128, 1433
 
 
 def get_config(name_or_path: str) -> LlamaConfig:
+    """A preset name, a HuggingFace config.json (or its directory), or ``<preset>@L<n>``: the preset's dimensions with
+    ``n`` decoder layers (e.g. ``llama-3.3-70b@L2``: the 70B's exact per-layer and vocabulary shapes -- every kernel,
+    shard and collective size of the headline -- at a depth that runs many times per test)."""
+    if "@L" in name_or_path:
+        base, n = name_or_path.rsplit("@L", 1)
+        c = get_config(base)
+        if not n.isdigit() or int(n) < 1:
+            raise KeyError(f"bad layer count in {name_or_path!r}")
+        return replace(c, name=f"{c.name}@L{n}", num_layers=int(n), extra=dict(c.extra))
     if name_or_path in PRESETS:
         return PRESETS[name_or_path]
     p = Path(name_or_path)

@@ -367,9 +367,19 @@ class LlamaModel:
             r = self.tp.reduce_scatter_rows(ops.linear(g, w.wdown), residual=r)   # r + MLP branch
         return self.tp.all_gather_rows(r)[:T]
 
+    # True: forward_* return the logits all-gathered over the TP ranks ([tp, S, Vs], shard-major).  False (the
+    # engine at TP > 1): this rank's vocab shard only ([1, S, Vs]), sampled vocab-parallel (ops.sample(tp=...)): a
+    # decode step then moves a few bytes per row between the ranks instead of rows x vocab x 4 B.
+    gather_logits = True
+
+    def _gather(self, logits: torch.Tensor) -> torch.Tensor:
+        if self.gather_logits or self.tp.world == 1:
+            return self.tp.all_gather_shards(logits)                           # [tp, S, Vs]
+        return logits.unsqueeze(0)                                             # [1, S, Vs]: this rank's shard
+
     def _logits_folded(self, r: torch.Tensor) -> torch.Tensor:
         logits = ops.linear_rms(r, self.lm_head, self.cfg.rms_eps, ops.EPI_F32)   # final norm folded: [S, Vs]
-        return self.tp.all_gather_shards(logits)                               # [tp, S, Vs]
+        return self._gather(logits)
 
     def _layers(self, h: torch.Tensor, attn) -> tuple:
         """Run all decoder layers.  ``attn(l, qkv) -> [T, nq*D]`` does rope + KV write + attention."""
@@ -392,7 +402,7 @@ class LlamaModel:
     def _logits(self, h: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
         x = ops.rmsnorm(h, self.norm, self.cfg.rms_eps, residual=res)
         logits = ops.linear(x, self.lm_head, out_dtype=torch.float32)   # [S, Vs]
-        return self.tp.all_gather_shards(logits)                         # [tp, S, Vs]
+        return self._gather(logits)
 
     def forward_prefill(self, ids: torch.Tensor, positions: torch.Tensor, slot_mapping: torch.Tensor,
                         cu_q: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
@@ -445,8 +455,6 @@ class LlamaModel:
         B = tokens.shape[0]
         self.tp.phase = "decode"
         if self.device.type == "cuda" and B <= ops.GEMV_MAX_M and self.fused_decode:
-            if self.persist_decode_ok(B, max_context):
-                return self._forward_decode_persist(tokens, context_lens, block_tables, max_context)
             return self._forward_decode_fused(tokens, context_lens, block_tables, max_context)
         kv = self.kv_cache
         fused_attn = self.device.type == "cuda" and self.fused_decode   # batched decode (B > 8)
@@ -472,47 +480,6 @@ class LlamaModel:
 
 
     fused_decode = True
-
-    # ------------------------------------------------------------------ layer-persistent decode (ops/persist.py)
-    _persist = None
-    persist_decode = None        # None: follow K8S_DECODE_PERSIST; True / False: force (tests, A/B)
-
-    def persist_decode_ok(self, B: int, max_context: int) -> bool:
-        """Every decoder layer of the step in ONE launch (decode_persist.hip): TP = 1 or one simulated TP rank, bf16
-        weights, gammas folded, <= 2 sequences, contexts <= 4096, shapes the kernel plans."""
-        from ..ops import persist
-
-        on = persist.enabled() if self.persist_decode is None else self.persist_decode
-        if not on or self.device.type != "cuda" or not self.norm_folded or self.weight_dtype != "bf16":
-            return False
-        if not (self.tp.world == 1 or self.tp.simulate):
-            return False
-        if self._persist is None:
-            self._persist = persist.PersistentDecode(self)
-        return self._persist.supports(B, max_context)
-
-    def _forward_decode_persist(self, tokens: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
-                                max_context: int) -> torch.Tensor:
-        h = ops.embedding(tokens, self.embed)
-        x = self._persist.run(h, context_lens, block_tables, max_context)
-        logits = ops.linear_norm(x, self.lm_head, None, self.cfg.rms_eps, None, None, epi=ops.EPI_F32)
-        return self.tp.all_gather_shards(logits)
-
-    def snapshot_decode_health(self) -> None:
-        """Enqueue a copy of the persistent decode kernel's error word (read by check_decode_health after the
-        caller's own stream synchronisation)."""
-        if self._persist is not None:
-            self._persist.snapshot_error()
-
-    def check_decode_health(self) -> None:
-        """Raise CollectiveError if an in-kernel wait of the persistent decode timed out (its outputs are not
-        trustworthy); the kernel state is reset for the next step."""
-        if self._persist is not None:
-            e = self._persist.take_error()
-            if e:
-                from ..parallel.comm import CollectiveError
-
-                raise CollectiveError(f"persistent decode kernel: in-kernel wait timed out (error bits {e:#x})")
 
     # ------------------------------------------------------------------ decode weight prefetch (opt-in experiment)
     # K8S_DECODE_PREFETCH_MB = M > 0: after each layer's QKV GEMV a side stream reads the first M MB of that layer's
@@ -573,7 +540,7 @@ class LlamaModel:
             self._pf_join()
         logits = ops.linear_norm(h, self.lm_head, None if self.norm_folded else self.norm, c.rms_eps, res_in, None,
                                  epi=ops.EPI_F32)
-        return self.tp.all_gather_shards(logits)
+        return self._gather(logits)
 
     def _forward_decode_fused_tp(self, h: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
                                  max_context: int) -> torch.Tensor:
@@ -590,23 +557,16 @@ class LlamaModel:
             qkv = ops.linear_norm(x, w.wqkv, g1(w) if g1 else None, c.rms_eps, None, None)
             if pf:
                 self._pf_layer(w, pf)
-            if ops.attn_oproj_fusable(B, w.wo, max_context, self.nq, self.nkv, self.D):
-                # attention + O projection: one launch (the W_o stream overlaps attention; opt-in)
-                o = ops.decode_attention_oproj(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
-                                               self.scale, self.block_size, max_context, self.nq, self.nkv, self.D,
-                                               w.wo)
-                self.tp.all_reduce_(o, residual=x)             # o = x + attention branch
-            else:
-                a = ops.decode_attention_fused(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
-                                               self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
-                o = self.tp.linear_all_reduce(a, w.wo, residual=x)   # o = x + attention branch (AR in the GEMV)
+            a = ops.decode_attention_fused(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
+                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
+            o = self.tp.linear_all_reduce(a, w.wo, residual=x)   # o = x + attention branch (AR in the GEMV)
             g = ops.linear_norm(o, w.wgu, g2(w) if g2 else None, c.rms_eps, None, None, epi=ops.EPI_SWIGLU)
             x = self.tp.linear_all_reduce(g, w.wdown, residual=o)    # x = o + MLP branch
         if pf:
             self._pf_join()
         logits = ops.linear_norm(x, self.lm_head, None if self.norm_folded else self.norm, c.rms_eps, None, None,
                                  epi=ops.EPI_F32)
-        return self.tp.all_gather_shards(logits)
+        return self._gather(logits)
 
 
 

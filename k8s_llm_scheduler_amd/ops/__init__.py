@@ -263,8 +263,6 @@ def _ref_act_quant(x: torch.Tensor, w) -> torch.Tensor:
     x2 = x.reshape(-1, x.shape[-1])
     if x2.shape[0] <= max(GEMV_MAX_M, SGEMV_MAX_M):   # GEMV / sgemv: bf16 activations against the fp8 weights
         return x
-    if w8_rows(x2.shape[0]):   # mgemm's W8 mode: bf16 activations against the fp8 weights
-        return x
     q, s = ref.quantize_fp8(x2)
     return ref.dequant_fp8(q, s, torch.float32).to(x.dtype).view(x.shape)
 
@@ -526,11 +524,10 @@ def mgemm_nwg(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int) 
 
 
 def mgemm_valid(cfg: int, M: int, N: int, K: int, epi: int, fp8: bool, grid: int = 1, mx_out: bool = False) -> bool:
-    """``fp8``: 0 / False bf16, 1 / True fp8 activations and weights, 2 W8 (fp8 weights, bf16 activations), 3 MX
-    activations (fp8 weights).  ``mx_out``: the SwiGLU epilogue writes MX e4m3 (fp8 / MX modes)."""
+    """``fp8``: 0 / False bf16, 1 / True fp8 activations and weights, 3 MX activations (fp8 weights).  ``mx_out``: the SwiGLU epilogue writes MX e4m3 (fp8 / MX modes)."""
     if cfg < 0 or cfg >= len(mgemm_configs()):
         return False
-    if int(fp8) in (2, 3) and _mg_mode_lds(cfg, int(fp8)) < 0:
+    if int(fp8) == 3 and _mg_mode_lds(cfg, 3) < 0:
         return False
     if mx_out and (int(fp8) not in (1, 3) or N % 128 or
                    (_mg_mode_lds(cfg, 4) < 0 if epi == EPI_SWIGLU else (epi != EPI_BF16 or _mg_mode_lds(cfg, 5) < 0))):
@@ -550,42 +547,9 @@ def _mgemm_ok(N: int, K: int, fp8: bool) -> bool:
 
 @functools.lru_cache(maxsize=256)
 def _mg_mode_lds(cfg: int, mode: int) -> int:
-    """LDS bytes of a configuration in a mode (2 W8, 3 MX activations; 4: 0 if its SwiGLU epilogue writes MX
-    output), -1 where the configuration is not built for it."""
+    """LDS bytes of a configuration in a mode (3 MX activations; 4: 0 if its SwiGLU epilogue writes MX output), -1
+    where the configuration is not built for it."""
     return native().mgemm_lds_bytes(cfg, mode)
-
-
-def _mg_w8_lds(cfg: int) -> int:
-    return _mg_mode_lds(cfg, 2)
-
-
-# W8: fp8 weights against bf16 activations in mgemm (17..W8_MAX_M rows: batched decode and short mixed steps): the
-# weight bytes streamed are the fp8 ones, the bf16 MFMA runs at the non-scaled fp8 MFMA's rate, and no activation is
-# quantized (no quantize_act_fp8 launch before the QKV / gate-up -- their RMS statistics are mgemm's prologue -- or the
-# O / down projections).  Measured SLOWER than per-token e4m3 activations (profiles/mgemm_w8_tune_r5.txt: 0.54-1.13x
-# per shape, 16 of 24 below; fp8 batch 64: 31.5 -> 23.7 decisions/s): mgemm re-stages x with W in every k-step, and
-# bf16 x doubles those bytes, more than the quantize launches cost.  Opt-in (K8S_MGEMM_W8=1) for A/B only.
-W8_ON = os.environ.get("K8S_MGEMM_W8", "0") == "1"
-W8_MAX_M = int(os.environ.get("K8S_MGEMM_W8_MAX_M", "128"))
-
-
-def w8_rows(M: int) -> bool:
-    """An fp8-weight GEMM of M rows runs mgemm's W8 mode (bf16 activations) on the GPU."""
-    return W8_ON and max(GEMV_MAX_M, SGEMV_MAX_M) < M <= W8_MAX_M and GEMM_BACKEND in ("auto", "mgemm")
-
-
-def mgemm_w8_plan(M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]:
-    """(cfg, grid) of the W8 mode for this shape, or None (no W8 configuration runs it)."""
-    if N % 4 or K % 128:
-        return None
-    pick = _mg_table_row(M, N, K, epi, 2)
-    if pick is not None and mgemm_valid(pick[1], M, N, K, epi, 2, pick[2]):
-        return pick[1], pick[2]
-    pick = _mg_table_row(M, N, K, epi, 1)   # the fp8 plan's tile, where W8 builds it
-    if pick is not None and mgemm_valid(pick[1], M, N, K, epi, 2, pick[2]):
-        return pick[1], pick[2]
-    cfg, grid = mgemm_heuristic(M, N, K, epi, 2)
-    return (cfg, grid) if mgemm_valid(cfg, M, N, K, epi, 2, grid) else None
 
 
 def mgemm_mx_plan(M: int, N: int, K: int, epi: int, act_mx: bool, mx_out: bool) -> Optional[Tuple[int, int]]:
@@ -632,11 +596,6 @@ def mgemm_heuristic(M: int, N: int, K: int, epi: int, fp8: bool, num_cus: int = 
         cfg = 19
     if not mgemm_valid(cfg, M, N, K, epi, fp8):   # K not a multiple of the config's k-step: 128-byte k-steps
         cfg = 5 if M <= 16 else 9 if M <= 32 else 13 if M <= 64 else 15 if M <= 128 else 17
-    if int(fp8) == 2 and not mgemm_valid(cfg, M, N, K, epi, fp8):   # W8: the weight-streaming tiles whose x fits
-        for c in ((29, 28, 8, 7, 6) if M <= 64 else (30, 29, 28, 8)):
-            if mgemm_valid(c, M, N, K, epi, fp8):
-                cfg = c
-                break
     tiles = _mg_tiles(cfg, M, N, epi)
     if tiles >= num_cus // 2:
         return cfg, 1
@@ -704,34 +663,34 @@ def mgemm_plan(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[int, int]:
     return mgemm_heuristic(M, N, K, epi, fp8)
 
 
+# split-K publish of mgemm (mgemm.hip): fence-free write-through slab stores + relaxed ticket (default) or the
+# round-4 agent-scope release / acquire fences (K8S_MGEMM_FENCED=1); the same summation order, the same bits
+MGEMM_FENCED = os.environ.get("K8S_MGEMM_FENCED", "0") == "1"
+
+
 def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
           grid: Optional[int] = None, res: Optional[torch.Tensor] = None, rms_eps: Optional[float] = None,
-          out: Optional[torch.Tensor] = None, act=None, w8: bool = False, mx_out: bool = False):
+          out: Optional[torch.Tensor] = None, act=None, mx_out: bool = False, fenced: Optional[bool] = None):
     """Hand-written MFMA GEMM (mgemm.hip): epi(x[M, K] @ w[N, K].T), any M (routed for M > GEMV_MAX_M).  ``w``: bf16 or
-    Fp8Weight (activations are then quantized per token by quantize_act_fp8, or with ``w8`` stay bf16: W8 mode).
+    Fp8Weight (activations are then quantized per token by quantize_act_fp8, or arrive as MX e4m3 in ``act``).
     SwiGLU: w = [Wg; Wu].  ``rms_eps``: RMSNorm prologue -- the result is scaled by 1/rms(x row) (the norm gamma must
-    be folded into ``w``), so the un-normalised residual stream feeds the GEMM directly (bf16 or W8).  ``res``:
+    be folded into ``w``), so the un-normalised residual stream feeds the GEMM directly (bf16 or MX).  ``res``:
     residual epilogue (bf16 output only) -- out = x @ w.T + res, one rounding; ``out`` may be ``res`` (in place).
     ``act``: an :class:`MxAct` (mode 3, the block-scaled MFMA) or the (e4m3, per-token scale) pair of quantize_act_fp8.
-    ``mx_out`` (fp8 weights, SwiGLU): returns the output as an :class:`MxAct` written by the epilogue."""
+    ``mx_out`` (fp8 weights, SwiGLU): returns the output as an :class:`MxAct` written by the epilogue.
+    ``fenced``: split-K tiles publish their slabs with agent-scope release / acquire fences (the round-4 form) instead
+    of the default fence-free write-through stores + relaxed ticket (None: ``K8S_MGEMM_FENCED``); same bits."""
     if isinstance(x, MxAct):
         act = x
     M, K = x.shape
     fp8 = _is_fp8(w)
     act_mx = isinstance(act, MxAct)
-    mode = (2 if w8 else 3 if act_mx else 1) if fp8 else 0
-    if w8 and (not fp8 or act is not None):
-        raise ValueError("mgemm: W8 mode takes fp8 weights and bf16 activations")
+    mode = (3 if act_mx else 1) if fp8 else 0
     if (act_mx or mx_out) and not fp8:
         raise ValueError("mgemm: MX activations / output need fp8 weights")
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     if cfg is None:
-        if mode == 2:
-            plan = mgemm_w8_plan(M, N, K, epi)
-            if plan is None:
-                raise ValueError(f"mgemm: no W8 configuration runs M={M} N={N} K={K} epi={epi}")
-            cfg, grid = plan
-        elif act_mx or mx_out:
+        if act_mx or mx_out:
             plan = mgemm_mx_plan(M, N, K, epi, act_mx, mx_out)
             if plan is None:
                 raise ValueError(f"mgemm: no MX configuration runs M={M} N={N} K={K} epi={epi}")
@@ -760,23 +719,22 @@ def mgemm(x: torch.Tensor, w, epi: int = EPI_BF16, cfg: Optional[int] = None,
     ws = torch.empty(n_ws, dtype=F32, device=x.device) if n_ws > 0 else None
     tk = _zeroed_scratch(x.device, "mgemm", 4 * tiles, 64 * 1024) if cmax > 1 else 0
     rp = _chk(res, BF16, "res") if res is not None else 0
+    fn = int(MGEMM_FENCED if fenced is None else bool(fenced))
     rms, eps = (1, float(rms_eps)) if rms_eps is not None else (0, 0.0)
     oq, oe = (mxo.q.data_ptr(), mxo.e.data_ptr()) if mxo is not None else (0, 0)
     if act_mx:
         if act.shape != (M, K) or not act.q.is_cuda:
             raise ValueError(f"mgemm: MX activations {tuple(act.shape)} for x {(M, K)}")
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, act.q.data_ptr(), w.q.data_ptr(),
-                       act.e.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 3, cfg, nwg, cmax, rp, rms, eps, -1, oq, oe)
-    elif mode == 2:
-        native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"), w.q.data_ptr(),
-                       0, w.scale.data_ptr(), M, N, K, epi, 2, cfg, nwg, cmax, rp, rms, eps, -1)
+                       act.e.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 3, cfg, nwg, cmax, rp, rms, eps, -1, oq, oe,
+                       fn)
     elif fp8:
         xq, sx = act if act is not None else quantize_act_fp8(x.contiguous())
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, xq.data_ptr(), w.q.data_ptr(),
-                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, nwg, cmax, rp, 0, 0.0, -1, oq, oe)
+                       sx.data_ptr(), w.scale.data_ptr(), M, N, K, epi, 1, cfg, nwg, cmax, rp, 0, 0.0, -1, oq, oe, fn)
     else:
         native().mgemm(out.data_ptr(), ws.data_ptr() if ws is not None else 0, tk, _chk(x, BF16, "x"),
-                       _chk(w, BF16, "w"), 0, 0, M, N, K, epi, 0, cfg, nwg, cmax, rp, rms, eps, -1)
+                       _chk(w, BF16, "w"), 0, 0, M, N, K, epi, 0, cfg, nwg, cmax, rp, rms, eps, -1, 0, 0, fn)
     del ws
     if mxo is not None:
         return (out, mxo) if res is not None else mxo
@@ -974,39 +932,10 @@ def gemm_route(M: int, N: int, K: int, epi: int, fp8: bool) -> Tuple[str, Option
     return plan[0], plan[1:]
 
 
-# bf16 GEMMs of (SGEMV_MAX_M, XGEMM_MAX_M] rows (batched decode) run the activation-resident xgemm.hip (x held in
-# registers per K slab, the weights alone through a deep LDS ring) where it plans the shape (K8S_XGEMM=0: mgemm).
-XGEMM_MAX_M = 64
-XGEMM_ON = os.environ.get("K8S_XGEMM", "0") == "1"   # opt-in until it beats mgemm (docs/PERF.md)
-
-
-def xgemm(x: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, res: Optional[torch.Tensor] = None,
-          rms_eps: Optional[float] = None, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-    """epi(x[M, K] @ w.T) for 1..64 rows with bf16 weights on xgemm.hip (``rms_eps``: scaled by 1/rms of each x row,
-    the norm gamma folded into ``w``; ``res``: + res, bf16 epilogue, ``out`` may be ``res``).  None where the kernel
-    does not plan the shape."""
-    M, K = x.shape
-    N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
-    rms = 1 if rms_eps is not None else 0
-    rc, ns, g, wf, rf = native().xgemm_plan(M, N, K, epi, rms)
-    if rc != 0:
-        return None
-    if out is None:
-        out = torch.empty(M, N, dtype=F32 if epi == EPI_F32 else BF16, device=x.device)
-    ws = torch.empty(wf, dtype=F32, device=x.device)
-    rs = torch.empty(rf, dtype=F32, device=x.device) if rf > 0 else None
-    native().xgemm(out.data_ptr(), ws.data_ptr(), rs.data_ptr() if rs is not None else 0, _chk(x, BF16, "x"),
-                   _chk(w, BF16, "w"), _chk(res, BF16, "res") if res is not None else 0, M, N, K, epi, rms,
-                   float(rms_eps or 0.0), -1)
-    del ws, rs
-    return out
-
-
 def mx_rows(M: int, w) -> bool:
     """An fp8 GEMM of M rows against ``w`` (the consumer: O or down) takes its input as MX e4m3 (:class:`MxAct`):
-    above the GEMV / sgemv rows (bf16 activations there), outside W8 mode, K % 128 == 0, on mgemm (or pgemm with
-    K8S_MX_PGEMM=1)."""
-    if not (MX_ON and _is_fp8(w) and M > max(GEMV_MAX_M, SGEMV_MAX_M) and not w8_rows(M)
+    above the GEMV / sgemv rows (bf16 activations there), K % 128 == 0, on mgemm (or pgemm with K8S_MX_PGEMM=1)."""
+    if not (MX_ON and _is_fp8(w) and M > max(GEMV_MAX_M, SGEMV_MAX_M)
             and GEMM_BACKEND != "library" and w.shape[1] % 128 == 0):
         return False
     return MX_PGEMM or gemm_route(M, w.shape[0], w.shape[1], EPI_BF16, True)[0] == "mgemm"
@@ -1059,14 +988,6 @@ def _gemm(x2: torch.Tensor, w, epi: int, res: Optional[torch.Tensor] = None, rms
             return y
     N = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
     kern, plan = gemm_route(M, N, K, epi, fp8)
-    if (XGEMM_ON and not fp8 and act is None and M <= XGEMM_MAX_M and kern != "library"
-            and GEMM_BACKEND not in ("mgemm", "pgemm")):
-        y = xgemm(x2, w, epi, res=res, rms_eps=rms_eps, out=out)
-        if y is not None:
-            return y
-    if (kern == "mgemm" and fp8 and act is None and w8_rows(M)
-            and mgemm_w8_plan(M, N, K, epi) is not None):   # fp8 weights, bf16 activations: no quantize launch
-        return mgemm(x2, w, epi, res=res, rms_eps=rms_eps, out=out, w8=True)
     if kern == "library" or (fp8 and rms_eps is not None):
         return None   # (fp8: the activations are quantized after the norm, so the caller normalises first)
     if kern == "mgemm":
@@ -1112,17 +1033,6 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16, mx_consumer=
         if gemm_route(M, n_out, K, epi, True)[0] == "mgemm" and \
                 mgemm_mx_plan(M, n_out, K, epi, True, mx_out) is not None:
             return mgemm(x_mx, w, epi, rms_eps=eps, mx_out=mx_out)
-    if _is_fp8(w) and w8_rows(M):
-        # W8 rows: mgemm's RMS prologue on the un-normalised bf16 rows against the fp8 weights (no quantize launch)
-        if _gpu(r):
-            n_out = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
-            if gemm_route(M, n_out, K, epi, True)[0] == "mgemm" and mgemm_w8_plan(M, n_out, K, epi) is not None:
-                return mgemm(r.contiguous(), w, epi, rms_eps=eps, w8=True)
-        else:
-            x = rmsnorm(r, _ones(K, r.device), eps)
-            if epi == EPI_SWIGLU:
-                return ref.linear_swiglu(x, w).to(BF16)
-            return ref.linear(x, w, F32 if epi == EPI_F32 else BF16)
     if _is_fp8(w) and M > max(GEMV_MAX_M, SGEMV_MAX_M):
         # fp8 GEMM rows: e4m3 of the UN-normalised rows with 1/rms folded into the per-token scales (one kernel
         # reads r once; no rmsnorm kernel, no normalised copy) -> the fp8 GEMM
@@ -1140,11 +1050,8 @@ def linear_rms(r: torch.Tensor, w, eps: float, epi: int = EPI_BF16, mx_consumer=
             return quantize_act_mx(y) if mx_out else y
         return ref.linear(xa, w, F32 if epi == EPI_F32 else BF16)
     n_out = w.shape[0] // 2 if epi == EPI_SWIGLU else w.shape[0]
-    xg = (XGEMM_ON and not _is_fp8(w) and M <= XGEMM_MAX_M and GEMM_BACKEND == "auto"
-          and native().xgemm_plan(M, n_out, K, epi, 1)[0] == 0) if _gpu(r) else False
     if _gpu(r) and M > GEMV_MAX_M and (M <= SGEMV_MAX_M or M > RMS_PROLOGUE_MAX_UNFUSED or _is_fp8(w)
-                                       or n_out < RMS_UNFUSED_MIN_N or xg
-                                       or (epi == EPI_SWIGLU and RMS_PROLOGUE_SWIGLU)):
+                                       or n_out < RMS_UNFUSED_MIN_N or (epi == EPI_SWIGLU and RMS_PROLOGUE_SWIGLU)):
         y = _gemm(r.contiguous(), w, epi, rms_eps=eps)
         if y is not None:
             return y
@@ -1349,59 +1256,6 @@ def _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, contex
     return out
 
 
-# split attention + O projection in one launch (decode_split_oproj_kernel), opt-in with K8S_FUSE_ATTN_O=1:
-# correct (tests/test_kernels_gpu.py, test_model_gpu.py) but measured slower than the two launches it replaces
-# (profiles/kbench_attn_oproj_fusion.txt: 13.3-14.3 vs 12.0 us at TP=8, ctx 564; decode 4.49 vs 4.30 ms/token)
-FUSE_ATTN_O = os.environ.get("K8S_FUSE_ATTN_O", "0") == "1"
-ATTN_O_DELAY = int(os.environ.get("K8S_ATTN_O_DELAY", "0"))        # ~1.7 us units before the W_o loads
-ATTN_O_POLL = int(os.environ.get("K8S_ATTN_O_POLL", "1"))          # ~0.1 us units between polls
-
-
-def attn_oproj_fusable(B: int, wo, max_context: int, nq: int, nkv: int, D: int) -> bool:
-    """The fused kernel covers TP >= 4 decode shards of Llama-3.3-70B (o_proj K = nq * D of 1024 / 2048,
-    bf16 W_o) at <= 2 sequences on the split-attention path."""
-    return (FUSE_ATTN_O and not _is_fp8(wo) and wo.is_cuda and B <= 2 and D == 128 and nq * D in (1024, 2048)
-            and wo.shape[1] == nq * D and B * nkv <= _split_pairs_limit(max_context)
-            and max_context <= 64 * SPLIT_PARTITION)
-
-
-def decode_attention_oproj(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
-                           block_tables: torch.Tensor, context_lens: torch.Tensor, scale: float, block_size: int,
-                           max_context: int, nq: int, nkv: int, D: int, wo: torch.Tensor) -> torch.Tensor:
-    """linear(decode_attention_fused(...), wo) as one launch: the O-projection workgroups hold their W_o rows
-    in registers while the attention chunks run and start the moment the last (sequence, kv head) output is
-    published.  Returns o [B, N] bf16.  CPU / unsupported shapes: the two separate ops."""
-    B = qkv.shape[0]
-    if not (_gpu(qkv, k_cache) and block_size == 16 and attn_oproj_fusable(B, wo, max_context, nq, nkv, D)):
-        a = decode_attention_fused(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
-                                   max_context, nq, nkv, D)
-        return linear(a, wo)
-    N = wo.shape[0]
-    pmax = max(1, math.ceil(max_context / SPLIT_PARTITION))
-    attn = torch.empty(B, nq * D, dtype=BF16, device=qkv.device)
-    o = torch.empty(B, N, dtype=BF16, device=qkv.device)
-    part = None
-    if pmax > 1:
-        part = torch.empty(native().decode_split_workspace(B, nq, nkv, pmax), dtype=F32, device=qkv.device)
-    counters = _zeroed_scratch(qkv.device, "attn_split", B * nkv * 4)
-    sync = _zeroed_scratch(qkv.device, "attn_oproj_sync", 1280)
-    native().decode_attention_split_oproj(attn.data_ptr(), part.data_ptr() if part is not None else 0, counters,
-                                          _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"),
-                                          _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
-                                          _chk(block_tables, I32, "block_tables"),
-                                          _chk(context_lens, I32, "context_lens"), float(scale), B, nq, nkv, D,
-                                          block_size, block_tables.shape[1], pmax, _chk(wo, BF16, "wo"), o.data_ptr(),
-                                          N, sync, ATTN_O_DELAY, ATTN_O_POLL, -1)
-    del part
-    return o
-
-
-def attn_oproj_timeouts(dev) -> int:
-    """Non-zero if an O-projection workgroup of decode_attention_oproj ever gave up waiting (a bug signal)."""
-    buf = _SCRATCH.get(("attn_oproj_sync", dev.index if dev.index is not None else torch.cuda.current_device()))
-    return 0 if buf is None else int(buf[1152:1156].view(torch.int32).item())
-
-
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     """silu(x @ Wg.T) * (x @ Wu.T) with w_gate_up = [Wg; Wu] ([2I, K]); the SwiGLU is the GEMM's epilogue."""
     if not _gpu(x, w_gate_up):
@@ -1452,7 +1306,7 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
            counter: torch.Tensor, *, shards: int = 1, tokens_out: Optional[torch.Tensor] = None,
            ctx_inc: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None,
            steps: Optional[torch.Tensor] = None, nucleus: Optional[bool] = None,
-           slots: Optional[torch.Tensor] = None, stop: Optional[dict] = None) -> torch.Tensor:
+           slots: Optional[torch.Tensor] = None, stop: Optional[dict] = None, tp=None) -> torch.Tensor:
     """Sample one token per row.  logits: [B, V] or sharded [shards, B, Vs] fp32.  Optionally
     updates decode state in place: tokens_out[s] = tok, ctx_inc[s] += 1, hist[s, steps[s]] = tok,
     steps[s] += 1 (slots with ctx_inc[s] <= 0 are padding and untouched), where s = slots[b] (or b).
@@ -1464,14 +1318,24 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
     ``stop``: device-side stop detection of the decode graphs (sampler.hip StopArgs): dict with ``cls``
     [vocab, 2] int32 token classes, ``json`` / ``cfg`` [slots] int32, optional ``forced`` [slots, n] /
     ``forced_len`` [slots] scripted tokens, ``eos_tok`` and ``done`` (GPU: a host-mapped device pointer int;
-    CPU: an int32 tensor).  A finished answer sets ctx_inc[s] = 0 and done[s] = 1."""
+    CPU: an int32 tensor).  A finished answer sets ctx_inc[s] = 0 and done[s] = 1.
+
+    ``tp`` (a TPGroup of world > 1) with ``logits`` [1, B, Vs] = this rank's vocab shard (the model's
+    ``gather_logits = False``): vocab-parallel sampling -- every rank samples its own shard with noise keyed by the
+    GLOBAL token id and the ranks exchange 8 bytes per row (plus, for top-p rows, the row max and two 256-bin integer
+    histograms), instead of all-gathering B x V fp32 logits.  Same tokens as the gathered path, bit for bit."""
     if logits.dim() == 3:
         S, B, Vs = logits.shape
     else:
         (B, Vs), S = logits.shape, 1
+    vp = tp is not None and tp.world > 1 and S == 1 and logits.dim() == 3
     if not _gpu(logits):
-        full = logits.permute(1, 0, 2).reshape(B, S * Vs) if logits.dim() == 3 else logits
-        toks = ref.sample(full, temperature, top_p, seeds, counter)
+        if vp:
+            toks = ref.sample_vocab_parallel(logits[0], temperature, top_p, seeds, counter, tp.rank,
+                                             tp.all_gather_shards)
+        else:
+            full = logits.permute(1, 0, 2).reshape(B, S * Vs) if logits.dim() == 3 else logits
+            toks = ref.sample(full, temperature, top_p, seeds, counter)
         idx = [int(slots[b]) if slots is not None else b for b in range(B)]
         if stop is not None and hist is not None and ctx_inc is not None:
             for b, s in enumerate(idx):
@@ -1504,15 +1368,52 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
                    fz.shape[1] if fz is not None else 0, int(stop["eos_tok"]), int(stop["done"]))
     else:
         st_args = (0, 0, 0, 0, 0, 0, 0, 0)
-    native().sample(_chk(out, I32, "tokens"), _chk(logits, F32, "logits"), B, Vs, S,
-                    _chk(temperature, F32, "temperature"), _chk(top_p, F32, "top_p"),
-                    _chk(seeds, I32, "seeds"), _chk(counter, I32, "counter"),
-                    _chk(ctx_inc, I32, "ctx_inc") if ctx_inc is not None else 0,
-                    _chk(hist, I32, "hist") if hist is not None else 0,
-                    hist.shape[1] if hist is not None else 0,
-                    _chk(steps, I32, "steps") if steps is not None else 0, _sample_scratch(logits.device, B), nuc,
-                    _chk(slots, I32, "slots") if slots is not None else 0, *st_args, -1)
+    p_temp, p_top, p_ctx = _chk(temperature, F32, "temperature"), _chk(top_p, F32, "top_p"), \
+        (_chk(ctx_inc, I32, "ctx_inc") if ctx_inc is not None else 0)
+    p_slots = _chk(slots, I32, "slots") if slots is not None else 0
+    p_hist = _chk(hist, I32, "hist") if hist is not None else 0
+    p_steps = _chk(steps, I32, "steps") if steps is not None else 0
+    hstride = hist.shape[1] if hist is not None else 0
+    if not vp:
+        native().sample(_chk(out, I32, "tokens"), _chk(logits, F32, "logits"), B, Vs, S, p_temp, p_top,
+                        _chk(seeds, I32, "seeds"), _chk(counter, I32, "counter"), p_ctx, p_hist, hstride, p_steps,
+                        _sample_scratch(logits.device, B), nuc, p_slots, *st_args, -1)
+        return out
+    # vocab-parallel (sampler.hip k8s_sample_nuc_local / _combine / k8s_sample_merge): the ranks exchange row maxima,
+    # bin totals and best keys through tp.all_gather_shards (xGMI inside the decode graphs: a few KiB)
+    dev, lg = logits.device, _chk(logits, F32, "logits")
+    if nucleus:
+        ld = (B + 3) // 4 * 4
+        mine = _zeroed_tensor(dev, "sample_tp_max", 4096, torch.int32)[:ld]   # re-armed by the combine
+        native().sample_nuc_local(-1, lg, B, Vs, p_temp, p_top, p_ctx, p_slots, nuc, mine.data_ptr(), -1)
+        g = tp.all_gather_shards(mine)
+        native().sample_nuc_combine(-1, g.data_ptr(), ld, tp.world, B, p_temp, p_top, p_ctx, p_slots, nuc,
+                                    mine.data_ptr(), -1)
+        for level in (0, 1):
+            h = torch.empty(B, 256, dtype=torch.int64, device=dev)
+            native().sample_nuc_local(level, lg, B, Vs, p_temp, p_top, p_ctx, p_slots, nuc, h.data_ptr(), -1)
+            g = tp.all_gather_shards(h.view(torch.int32))
+            native().sample_nuc_combine(level, g.data_ptr(), B, tp.world, B, p_temp, p_top, p_ctx, p_slots, nuc, 0, -1)
+    ldk = (B + 1) // 2 * 2
+    keys = torch.empty(ldk, dtype=torch.int64, device=dev)   # every live row's key is written; the rest unread
+    native().sample(_chk(out, I32, "tokens"), lg, B, Vs, 1, p_temp, p_top, _chk(seeds, I32, "seeds"),
+                    _chk(counter, I32, "counter"), p_ctx, p_hist, hstride, p_steps, _sample_scratch(dev, B), nuc,
+                    p_slots, *st_args, -1, id_base=tp.rank * Vs, keys_out=keys.data_ptr(), nuc_passes=0)
+    g = tp.all_gather_shards(keys.view(torch.int32))
+    native().sample_merge(out.data_ptr(), g.data_ptr(), ldk, tp.world, B, p_ctx, p_hist, hstride, p_steps, p_slots,
+                          *st_args, -1)
     return out
+
+
+def _zeroed_tensor(dev: torch.device, kind: str, numel: int, dtype: torch.dtype) -> torch.Tensor:
+    """A persistent zero-initialised device tensor that its kernels leave zeroed again (see _zeroed_scratch)."""
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    t = _SCRATCH.get((kind, "tensor", i))
+    if t is None or t.numel() < numel:
+        t = torch.zeros(numel, dtype=dtype, device=dev)
+        _SCRATCH.setdefault(("keep", i), []).append(t)
+        _SCRATCH[(kind, "tensor", i)] = t
+    return t
 
 
 _STOP_CLS: dict = {}

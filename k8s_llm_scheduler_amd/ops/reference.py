@@ -260,32 +260,72 @@ def _ord_key(l: torch.Tensor) -> torch.Tensor:
 NUC_FS = float(np.float32(65536.0 / 28.0))   # sampler.hip NUC_FS
 
 
-def nucleus_mask(l: torch.Tensor, T: float, P: float) -> torch.Tensor:
-    """The nucleus of sampler.hip for one row of fp32 logits: fine bin f = floor((M - l) / T * 65536/28)
-    (none beyond 28), mass = floor(exp((l - M) / T) * 2^40) as an integer, target = floor(Z * P); the
-    smallest f* with mass{f <= f*} >= target is found coarse (f >> 8) then fine (f & 255); keep f <= f*."""
+def nucleus_fine_mass(l: torch.Tensor, M: float, T: float):
+    """Per token of an fp32 logits row: fine bin f = floor((M - l) / T * 65536/28) (65536 = none beyond 28) and the
+    integer mass floor(exp((l - M) / T) * 2^40) (0 for none), as sampler.hip computes them for row max M."""
     l = l.float().cpu()
     invT = torch.tensor(1.0, dtype=torch.float32) / torch.tensor(T, dtype=torch.float32)
-    M = l.max()
+    M = torch.tensor(M, dtype=torch.float32)
     x = ((M - l) * invT) * torch.tensor(NUC_FS, dtype=torch.float32)
     valid = x < 65536.0
     f = torch.where(valid, x, torch.zeros_like(x)).to(torch.int64)
     f = torch.where(valid, f, torch.full_like(f, 65536))
     mass = (torch.exp((l - M) * invT) * 1099511627776.0).to(torch.int64)
-    mass = torch.where(valid, mass, torch.zeros_like(mass))
-    Z = int(mass.sum())
-    target = int(float(Z) * float(np.float32(P)))
-    coarse = torch.zeros(257, dtype=torch.int64).index_add_(0, torch.clamp(f >> 8, max=256), mass)[:256]
-    cum = torch.cumsum(coarse, 0)
-    hit = ((cum >= target) & (coarse != 0)).nonzero()
-    bstar = int(hit[0]) if len(hit) else 255
-    above = int(cum[bstar] - coarse[bstar])
+    return f, torch.where(valid, mass, torch.zeros_like(mass))
+
+
+def nucleus_coarse_hist(f: torch.Tensor, mass: torch.Tensor) -> torch.Tensor:
+    return torch.zeros(257, dtype=torch.int64).index_add_(0, torch.clamp(f >> 8, max=256), mass)[:256]
+
+
+def nucleus_fine_hist(f: torch.Tensor, mass: torch.Tensor, bstar: int) -> torch.Tensor:
     inb = (f >> 8) == bstar
-    fine = torch.zeros(256, dtype=torch.int64).index_add_(0, (f & 255)[inb], mass[inb])
-    cum = above + torch.cumsum(fine, 0)
-    hit = ((cum >= target) & (fine != 0)).nonzero()
-    fstar = bstar * 256 + (int(hit[0]) if len(hit) else 255)
+    return torch.zeros(256, dtype=torch.int64).index_add_(0, (f & 255)[inb], mass[inb])
+
+
+def nucleus_pick(hist: torch.Tensor, target: int, above: int = 0):
+    """(first bin where above + the cumulative mass reaches target -- 255 if none --, mass before that bin)."""
+    cum = above + torch.cumsum(hist, 0)
+    hit = ((cum >= target) & (hist != 0)).nonzero()
+    b = int(hit[0]) if len(hit) else 255
+    return b, int(cum[b] - hist[b])
+
+
+def nucleus_target(coarse: torch.Tensor, P: float) -> int:
+    return int(float(int(coarse.sum())) * float(np.float32(P)))
+
+
+def nucleus_mask(l: torch.Tensor, T: float, P: float) -> torch.Tensor:
+    """The nucleus of sampler.hip for one row of fp32 logits: fine bin f = floor((M - l) / T * 65536/28)
+    (none beyond 28), mass = floor(exp((l - M) / T) * 2^40) as an integer, target = floor(Z * P); the
+    smallest f* with mass{f <= f*} >= target is found coarse (f >> 8) then fine (f & 255); keep f <= f*."""
+    l = l.float().cpu()
+    f, mass = nucleus_fine_mass(l, float(l.max()), T)
+    coarse = nucleus_coarse_hist(f, mass)
+    target = nucleus_target(coarse, P)
+    bstar, above = nucleus_pick(coarse, target)
+    fstar = bstar * 256 + nucleus_pick(nucleus_fine_hist(f, mass, bstar), target, above)[0]
     return f <= fstar
+
+
+def sample_key(l: torch.Tensor, T: float, seed: int, ctr: int, id0: int, keep=None):
+    """(score, global id) of the best token of one logits row whose token ids start at ``id0`` (a vocab shard):
+    greedy (T <= 0) or Gumbel-max over ``keep``; ties to the lowest id, like sampler.hip's packed keys.  None if
+    ``keep`` leaves no token."""
+    l = l.float()
+    vid = torch.arange(l.numel(), dtype=torch.int64, device=l.device) + id0
+    if T <= 0:
+        score = l
+    else:
+        u = u01(hash3(int(seed), int(ctr), vid)).float()
+        score = l / T - torch.log(-torch.log(u))
+    if keep is not None:
+        score = torch.where(keep.to(score.device), score, torch.full_like(score, float("-inf")))
+        if not bool(keep.any()):
+            return None
+    m = score.max()
+    i = int((score == m).nonzero()[0])
+    return float(m), int(vid[i])
 
 
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor,
@@ -294,21 +334,49 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
     of the Gumbel scores and of the per-token masses at a nucleus boundary)."""
     B, V = logits.shape
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
-    vid = torch.arange(V, dtype=torch.int64, device=logits.device)
     for b in range(B):
         l = logits[b].float()
-        T = float(temperature[b])
-        if T <= 0:
-            out[b] = int(torch.argmax(l))
-            continue
-        keep = torch.ones(V, dtype=torch.bool, device=l.device)
-        P = float(top_p[b])
-        if P < 1.0:
-            keep = nucleus_mask(l, T, P).to(l.device)
-        u = u01(hash3(int(seeds[b]), int(counter[b]), vid)).float()
-        g = -torch.log(-torch.log(u))
-        score = torch.where(keep, l / T + g, torch.full_like(l, float("-inf")))
-        out[b] = int(torch.argmax(score))
+        T, P = float(temperature[b]), float(top_p[b])
+        keep = nucleus_mask(l, T, P) if T > 0 and P < 1.0 else None
+        out[b] = sample_key(l, T, int(seeds[b]), int(counter[b]), 0, keep)[1]
+    return out
+
+
+def sample_vocab_parallel(local: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor,
+                          counter: torch.Tensor, rank: int, gather) -> torch.Tensor:
+    """Vocab-parallel form of :func:`sample` (sampler.hip's TP path, on CPU): ``local`` [B, Vs] is this rank's vocab
+    shard (global ids rank * Vs ..), ``gather(t)`` all-gathers a tensor over the ranks ([world, *t.shape]).  Nucleus
+    rows combine the row max and the two integer bin histograms over the ranks, then every rank's best (score, id)
+    is gathered and the best of them taken: the tokens of :func:`sample` over the concatenated shards."""
+    B, Vs = local.shape
+    id0 = rank * Vs
+    nuc = [float(temperature[b]) > 0 and float(top_p[b]) < 1.0 for b in range(B)]
+    keep = [None] * B
+    if any(nuc):
+        M = gather(local.float().max(dim=1).values).max(dim=0).values
+        fm = [nucleus_fine_mass(local[b], float(M[b]), float(temperature[b])) if nuc[b] else None for b in range(B)]
+        z = torch.zeros(256, dtype=torch.int64)
+        coarse = gather(torch.stack([nucleus_coarse_hist(*fm[b]) if nuc[b] else z for b in range(B)])).sum(0)
+        sel = {}
+        for b in range(B):
+            if nuc[b]:
+                target = nucleus_target(coarse[b], float(top_p[b]))
+                sel[b] = (target,) + nucleus_pick(coarse[b], target)
+        fine = gather(torch.stack([nucleus_fine_hist(*fm[b], sel[b][1]) if nuc[b] else z for b in range(B)])).sum(0)
+        for b in range(B):
+            if nuc[b]:
+                target, bstar, above = sel[b]
+                keep[b] = fm[b][0] <= bstar * 256 + nucleus_pick(fine[b], target, above)[0]
+    best = torch.full((B, 2), float("-inf"), dtype=torch.float64)
+    for b in range(B):
+        k = sample_key(local[b], float(temperature[b]), int(seeds[b]), int(counter[b]), id0, keep[b])
+        if k is not None:
+            best[b, 0], best[b, 1] = k[0], -k[1]
+    g = gather(best)                                  # [world, B, 2]: (score, -id); max = best score, lowest id
+    out = torch.empty(B, dtype=torch.int32)
+    for b in range(B):
+        cand = [tuple(g[r, b].tolist()) for r in range(g.shape[0])]
+        out[b] = int(-max(cand)[1])
     return out
 
 

@@ -72,6 +72,12 @@ class ReplicaLink:
         return box[0]
 
     # ---- rank-0 side
+    def start(self) -> None:
+        """Rank 0, once its engine is built (ReplicaRouterBackend does this): start the receive thread and the
+        keepalive, whose first ping goes out at once -- the remote leader is parked in ``receive`` since ITS engine
+        build, and an idle link must not let that wait reach the gloo timeout."""
+        self._start_rx()
+
     def _start_rx(self) -> None:
         if self._rx is not None:
             return
@@ -103,11 +109,13 @@ class ReplicaLink:
 
         def keepalive():
             every = max(0.05, self.timeout_s / 4)
-            while not self._closing.wait(every / 4):
+            first = True
+            while first or not self._closing.wait(every / 4):
                 if self.dead:
                     return
-                if time.monotonic() - self._last_send < every:
+                if not first and time.monotonic() - self._last_send < every:
                     continue
+                first = False
                 try:
                     self._send(_PING)
                 except Exception as e:  # noqa: BLE001
@@ -213,6 +221,8 @@ class ReplicaRouterBackend:
         self._local_inflight = 0
         self._lock = threading.Lock()
         self._cursor = 0
+        for link in self.links:    # keepalives from now on, whether or not a request ever comes
+            link.start()
 
     @property
     def replicas(self) -> int:

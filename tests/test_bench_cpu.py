@@ -106,3 +106,13 @@ def test_bench_refuses_gpus_that_disagree_with_world_size():
                         "--steps", "1", "--warmup", "0"], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=120)
     assert p.returncode != 0 and "WORLD_SIZE" in p.stderr and not p.stdout.strip()
+
+
+def test_simulated_tp_reports_the_gpus_it_used():
+    """--simulate-tp runs ONE rank's shapes on one device with the collectives skipped; its line
+    must not read as a multi-GPU result: n_gpus is the devices used, the simulated degree has its own field."""
+    p = _run("--preset", "tiny-tp8", "--simulate-tp", "4", "--steps", "1", "--warmup", "1", "--gen-tokens", "4")
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 1 and d["simulated_tp"] == 4, d
+    assert d["config"]["parallelism"] == "tp4-SIMULATED-no-comm"

@@ -61,6 +61,7 @@ class _Apiserver(BaseHTTPRequestHandler):
 
     fake: FakeKubeAPI = None
     token = "s3cret"
+    script = None        # raw watch events to stream instead of the fake's (ERROR / BOOKMARK tests)
 
     def log_message(self, *a):
         pass
@@ -92,7 +93,9 @@ class _Apiserver(BaseHTTPRequestHandler):
             self.send_response(200)
             self.send_header("Content-Type", "application/json")
             self.end_headers()
-            for typ, obj in self.fake.watch_pods(None, timeout_seconds=float(q.get("timeoutSeconds", 1))):
+            evs = self.script if self.script is not None else \
+                self.fake.watch_pods(None, timeout_seconds=float(q.get("timeoutSeconds", 1)))
+            for typ, obj in evs:
                 self.wfile.write((json.dumps({"type": typ, "object": obj}) + "\n").encode())
                 self.wfile.flush()
             return
@@ -157,3 +160,36 @@ def test_rest_client_auth_error(apiserver):
     with pytest.raises(ApiError) as ei:
         RestKubeAPI(conn).list_nodes()
     assert ei.value.status == 401
+
+
+def test_rest_watch_ends_on_410_and_hides_bookmarks(apiserver):
+    """ERROR events carry a Status, BOOKMARK events only a resourceVersion.  A 410 Gone ends the
+    stream at once (the watch loop then re-LISTs), a bookmark advances the client's resourceVersion and never reaches
+    the consumer as a pod, any other ERROR raises (the loop's error back-off)."""
+    fake, kc = apiserver
+    api = RestKubeAPI(KubeConnection.from_kubeconfig(kc))
+    p1, p2 = make_pod("p1"), make_pod("p2")
+    p1["metadata"]["resourceVersion"] = "40"
+    bookmark = {"kind": "Pod", "metadata": {"resourceVersion": "42"}}
+    gone = {"kind": "Status", "status": "Failure", "reason": "Expired", "code": 410,
+            "message": "too old resource version: 7 (40)"}
+    try:
+        _Apiserver.script = [("ADDED", p1), ("BOOKMARK", bookmark), ("ERROR", gone), ("ADDED", p2)]
+        events = list(api.watch_pods("7", timeout_seconds=1))
+        assert [(t, o["metadata"]["name"]) for t, o in events] == [("ADDED", "p1")]
+        assert api.last_resource_version == "42"
+        _Apiserver.script = [("ERROR", {"kind": "Status", "code": 500, "reason": "InternalError"})]
+        with pytest.raises(ApiError) as ei:
+            list(api.watch_pods(None, timeout_seconds=1))
+        assert ei.value.status == 500
+    finally:
+        _Apiserver.script = None
+    # the snapshotter never sees a Status / bookmark object as a pod: the informer counts stay the pods' own
+    from k8s_llm_scheduler_amd.control.cluster import ClusterSnapshotter
+
+    snap = ClusterSnapshotter(api)
+    fake.create_pod(make_pod("p3", node_name="n1", phase="Running"))
+    snap.seed()
+    for typ, obj in [("ADDED", p1)]:
+        snap.observe(typ, obj)
+    assert {m.name: m.pod_count for m in snap.get_node_metrics()} == {"n1": 1, "n2": 0}

@@ -594,50 +594,6 @@ def test_linear_norm_folded(M, epi, N):
     close(got8, exact(ref.dequant_fp8(wq.q.cpu(), wq.scale.cpu())), 3e-2)
 
 
-@pytest.mark.parametrize("nq,nkv,B", [(8, 1, 1), (8, 1, 2), (16, 2, 1), (16, 2, 2)])
-def test_attention_oproj_fused_matches_separate(nq, nkv, B, monkeypatch):
-    """decode_split_oproj_kernel (split attention + O projection in one launch, the TP=8 / TP=4 decode
-    shards) against the two separate kernels, over short / chunk-merge / padded-row contexts, eager and
-    replayed from a hipGraph (the sync words re-arm every launch), and no wait ever timed out."""
-    D, bs, N = 128, 16, 8192
-    maxb = 4096 // bs
-    kc = rnd(B * maxb * bs, nkv, D)
-    vc = rnd(B * maxb * bs, nkv, D)
-    bt = torch.arange(B * maxb, device=DEV, dtype=torch.int32).view(B, maxb)
-    cs = ref.rope_table(D, 4096, 500000.0, None).to(DEV)
-    wo = rnd(N, nq * D, scale=0.05)
-    monkeypatch.setattr(ops, "FUSE_ATTN_O", True)   # opt-in kernel
-    assert ops.attn_oproj_fusable(B, wo, 4096, nq, nkv, D)
-    for ctxs in ([1] * B, [64] * B, [564, 300][:B], [2000, 0][:B]):
-        qkv = rnd(B, (nq + 2 * nkv) * D)
-        cl = torch.tensor(ctxs, device=DEV, dtype=torch.int32)
-        k0, v0 = kc.clone(), vc.clone()
-        a = ops.decode_attention_fused(qkv, cs, k0, v0, bt, cl, 0.088, bs, 4096, nq, nkv, D)
-        want = ops.linear(a, wo).float()
-        k1, v1 = kc.clone(), vc.clone()
-        got = ops.decode_attention_oproj(qkv, cs, k1, v1, bt, cl, 0.088, bs, 4096, nq, nkv, D, wo).float()
-        torch.cuda.synchronize()
-        live = cl > 0
-        close(got[live], want[live], 2e-2)
-        assert torch.equal(k0, k1) and torch.equal(v0, v1)      # the same KV-cache writes
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    cl = torch.tensor([564, 300][:B], device=DEV, dtype=torch.int32)
-    with torch.cuda.stream(s):
-        ops.decode_attention_oproj(qkv, cs, kc, vc, bt, cl, 0.088, bs, 4096, nq, nkv, D, wo)
-    torch.cuda.current_stream().wait_stream(s)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
-        og = ops.decode_attention_oproj(qkv, cs, kc, vc, bt, cl, 0.088, bs, 4096, nq, nkv, D, wo)
-    ref_o = None
-    for _ in range(4):
-        g.replay()
-        torch.cuda.synchronize()
-        ref_o = og.clone() if ref_o is None else ref_o
-        assert torch.equal(og, ref_o)
-    assert ops.attn_oproj_timeouts(torch.device(DEV)) == 0
-
-
 @pytest.mark.parametrize("M", [1, 2])
 @pytest.mark.parametrize("epi,folded", [(0, False), (1, True), (2, True), (2, False), (0, True)])
 @pytest.mark.parametrize("fp8", [False, True])

@@ -190,32 +190,6 @@ def test_fp8_model_gpu_matches_cpu_reference():
     torch.testing.assert_close(dec_g.cpu(), dec_c, atol=8e-2, rtol=5e-2)
 
 
-def test_tp8_shard_decode_with_fused_attention_oproj(monkeypatch):
-    """One TP=8 rank's decode (64 q / 8 kv heads -> 8 / 1 per rank, o_proj K = 1024): the one-launch
-    attention + O projection gives the logits of the separate kernels, over two decode steps."""
-    from k8s_llm_scheduler_amd.parallel import TPGroup
-
-    cfg = LlamaConfig("tp8shape", 2, 2048, 64, 8, 128, 4096, 16384, bos_id=16128, eos_ids=(16137,),
-                      max_position=4096)
-    m = LlamaModel(cfg, TPGroup(0, 8, None, "none", simulate=True), device="cuda", seed=5, max_model_len=2048)
-    ids = list(range(60, 460, 3))
-    _, bt = _prefill(m, ids)
-    kv0 = m.kv_cache.clone()
-    outs = {}
-    for fused in (False, True):
-        monkeypatch.setattr(ops, "FUSE_ATTN_O", fused)
-        m.kv_cache.copy_(kv0)
-        steps = []
-        for i in range(2):
-            ctx = torch.tensor([len(ids) + 1 + i], dtype=torch.int32, device="cuda")
-            tok = torch.tensor([200 + i], dtype=torch.int32, device="cuda")
-            steps.append(m.forward_decode(tok, ctx, bt, 2048).float())
-        outs[fused] = torch.cat(steps)
-    torch.cuda.synchronize()
-    torch.testing.assert_close(outs[True], outs[False], atol=3e-2, rtol=3e-2)
-    assert ops.attn_oproj_timeouts(torch.device("cuda")) == 0
-
-
 @pytest.mark.parametrize("k", [1, 6])
 def test_engine_gpu_forced_json_close_exact_decode_steps(k):
     """Device-side stop detection in the decode graphs: the closing brace at answer token k costs exactly k decode

@@ -125,6 +125,15 @@ def _vote_rank(rank, world):
             out["raised"] = True
         out["took"] = time.monotonic() - t0
     dist.barrier()
+    # rank 0's failed vote advanced only ITS round counter; the next reset generation (bumped by the leader)
+    # restarts the rounds on every rank, so the ranks vote in the same round again -- and finished rounds leave no keys
+    if rank == 0:
+        control.request_reset()
+    dist.barrier()
+    out["after"] = control.any_rank(rank == 0, timeout_s=30)
+    st = control.store()
+    out["first_round_keys_left"] = st.check([f"k8s_vote/0/0.1/{r}" for r in range(world)])
+    dist.barrier()
     dist.destroy_process_group()
     return out
 
@@ -135,3 +144,5 @@ def test_recovery_vote_is_bounded():
     res = run_ranks(_vote_rank, 2, timeout_s=120)
     assert res[0]["both"] and res[1]["both"]
     assert res[0]["raised"] and res[0]["took"] < 10
+    assert res[0]["after"] and res[1]["after"]
+    assert not res[0]["first_round_keys_left"] and not res[1]["first_round_keys_left"]

@@ -202,7 +202,7 @@ def test_idle_link_sends_keepalives_and_leader_answers_them():
             return obj
 
     link = _Link(1, 4, "down", "up", timeout_s=0.2)
-    link._start_rx()
+    link.start()
     _t.sleep(0.5)
     assert R._PING in sent and not link.dead
     pong.set()
@@ -226,3 +226,59 @@ def test_idle_link_sends_keepalives_and_leader_answers_them():
     R.serve_replica(_Backend(), _Leader(1, 4, "down", "up"), engine=None, workers=1)
     assert up == [R._PONG, R._STOP]
     link._closing.set()
+
+
+def _idle_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), K8S_REPLICA_LINK_TIMEOUT_S="2")
+    torch.set_num_threads(1)
+    import time as _t
+
+    from k8s_llm_scheduler_amd.parallel import init_from_env
+    from k8s_llm_scheduler_amd.parallel.replicas import ReplicaRouterBackend, make_replica_links, serve_replica
+
+    try:
+        tp = init_from_env("cpu", backend="gloo", tp_size=1)
+        links = make_replica_links(tp)
+        assert links and links[0].timeout_s == 2.0
+        eng = build_engine("tiny", tp=tp, device="cpu", max_batch=2, max_model_len=256, num_blocks=64, seed=1)
+        local = LocalEngineBackend(eng, ignore_eos=True)
+        if tp.global_rank == 0:
+            router = ReplicaRouterBackend(local, links)     # no request yet: the link must stay up on its own
+            _t.sleep(7.0)                                   # 3.5 x the gloo link timeout, idle
+            texts = router.complete(_requests()[:2])        # one request per replica
+            disp, dead = list(router.dispatched), links[0].dead
+            router.shutdown()
+            q.put(("router", texts, disp, dead))
+        else:
+            serve_replica(local, links[0], eng)
+            q.put(("leader",))
+    except BaseException:  # noqa: BLE001
+        import traceback
+
+        q.put(("error", rank, traceback.format_exc()))
+        raise
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_idle_router_keeps_remote_replica_alive_past_the_link_timeout():
+    """a scheduler that sends no pod for longer than the link timeout must not lose its remote
+    replicas.  The router starts each link's keepalive when it is built (not on the first submit), so the remote
+    leader's receive is answered within a quarter of the timeout from the start; after idling 3.5 timeouts both
+    replicas still answer."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_idle_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(60)
+    errs = [g for g in got if g[0] == "error"]
+    assert not errs, errs
+    router = next(g for g in got if g[0] == "router")
+    _, texts, disp, dead = router
+    assert len(texts) == 2 and disp == [1, 1] and not dead, router

@@ -29,6 +29,8 @@ class CycleModel(LlamaModel):
 
     def _force(self, logits, inputs):
         out = torch.full_like(logits, -30.0)
+        if logits.shape[0] == 1 and self.tp.world > 1 and self.tp.rank != 0:
+            return out                                  # this rank's vocab shard (vocab-parallel): ids >= Vs only
         t = inputs.long().to(logits.device)
         nxt = torch.where((t >= 10) & (t < 15), 10 + (t - 9) % 5, torch.full_like(t, 10))
         out[0].scatter_(1, nxt.view(-1, 1), 30.0)      # capturable (no host index or value tensors)

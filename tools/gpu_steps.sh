@@ -2,15 +2,14 @@
 #   tests       pytest -m gpu (the driver's round-end suite)
 #   smoke       __graft_entry__.smoke()
 #   bench       bench.py defaults (the driver's N=1 run)
-#   tp8sim      bench.py --simulate-tp 8 (one TP=8 rank's shapes, collectives skipped); PERSIST=0/1 picks the decode
+#   tp8sim      bench.py --simulate-tp 8 (one TP=8 rank's shapes, collectives skipped)
 #   b64         bench.py --batch 64 (config 4 at N=1)
 #   fp8         bench.py --dtype fp8 (config 5 shapes at TP=1) and --dtype fp8 --simulate-tp 4
 #   prof        rocprofv3 kernel stats + last-forward timeline of the default bench (tools/gpu_prof.sh)
-#   proftp8     the same for --simulate-tp 8 (PERSIST=0/1)
+#   proftp8     the same for --simulate-tp 8
 #   kbench      tools/kbench.py per-kernel microbench at TP=1 and TP=8 shapes
 #   nodes256    bench.py --nodes 256 (22k-token prompts), 10 timed steps
 #   gen200      bench.py --gen-tokens 200 (the reference's max_tokens) at TP=1 and --simulate-tp 8
-#   persist     the layer-persistent decode: its GPU tests, then --simulate-tp 8 and Llama-3-8B A/B (off vs on)
 # Each step has its own time limit; test failures (rc 1) do not stop later steps, a timeout / abort / fault (any other
 # rc) ends the script.  Logs land in gpurun_out/$OUT (default run).
 set -o pipefail
@@ -31,14 +30,14 @@ for spec in ${RUNS:-tests smoke bench}; do
     tests)   step 1100 gpu_tests.log $PT -m gpu tests; tail -3 "$O/gpu_tests.log" ;;
     smoke)   step 300 smoke.log python -u -c "import __graft_entry__ as g; g.smoke()"; tail -2 "$O/smoke.log" ;;
     bench)   step 400 bench_default.json python -u bench.py --steps ${STEPS:-10} --warmup 2; tail -1 "$O/bench_default.json" ;;
-    tp8sim)  K8S_DECODE_PERSIST=${PERSIST:-0} step 400 bench_tp8sim_p${PERSIST:-0}.json python -u bench.py --simulate-tp 8 --steps ${STEPS:-10} --warmup 2
-             tail -1 "$O/bench_tp8sim_p${PERSIST:-0}.json" ;;
+    tp8sim)  step 400 bench_tp8sim.json python -u bench.py --simulate-tp 8 --steps ${STEPS:-10} --warmup 2
+             tail -1 "$O/bench_tp8sim.json" ;;
     b64)     step 600 bench_b64.json python -u bench.py --batch 64 --steps ${STEPS:-3} --warmup 1; tail -1 "$O/bench_b64.json" ;;
     fp8)     step 400 bench_fp8.json python -u bench.py --dtype fp8 --steps ${STEPS:-10} --warmup 2; tail -1 "$O/bench_fp8.json"
              step 400 bench_fp8_tp4sim.json python -u bench.py --dtype fp8 --simulate-tp 4 --steps ${STEPS:-10} --warmup 2
              tail -1 "$O/bench_fp8_tp4sim.json" ;;
     prof)    step 700 prof_default.log bash tools/gpu_prof.sh default ""; cat "$O/prof_default.log" | head -25 ;;
-    proftp8) K8S_DECODE_PERSIST=${PERSIST:-0} step 700 prof_tp8sim.log bash tools/gpu_prof.sh tp8sim_p${PERSIST:-0} "--simulate-tp 8"
+    proftp8) step 700 prof_tp8sim.log bash tools/gpu_prof.sh tp8sim "--simulate-tp 8"
              head -25 "$O/prof_tp8sim.log" ;;
     nodes256) step 900 bench_nodes256.json python -u bench.py --nodes 256 --max-model-len 32768 --steps ${STEPS:-10} --warmup 1
              tail -1 "$O/bench_nodes256.json" ;;
@@ -47,13 +46,6 @@ for spec in ${RUNS:-tests smoke bench}; do
              step 400 bench_tp8sim_gen200.json python -u bench.py --gen-tokens 200 --simulate-tp 8 --steps ${STEPS:-10} --warmup 2
              tail -1 "$O/bench_tp8sim_gen200.json" ;;
     kbench)  step 300 kbench_tp1.txt python -u tools/kbench.py --tp 1; step 300 kbench_tp8.txt python -u tools/kbench.py --tp 8 ;;
-    persist) step 600 persist_tests.log $PT tests/test_persist_gpu.py; tail -3 "$O/persist_tests.log"
-             for p in 0 1; do
-               K8S_DECODE_PERSIST=$p step 400 bench_tp8sim_p$p.json python -u bench.py --simulate-tp 8 --steps ${STEPS:-10} --warmup 2
-               tail -1 "$O/bench_tp8sim_p$p.json"
-               K8S_DECODE_PERSIST=$p step 400 bench_8b_p$p.json python -u bench.py --preset llama-3-8b --steps ${STEPS:-10} --warmup 2
-               tail -1 "$O/bench_8b_p$p.json"
-             done ;;
     *) echo "unknown step $spec"; exit 2 ;;
   esac
 done

@@ -104,22 +104,6 @@ def main():
                         a.iters)
             res.append((f"decode_attn[{tag}] ctx={c2}", us, 0))
     ops.SPLIT_MAX_PAIRS = default_pairs
-    wo = (torch.randn(H, nq * D, device=dev) * 0.02).to(bf)
-    fuse = ops.FUSE_ATTN_O
-    ops.FUSE_ATTN_O = True   # time the opt-in one-launch kernel against the default two launches
-    if ops.attn_oproj_fusable(M, wo, 1024, nq, nkv, D):
-        us = timeit(lambda: ops.linear(ops.decode_attention_fused(qkv, cs, kc, vc, bt, cl, 0.088, bs, 1024, nq, nkv, D),
-                                       wo), a.iters)
-        res.append((f"attn + o_proj, two launches ctx={ctx}", us, 0))
-        keep = (ops.ATTN_O_DELAY, ops.ATTN_O_POLL)
-        for delay in (0, 1, 2, 3):
-            for poll in (1, 4, 16):
-                ops.ATTN_O_DELAY, ops.ATTN_O_POLL = delay, poll
-                us = timeit(lambda: ops.decode_attention_oproj(qkv, cs, kc, vc, bt, cl, 0.088, bs, 1024, nq, nkv, D,
-                                                               wo), a.iters)
-                res.append((f"attn + o_proj, one launch ctx={ctx} delay={delay} poll={poll}", us, 0))
-        ops.ATTN_O_DELAY, ops.ATTN_O_POLL = keep
-    ops.FUSE_ATTN_O = fuse
     q = torch.randn(M, nq, D, device=dev).to(bf)
     us = timeit(lambda: ops.paged_decode_attention(q, kc, vc, bt, cl, 0.088, bs, 1024), a.iters)
     res.append((f"paged_decode_attention(split64) ctx={ctx}", us, 2 * ctx * nkv * D * 2 * M / us / 1e6))

@@ -71,7 +71,7 @@ def main() -> int:
 
 def layer_view(rows) -> None:
     att = [i for i, (n, _, _) in enumerate(rows)
-           if any(k in n for k in ("decode_fused", "decode_split", "decode_persist", "paged_decode"))]
+           if any(k in n for k in ("decode_fused", "decode_split", "paged_decode"))]
     if len(att) < 4:
         return
     per = att[1] - att[0]

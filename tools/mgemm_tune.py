@@ -6,10 +6,7 @@ separate silu_mul kernel for gate/up; fp8: per-token quantization + torch._scale
 Every candidate (tile config x split-K) is timed as a captured hipGraph of REPS launches that cycle over enough
 copies of the weight to exceed the 256 MiB Infinity Cache (weights are cold in the real decode / prefill loop).
 
-    python tools/mgemm_tune.py --tp 1 8 --m 16 64 256 [--fp8 | --w8] [--write]
-
---w8 tunes mgemm's W8 mode (fp8 weights, bf16 activations; table key fp8 = 2) against the per-token e4m3 path it
-replaces (quantize_act_fp8 + the tuned fp8 mgemm plan).
+    python tools/mgemm_tune.py --tp 1 8 --m 16 64 256 [--fp8 | --mx] [--write]
 
 --mx tunes the K16 MX modes (fp8 weights) as the decode layer runs them: QKV with MX activations and the RMS
 prologue, O / down with MX activations and the residual epilogue writing the stream's MX copy (table key fp8 = 3),
@@ -83,7 +80,7 @@ def candidates(M, N, K, epi, fp8, mx_out=False):
     mode = 3 if fp8 == 4 else fp8
     for c, (bm, bn, _th, _lds, _sw, rb) in enumerate(cfgs):
         steps = K * (1 if fp8 else 2) // rb
-        if fp8 in (2, 3, 4) and not ops.mgemm_valid(c, M, N, K, epi, mode, 1, mx_out):
+        if fp8 in (3, 4) and not ops.mgemm_valid(c, M, N, K, epi, mode, 1, mx_out):
             continue
         if bm > max(16, 2 * M) or (M > 64 and bm < 64) or (M > 256 and bm < 128):
             continue
@@ -103,7 +100,7 @@ def candidates(M, N, K, epi, fp8, mx_out=False):
 def lib_fn(x, Ws, epi, fp8):
     def f(i):
         w = Ws[i]
-        if fp8 in (2, 3, 4):   # W8 / MX tuning: the per-token e4m3 path it replaces (quantize + the tuned fp8 plan)
+        if fp8 in (3, 4):   # MX tuning: the per-token e4m3 path it replaces (quantize + the tuned fp8 plan)
             return ops.mgemm(x, w, epi)
         if fp8:
             y = ops._fp8_gemm(x, w)
@@ -126,7 +123,6 @@ def main() -> int:
     ap.add_argument("--all-buckets", action="store_true", help="every row bucket of ops.GEMM_M_BUCKETS + 2048..8192")
     ap.add_argument("--only", nargs="*", default=None, help="projection names")
     ap.add_argument("--fp8", action="store_true")
-    ap.add_argument("--w8", action="store_true", help="tune the W8 mode (fp8 weights, bf16 activations)")
     ap.add_argument("--mx", action="store_true", help="tune the MX modes (MX activations; MX SwiGLU output)")
     ap.add_argument("--insitu", action="store_true",
                     help="bf16: time O / down with the residual epilogue and gate/up with the RMS prologue, as the "
@@ -137,8 +133,6 @@ def main() -> int:
     ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
     a = ap.parse_args()
 
-    if a.w8:
-        a.fp8 = 2
     if a.all_buckets:
         a.m = list(ops.GEMM_M_BUCKETS) + [2048, 4096, 8192]
     torch.manual_seed(0)
@@ -175,7 +169,7 @@ def main() -> int:
                 best = (float("inf"), None)
 
                 def run(i, c, gr):
-                    return ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr, w8=a.fp8 == 2, act=ACT[0],
+                    return ops.mgemm(x, Ws[i], epi, cfg=c, grid=gr, act=ACT[0],
                                      mx_out=a.fp8 == 4 or (res_mx and a.mx), res=RES,
                                      rms_eps=1e-5 if rms_mx else None)
 
