@@ -33,12 +33,52 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
 
 __device__ __forceinline__ int vswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
+// Cascade decode attention: sh shared 64-token spans are cut into groups of ceil(sh / ngm) spans, one partial
+// (max, sum, unnormalised P.V, per query head) per group; every reader derives the same group count from sh.
+constexpr int CASCADE_MAX_GROUPS = 32;
+__device__ __forceinline__ int cascade_groups(int sh, int ngm) {
+  if (sh <= 0 || ngm <= 0) return 0;
+  const int spg = (sh + ngm - 1) / ngm;
+  return (sh + spg - 1) / spg;
+}
+// Fold the npre prefix partials of one (row, head) into (M, num, den) at element d: every load issued up front
+// (unconditional, clamped to the last live group -- a loop of dependent waits would cost one round trip per group).
+__device__ __forceinline__ void cascade_fold(const float* __restrict__ pre_acc, const float* __restrict__ pre_ml,
+                                             size_t pb, int npre, int d, float& M, float& num, float& den) {
+  constexpr int D = 128;
+  float pm[CASCADE_MAX_GROUPS], pl[CASCADE_MAX_GROUPS], pa[CASCADE_MAX_GROUPS];
+#pragma unroll
+  for (int k = 0; k < CASCADE_MAX_GROUPS; ++k) {
+    const size_t kk = pb + (size_t)min(k, npre - 1);
+    pm[k] = pre_ml[kk * 2];
+    pl[k] = pre_ml[kk * 2 + 1];
+    pa[k] = pre_acc[kk * D + d];
+  }
+  float Mt = M;
+#pragma unroll
+  for (int k = 0; k < CASCADE_MAX_GROUPS; ++k)
+    if (k < npre) Mt = fmaxf(Mt, pm[k]);
+  const float a = exp2f(M - Mt);   // (M = -inf: no per-row part yet, a = 0)
+  num *= a;
+  den *= a;
+#pragma unroll
+  for (int k = 0; k < CASCADE_MAX_GROUPS; ++k) {
+    if (k < npre) {
+      const float w = exp2f(pm[k] - Mt);
+      num += w * pa[k];
+      den += w * pl[k];
+    }
+  }
+  M = Mt;
+}
+
 template <int D, int G, int PART, int NW>
 __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_acc, float* __restrict__ part_ml, const bf16_t* __restrict__ qkv,
     const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ context_lens, float scale, int block_size,
-    int max_blocks, int nkv, int pmax, uint8_t* __restrict__ oq, uint8_t* __restrict__ oe) {
+    int max_blocks, int nkv, int pmax, uint8_t* __restrict__ oq, uint8_t* __restrict__ oe,
+    const int* __restrict__ cas, const float* __restrict__ pre_acc, const float* __restrict__ pre_ml, int ngm) {
   static_assert(D == 128 && G <= 16, "head_dim 128, group <= 16");
   static_assert(PART / NW == 64, "64 tokens per wave");
   constexpr int NT = NW * WAVE;
@@ -57,7 +97,12 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
   const int li = lane & 15, g4 = lane >> 4;
   const int* bt = block_tables + (size_t)b * max_blocks;
   const size_t kvs = (size_t)nkv * D;
-  const int start = p * PART;
+  // cascade (decode_prefix_kernel ran first): the first 64 * sh context tokens are the batch's shared prefix, already
+  // attended by that kernel; the partitions start after it (p * PART tokens past it) and the row's prefix partials
+  // join the merge.  (sh: one extra round trip before the block ids, cascade launches only)
+  const int sh = cas != nullptr ? max(0, __builtin_amdgcn_readfirstlane(*(volatile const int*)cas)) : 0;
+  const int pst = 64 * sh;
+  const int start = pst + p * PART;
   const int wbase = wid * TW;
   // With 16-token blocks a 16-token tile is exactly one cache block, so the rows of this wave depend only on 4
   // block-table entries.  The context length and those entries are one round trip; then every live wave issues
@@ -307,7 +352,9 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
     (&red[0][0])[i] = a;
   }
   __syncthreads();
-  const bool single = ctx <= PART;
+  // (pmax == 1 with a longer context: the caller's max_context is below the row's context -- a precondition
+  // violation; the partition's own tokens are written as the output instead of through absent partial buffers)
+  const bool single = ctx - pst <= PART || pmax == 1;
   for (int i = tid; i < G * D; i += NT) {
     const int g = i / D, d = i - g * D;
     float L = 0.f;
@@ -316,10 +363,18 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
     const int h = kvh * G + g;
     const float sacc_v = red[g][d];
     if (single) {
+      float num = sacc_v, den = L;
+      const int npre = cascade_groups(sh, ngm);
+      if (npre > 0) {   // the shared prefix's partials (log2 domain, the same scale) join this row's
+        float Mw = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) Mw = fmaxf(Mw, wm[w][g]);
+        cascade_fold(pre_acc, pre_ml, ((size_t)b * nq + h) * ngm, npre, d, Mw, num, den);
+      }
       if (oq != nullptr) {   // MX output: the 32 lanes of (head, d / 32) form one half-wave (NT, D: multiples of 32)
-        mx_store_lane(oq, oe, b, h * D + d, nq * D, gridDim.z, bf_round(sacc_v / L));
+        mx_store_lane(oq, oe, b, h * D + d, nq * D, gridDim.z, bf_round(num / den));
       } else {
-        out[((size_t)b * nq + h) * D + d] = f2bf(sacc_v / L);
+        out[((size_t)b * nq + h) * D + d] = f2bf(num / den);
       }
     } else {
       float Mx = -INFINITY;
@@ -332,16 +387,235 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
   }
 }
 
+// ---- Cascade part 1: the shared prefix of a decode batch, read ONCE for every row that shares it.
+// Batched scheduling decides many pods against one cluster snapshot; with the cluster-first prompt layout every
+// prompt of a batch starts with the same thousands of tokens, which the prefix cache stores once -- but the
+// per-row attention above would still read those K/V bytes once per row (B times per layer and step).  Here one
+// workgroup = (group of shared 64-token spans, kv head, 8 x 16 query columns): the 16 columns of a wave are the G
+// query heads of 16 / G rows, so one staged K/V span feeds 8 waves x 16 (row, head) columns -- an MFMA-shaped GEMM
+// (S^T = K . Q^T, then P . V) instead of B separate GEMVs over the same bytes.
+//  * the span's K and V (64 tokens x 256 B each) go HBM -> registers -> LDS (one 16-byte load and one ds_write per
+//    thread and operand; the next span's loads in flight under this span's MFMAs), double-buffered, one barrier per
+//    span; K rows in an XOR-swizzled image (conflict-free ds_read_b128 A fragments), V in the attention kernel's
+//    image for the transposing ds_read_b64_tr_b16 B fragments;
+//  * online softmax across the group's spans in the log2 domain (scores x scale x log2 e), the attention kernel's
+//    convention, so the partials merge with its own (decode_fused_kernel / decode_merge_kernel above);
+//  * q is rotated here (RoPE at each row's own position) from the pre-RoPE QKV rows.
+// cas = {sh, r0}: sh spans shared by every active row (the host's longest common block-table prefix, never reaching a
+// row's new token), read from row r0's block table.  Partials: pre_acc [B, nq, ngm, D], pre_ml [B, nq, ngm, 2].
+template <int G>
+__global__ void __launch_bounds__(512) decode_prefix_kernel(
+    float* __restrict__ pre_acc, float* __restrict__ pre_ml, const bf16_t* __restrict__ qkv,
+    const float* __restrict__ cos_sin, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    const int* __restrict__ block_tables, const int* __restrict__ context_lens, const int* __restrict__ cas,
+    float scale, int B, int nkv, int max_blocks, int ngm) {
+  constexpr int D = 128, HALF = D / 2, SPT = 16 / G, ROWB = D * 2;   // rows per 16-column tile, bytes per K/V row
+  static_assert(G >= 1 && G <= 16 && 16 % G == 0, "GQA group of 1, 2, 4, 8 or 16 heads");
+  __shared__ __attribute__((aligned(16))) char stage[2][2][64 * ROWB];   // [buffer][K | V][64 tokens x 256 B]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, li = lane & 15, g4 = lane >> 4;
+  const int sh = cas[0];
+  if (sh <= 0) return;
+  const int spg = (sh + ngm - 1) / ngm;
+  const int s0 = blockIdx.x * spg, s1 = min(s0 + spg, sh);
+  if (s0 >= s1) return;
+  int r0 = cas[1];
+  K8S_CHECK_RANGE(r0, 0, K8S_CHK_SLOT, 0);   // (a host value; checked builds clamp it like any index)
+  r0 = min(max(r0, 0), B - 1);
+  const int kvh = blockIdx.y, nq = nkv * G;
+  const size_t kvs = (size_t)nkv * D;
+  const int* bt0 = block_tables + (size_t)r0 * max_blocks;
+
+  // ---- this lane's query column li: row b = tile * SPT + li / G, head kvh * G + li % G; rotated q as the MFMA B
+  // operand (qf[kk][j] = q[d = 32 kk + 8 g4 + j]: d < 64 for kk < 2, so the lane holds both halves of its RoPE pairs)
+  const int tile = blockIdx.z * 8 + wid;
+  const int bq = tile * SPT + li / G, hq = kvh * G + li % G;
+  const int ctxq = bq < B ? context_lens[bq] : 0;
+  const bool live = ctxq > 0;
+  bf16x8 qf[D / 32];
+#pragma unroll
+  for (int kk = 0; kk < D / 32; ++kk)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[kk][j] = (__bf16)0.f;
+  if (live) {
+    const bf16_t* x = qkv + (size_t)bq * (nq + 2 * nkv) * D + (size_t)hq * D;
+    const float* cs = cos_sin + (size_t)(ctxq - 1) * D;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int d0 = 32 * kk + 8 * g4;
+      const u32x4 xl = *reinterpret_cast<const u32x4*>(x + d0);
+      const u32x4 xh = *reinterpret_cast<const u32x4*>(x + d0 + HALF);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float a = (e & 1) ? hi_bf(xl[e >> 1]) : lo_bf(xl[e >> 1]);
+        const float c2 = (e & 1) ? hi_bf(xh[e >> 1]) : lo_bf(xh[e >> 1]);
+        const float c = cs[d0 + e], sn = cs[d0 + e + HALF];
+        qf[kk][e] = (__bf16)(a * c - c2 * sn);
+        qf[kk + 2][e] = (__bf16)(c2 * c + a * sn);
+      }
+    }
+  }
+
+  // ---- staging: thread tid moves K and V rows (tid >> 4) and 32 + (tid >> 4), 16-byte chunk tid & 15
+  const int srow = tid >> 4, sch = tid & 15;
+  auto blk_of = [&](int s, int j) {   // cache block of this thread's row j of span s
+    int v = bt0[4 * s + (srow >> 4) + 2 * j];
+    K8S_CHECK_RANGE(v, 0, K8S_CHK_BLOCK, 0);
+    return v;
+  };
+  auto load = [&](const int (&bl)[2], u32x4 (&kr)[2], u32x4 (&vr)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const size_t off = (size_t)(bl[j] * 16 + (srow & 15)) * kvs + (size_t)kvh * D + sch * 8;
+      kr[j] = *reinterpret_cast<const u32x4*>(k_cache + off);
+      vr[j] = *reinterpret_cast<const u32x4*>(v_cache + off);
+    }
+  };
+  auto store = [&](int buf, const u32x4 (&kr)[2], const u32x4 (&vr)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = srow + 32 * j;
+      *reinterpret_cast<u32x4*>(&stage[buf][0][r * ROWB + 16 * (sch ^ (r & 15))]) = kr[j];
+      *reinterpret_cast<u32x4*>(&stage[buf][1][r * ROWB + 16 * (sch ^ vswz(r))]) = vr[j];
+    }
+  };
+
+  u32x4 kr[2], vr[2];
+  int bl[2] = {blk_of(s0, 0), blk_of(s0, 1)};
+  load(bl, kr, vr);
+  if (s0 + 1 < s1) {
+    bl[0] = blk_of(s0 + 1, 0);
+    bl[1] = blk_of(s0 + 1, 1);
+  }
+  store(0, kr, vr);
+  __syncthreads();
+
+  const float qscale = scale * LOG2E_F;
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 o[D / 16];
+#pragma unroll
+  for (int nn = 0; nn < D / 16; ++nn) o[nn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int qd = li >> 2, pd = li & 3;
+  for (int s = s0; s < s1; ++s) {
+    const int buf = (s - s0) & 1;
+    const bool more = s + 1 < s1;
+    if (more) {   // (block-uniform) the next span's rows in flight under this span's math
+      load(bl, kr, vr);
+      if (s + 2 < s1) {
+        bl[0] = blk_of(s + 2, 0);
+        bl[1] = blk_of(s + 2, 1);
+      }
+    }
+    const char* kb = stage[buf][0];
+    const char* vb = stage[buf][1];
+    // S^T = K . Q^T: lane holds S[token 16 t + 4 g4 + i][column li]
+    f32x4 sacc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < D / 32; ++kk) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + (16 * t + li) * ROWB + 16 * ((4 * kk + g4) ^ li));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], acc, 0, 0, 0);
+      }
+      sacc[t] = acc;
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sacc[t][i] *= qscale;
+        mloc = fmaxf(mloc, sacc[t][i]);
+      }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, WAVE));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, WAVE));
+    const float m_new = fmaxf(m_run, mloc);
+    const float alpha = exp2f(m_run - m_new);   // (0 on the first span: m_run = -inf)
+    float lsum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = exp2f(sacc[t][i] - m_new);
+        sacc[t][i] = e;
+        lsum += e;
+      }
+    lsum += __shfl_xor(lsum, 16, WAVE);
+    lsum += __shfl_xor(lsum, 32, WAVE);
+    l_run = l_run * alpha + lsum;
+    m_run = m_new;
+    // o[nn][i] holds column 4 g4 + i: its rescale factor lives in lane 4 g4 + i (g4 = 0 there, li = the column)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float ai = __shfl(alpha, 4 * g4 + i, WAVE);
+#pragma unroll
+      for (int nn = 0; nn < D / 16; ++nn) o[nn][i] *= ai;
+    }
+    // O += P . V over the span's two 32-key steps (the attention kernel's key order and V fragments)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      bf16x8 pa;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pa[j] = (__bf16)sacc[2 * st][j];
+        pa[4 + j] = (__bf16)sacc[2 * st + 1][j];
+      }
+      const int ra = 32 * st + 4 * g4 + qd, rb = ra + 16;
+#pragma unroll
+      for (int nn = 0; nn < D / 16; ++nn) {
+        const int col = 16 * nn + 4 * pd;
+        const int ch = col >> 3, hb = (col & 7) * 2;
+        const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4_t*)(vb + ra * ROWB + 16 * (ch ^ vswz(ra)) + hb));
+        const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4_t*)(vb + rb * ROWB + 16 * (ch ^ vswz(rb)) + hb));
+        bf16x8 vbf;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          vbf[j] = v0[j];
+          vbf[4 + j] = v1[j];
+        }
+        o[nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vbf, o[nn], 0, 0, 0);
+      }
+    }
+    if (more) store(buf ^ 1, kr, vr);   // (that buffer's last readers passed the previous span's barrier)
+    __syncthreads();                    // next span staged; this one's reads done before it is refilled
+  }
+
+  // ---- partials of this group: column c's (max, sum) from lane c, its P.V row from lanes (c / 4 = g4, c % 4 = i)
+  const int gi = blockIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 4 * g4 + i;
+    const bool ok = __shfl((int)live, c, WAVE) != 0;
+    if (ok) {
+      const int b = tile * SPT + c / G, h = kvh * G + c % G;
+      float* dst = pre_acc + (((size_t)b * nq + h) * ngm + gi) * D;
+#pragma unroll
+      for (int nn = 0; nn < D / 16; ++nn) dst[16 * nn + li] = o[nn][i];
+    }
+  }
+  if (g4 == 0 && live) {
+    float* dst = pre_ml + (((size_t)bq * nq + hq) * ngm + gi) * 2;
+    dst[0] = m_run;
+    dst[1] = l_run;
+  }
+}
+
 template <int D>
 __global__ void __launch_bounds__(D) decode_merge_kernel(bf16_t* __restrict__ out, const float* __restrict__ part_acc,
                                                          const float* __restrict__ part_ml,
                                                          const int* __restrict__ context_lens, int part, int pmax,
-                                                         int nq, uint8_t* __restrict__ oq, uint8_t* __restrict__ oe) {
+                                                         int nq, uint8_t* __restrict__ oq, uint8_t* __restrict__ oe,
+                                                         const int* __restrict__ cas, const float* __restrict__ pre_acc,
+                                                         const float* __restrict__ pre_ml, int ngm) {
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
-  const int ctx = context_lens[b];
-  if (ctx <= part) return;  // single-partition rows were finished by the attention kernel
+  const int sh = cas != nullptr ? max(0, cas[0]) : 0;
+  const int ctx = context_lens[b] - 64 * sh;   // (cascade: the partitions start after the shared prefix)
+  if (context_lens[b] <= 0 || ctx <= part) return;  // single-partition rows were finished by the attention kernel
   const int np = min(pmax, (ctx + part - 1) / part);
   const size_t base = ((size_t)b * nq + h) * pmax;
+  const int npre = cascade_groups(sh, ngm);
   float M = -INFINITY;
   for (int q = 0; q < np; ++q) M = fmaxf(M, part_ml[(base + q) * 2]);
   float num = 0.f, den = 0.f;
@@ -350,6 +624,7 @@ __global__ void __launch_bounds__(D) decode_merge_kernel(bf16_t* __restrict__ ou
     num += w * part_acc[(base + q) * D + d];
     den += w * part_ml[(base + q) * 2 + 1];
   }
+  if (npre > 0) cascade_fold(pre_acc, pre_ml, ((size_t)b * nq + h) * ngm, npre, d, M, num, den);
   if (oq != nullptr) mx_store_lane(oq, oe, b, h * D + d, nq * D, gridDim.y, bf_round(num / den));
   else out[((size_t)b * nq + h) * D + d] = f2bf(num / den);
 }
@@ -366,23 +641,27 @@ K8S_CHECK_UNIT(attn_decode_fused)
 // workgroups would run in two rounds).  pmax = ceil(max context / part).
 // oq / oe (optional): the output as MX e4m3 [B][nq * D] + E8M0 scales (common.h mx_scale_off layout) (K16: the fp8 O projection's input
 // quantized by its producer) instead of bf16.
+// cas / pre_acc / pre_ml / ngm (optional, all or none): the cascade inputs -- k8s_decode_prefix ran on the same
+// stream first; the rows' first 64 * cas[0] tokens are skipped here and that kernel's partials merged instead.
 extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const void* qkv,
                                           const float* cos_sin, void* k_cache, void* v_cache, const int* block_tables,
                                           const int* context_lens, float scale, int B, int nq, int nkv, int D,
                                           int block_size, int max_blocks, int pmax, int part, void* oq, void* oe,
+                                          const int* cas, const float* pre_acc, const float* pre_ml, int ngm,
                                           hipStream_t stream) {
   if (B <= 0) return 0;
   if (D != 128 || nq % nkv != 0) return -1;
   if (block_size != 16) return -4;  // the speculative K loads assume one 16-token block per tile
   if (pmax > 1 && (part_acc == nullptr || part_ml == nullptr)) return -3;
   if (part != 1024 && part != 512) return -5;
+  if (cas != nullptr && (pre_acc == nullptr || pre_ml == nullptr || ngm < 1 || ngm > CASCADE_MAX_GROUPS)) return -6;
   const int G = nq / nkv;
   dim3 grid(pmax, nkv, B);
 #define L(GG, PP, WW)                                                                                       \
   decode_fused_kernel<128, GG, PP, WW><<<grid, WW * 64, 0, stream>>>(                                        \
       (bf16_t*)out, (float*)part_acc, (float*)part_ml, (const bf16_t*)qkv, cos_sin, (bf16_t*)k_cache,       \
       (bf16_t*)v_cache, block_tables, context_lens, scale, block_size, max_blocks, nkv, pmax, (uint8_t*)oq,   \
-      (uint8_t*)oe)
+      (uint8_t*)oe, cas, pre_acc, pre_ml, ngm)
 #define LG(PP, WW)                 \
   switch (G) {                     \
     case 1: L(1, PP, WW); break;   \
@@ -402,6 +681,42 @@ extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_
   if (pmax > 1)
     decode_merge_kernel<128><<<dim3(nq, B), 128, 0, stream>>>((bf16_t*)out, (const float*)part_acc,
                                                               (const float*)part_ml, context_lens, part, pmax, nq,
-                                                              (uint8_t*)oq, (uint8_t*)oe);
+                                                              (uint8_t*)oq, (uint8_t*)oe, cas, pre_acc, pre_ml, ngm);
+  return (int)hipGetLastError();
+}
+
+// Workgroups of k8s_decode_prefix along the query columns: 8 waves x 16 (row, head) columns each.
+extern "C" int k8s_decode_prefix_col_blocks(int B, int nq, int nkv) {
+  if (nkv <= 0 || nq % nkv != 0 || 16 % (nq / nkv) != 0) return -1;
+  const int spt = 16 / (nq / nkv);
+  return (B + 8 * spt - 1) / (8 * spt);
+}
+
+// Cascade part 1 (decode_prefix_kernel): the batch's shared prefix (cas = {spans, reference row}, device ints the
+// host writes before the step) attended once for every row; grid (ngm, nkv, column blocks).  The rows' partials go
+// to pre_acc [B, nq, ngm, D] / pre_ml [B, nq, ngm, 2]; k8s_decode_attention_fused with the same cas merges them.
+extern "C" int k8s_decode_prefix(void* pre_acc, void* pre_ml, const void* qkv, const float* cos_sin, const void* k_cache,
+                                 const void* v_cache, const int* block_tables, const int* context_lens, const int* cas,
+                                 float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int ngm,
+                                 hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (D != 128 || block_size != 16 || ngm < 1 || ngm > CASCADE_MAX_GROUPS) return -1;
+  if (pre_acc == nullptr || pre_ml == nullptr || cas == nullptr) return -3;
+  const int cb = k8s_decode_prefix_col_blocks(B, nq, nkv);
+  if (cb < 1) return -2;
+  const dim3 grid(ngm, nkv, cb);
+#define LP(GG)                                                                                                   \
+  decode_prefix_kernel<GG><<<grid, 512, 0, stream>>>((float*)pre_acc, (float*)pre_ml, (const bf16_t*)qkv, cos_sin, \
+                                                     (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,   \
+                                                     context_lens, cas, scale, B, nkv, max_blocks, ngm)
+  switch (nq / nkv) {
+    case 1: LP(1); break;
+    case 2: LP(2); break;
+    case 4: LP(4); break;
+    case 8: LP(8); break;
+    case 16: LP(16); break;
+    default: return -2;
+  }
+#undef LP
   return (int)hipGetLastError();
 }

@@ -165,7 +165,16 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
         self.requests: Dict[int, Request] = {}
         self.free_slots = list(range(max_batch - 1, -1, -1))
         self.use_graphs = cuda_graphs and self.gpu
-        self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}   # (batch bucket, context class, nucleus)
+        self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}   # (batch bucket, context class, nucleus, cascade)
+        # cascade decode attention (ops.decode_attention_fused): a chunk whose running rows share a prefix of at least
+        # K8S_DECODE_CASCADE_MIN tokens (batched decisions on one cluster snapshot with the cluster-first prompt
+        # layout) attends it once for every row instead of once per row; K8S_DECODE_CASCADE=0 turns it off
+        m = model
+        self.cascade = (self.gpu and os.environ.get("K8S_DECODE_CASCADE", "1") != "0" and max_batch >= 2
+                        and ops.cascade_ok(getattr(m, "nq", 0), getattr(m, "nkv", 0), block_size, getattr(m, "D", 0)))
+        self.cascade_min = max(64, int(os.environ.get("K8S_DECODE_CASCADE_MIN", "512")))
+        self._cas_key: Optional[tuple] = None
+        self._cas_val = (0, 0)
         self.prefill_graphs: Dict[int, tuple] = {}             # token bucket -> (graph, logits)
         self._graph_pool = None
         self.lock = threading.RLock()
@@ -187,7 +196,7 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
                       "graph_replays": 0, "prefill_graph_replays": 0, "prefill_overlap_chunks": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "spec_steps": 0, "spec_graph_replays": 0, "spec_drafted": 0,
                       "spec_accepted": 0, "stalls": 0, "mixed_steps": 0, "mixed_decode_rows": 0,
-                      "early_chunk_stops": 0}
+                      "early_chunk_stops": 0, "cascade_chunks": 0}
 
     def _dev(self, x, dtype=torch.int32) -> torch.Tensor:
         """Host data -> the engine's device without ever blocking the host.  A copy from pageable memory waits for
@@ -213,6 +222,7 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
         self.s_seeds = torch.zeros(B, **i32)
         self.s_steps = torch.zeros(B, **i32)
         self.s_hist = torch.zeros(B, self.max_new_cap, **i32)
+        self.s_cas = torch.zeros(2, **i32)   # cascade: (shared 64-token spans, a slot holding them)
         # prefill-graph inputs, one packed buffer filled by one host->device copy per chunk:
         # [ids | positions | slots] x Tmax, then cu_q (2), context_lens (1), last_idx (1), then the two
         # micro-batch halves' cu_q / context_lens (_P_SPLIT)
@@ -245,6 +255,21 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
         return {"cls": self.stop_cls, "json": self.s_json, "cfg": self.s_cfg, "forced": self.s_forced,
                 "forced_len": self.s_forced_len, "eos_tok": self.tok.eot_id,
                 "done": self._done_ptr if self.gpu else self._done_cpu}
+
+    def _shared_prefix(self) -> tuple:
+        """(64-token spans every running row shares, a slot holding them): the running rows' longest common block-list
+        prefix, cut at the earliest prompt end (a row's new token always lies past its prompt, so the shared spans
+        never reach one).  Recomputed only when the running set changes (the blocks of a request never do)."""
+        rs = sorted(self.running.values(), key=lambda r: r.slot)
+        key = tuple((r.slot, r.rid) for r in rs)
+        if key != self._cas_key:
+            first = rs[0].blocks
+            n = min(min(len(r.blocks) for r in rs), min(len(r.prompt_ids) for r in rs) // self.block_size)
+            lcp = 0
+            while lcp < n and all(r.blocks[lcp] == first[lcp] for r in rs[1:]):
+                lcp += 1
+            self._cas_key, self._cas_val = key, ((lcp * self.block_size) // 64, rs[0].slot)
+        return self._cas_val
 
     def _ctx_classes(self) -> List[int]:
         """Context-length classes with their own decode graph: contexts <= 1024 tokens (one
@@ -581,8 +606,18 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
         top = max(len(r.prompt_ids) + max(len(r.output_ids), 1) for r in self.running.values()) + steps
         mc = next(c for c in self._ctx_classes() if top <= c)
         nuc = self._wants_nucleus(self.running.values())
+        cas = False
+        if self.cascade and not nuc and len(self.running) >= 2:
+            sh, r0 = self._shared_prefix()
+            if sh * 64 >= self.cascade_min:
+                cas = True
+                self.s_cas.copy_(self._dev([sh, r0]))
+                self.stats["cascade_chunks"] += 1
+                # the per-row attention covers only the tokens past the shared prefix: its context class (partition
+                # count) follows the longest suffix
+                mc = next(c for c in self._ctx_classes() if top - 64 * sh <= c)
         t0 = time.perf_counter()
-        graph = self.graphs.get((B, mc, nuc)) if self.use_graphs else None
+        graph = self.graphs.get((B, mc, nuc, cas)) if self.use_graphs else None
         # device-side stop detection: the sampler sets a host-mapped done flag when an answer ends (EOS, closed
         # JSON object, max_tokens, end of a scripted answer), so the chunk ends after the replay that finished a
         # request instead of running its remaining replays.  The flags are read after a wait for the replay that
@@ -615,7 +650,7 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
                 graph.replay()
                 self.stats["graph_replays"] += 1
             else:
-                self._decode_step(B, mc, nuc)
+                self._decode_step(B, mc, nuc, cas)
             ran += 1
             if tr is not None:
                 tr.append((time.monotonic(), f"decode: replay {i} enqueued"))

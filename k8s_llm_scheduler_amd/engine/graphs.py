@@ -26,9 +26,12 @@ def logits_exchange_bytes(model, rows: int) -> int:
 class GraphCaptureMixin:
     """Decode / prefill / verify graph capture and the static state the graphs read."""
 
-    def _decode_step(self, B: int, max_context: Optional[int] = None, nucleus: bool = False) -> None:
-        logits = self.model.forward_decode(self.s_tokens[:B], self.s_ctx[:B], self.s_bt[:B],
-                                           max_context or self.max_model_len)
+    def _decode_step(self, B: int, max_context: Optional[int] = None, nucleus: bool = False,
+                     cascade: bool = False) -> None:
+        m = self.model
+        kw = {"cascade": (self.s_cas, ops.cascade_groups_max(B, m.nq, m.nkv))} if cascade else {}
+        logits = m.forward_decode(self.s_tokens[:B], self.s_ctx[:B], self.s_bt[:B], max_context or self.max_model_len,
+                                  **kw)
         ops.sample(logits, self.s_temp[:B], self.s_top_p[:B], self.s_seeds[:B], self.s_ctx[:B],
                    shards=logits.shape[0], tokens_out=self.s_tokens[:B], ctx_inc=self.s_ctx[:B],
                    hist=self.s_hist[:B], steps=self.s_steps[:B], nucleus=nucleus, stop=self._stop_args(),
@@ -84,20 +87,22 @@ class GraphCaptureMixin:
             if not self._decode_bucket_capturable(B):
                 continue    # decodes eagerly (its collectives do not all fit the graph-capturable transport)
             for mc in self._ctx_classes():
-                for nuc in ((False, True) if nucleus else (False,)):
-                    if (B, mc, nuc) in self.graphs:
+                # (cascade variants: batches of >= 2 rows without top-p passes; a top-p chunk decodes per row)
+                for nuc, cas in [(n, c) for n in ((False, True) if nucleus else (False,))
+                                 for c in ((False, True) if self.cascade and B >= 2 and not n else (False,))]:
+                    if (B, mc, nuc, cas) in self.graphs:
                         continue
                     stream.wait_stream(torch.cuda.current_stream(self.device))
                     with torch.cuda.stream(stream):
-                        self._decode_step(B, mc, nuc)   # warm-up: allocator + lazy init outside capture
+                        self._decode_step(B, mc, nuc, cas)   # warm-up: allocator + lazy init outside capture
                     torch.cuda.current_stream(self.device).wait_stream(stream)
                     torch.cuda.synchronize(self.device)
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=self._graph_pool, stream=stream):
-                        self._decode_step(B, mc, nuc)
+                        self._decode_step(B, mc, nuc, cas)
                     if self._graph_pool is None:
                         self._graph_pool = g.pool()
-                    self.graphs[(B, mc, nuc)] = g
+                    self.graphs[(B, mc, nuc, cas)] = g
         if self.prefill_graphs_enabled():
             for Tb in PREFILL_GRAPH_BUCKETS:
                 if Tb in self.prefill_graphs or not self._prefill_bucket_capturable(Tb):

@@ -450,12 +450,13 @@ class LlamaModel:
         return self._logits(h.index_select(0, li).contiguous(), res.index_select(0, li).contiguous())
 
     def forward_decode(self, tokens: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
-                       max_context: int) -> torch.Tensor:
-        """One decode step for B sequences (one token each, positions from context_lens)."""
+                       max_context: int, cascade=None) -> torch.Tensor:
+        """One decode step for B sequences (one token each, positions from context_lens).  ``cascade`` = (cas, ngm):
+        the rows' shared prefix is attended once for the batch (ops.decode_attention_fused)."""
         B = tokens.shape[0]
         self.tp.phase = "decode"
         if self.device.type == "cuda" and B <= ops.GEMV_MAX_M and self.fused_decode:
-            return self._forward_decode_fused(tokens, context_lens, block_tables, max_context)
+            return self._forward_decode_fused(tokens, context_lens, block_tables, max_context, cascade)
         kv = self.kv_cache
         fused_attn = self.device.type == "cuda" and self.fused_decode   # batched decode (B > 8)
         # fp8 GEMM rows: the attention kernel writes the O projection's input as MX e4m3 (K16)
@@ -465,7 +466,7 @@ class LlamaModel:
             if fused_attn:
                 return ops.decode_attention_fused(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
                                                   self.scale, self.block_size, max_context, self.nq, self.nkv, self.D,
-                                                  mx=mx)
+                                                  mx=mx, cascade=cascade)
             q = ops.rope_kv_write(qkv, self.cos_sin, kv[l, 0], kv[l, 1], self.nq, self.nkv, self.D,
                                   context_lens=context_lens, block_tables=block_tables, block_size=self.block_size)
             a = ops.paged_decode_attention(q, kv[l, 0], kv[l, 1], block_tables, context_lens, self.scale,
@@ -511,14 +512,14 @@ class LlamaModel:
             torch.cuda.current_stream(self.device).wait_stream(self._pf_stream)
 
     def _forward_decode_fused(self, tokens: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
-                              max_context: int) -> torch.Tensor:
+                              max_context: int, cascade=None) -> torch.Tensor:
         """Decode step with 5 kernels per layer: [norm+QKV GEMV] -> [RoPE+KV write+attention] ->
         [O GEMV] -> all-reduce -> [norm+gate/up GEMV+SwiGLU] -> [down GEMV] -> all-reduce.
         The residual stream ping-pongs between two buffers (a norm-GEMV reads one, writes the other)."""
         c, kv = self.cfg, self.kv_cache
         h = ops.embedding(tokens, self.embed)
         if self.tp.world > 1:
-            return self._forward_decode_fused_tp(h, context_lens, block_tables, max_context)
+            return self._forward_decode_fused_tp(h, context_lens, block_tables, max_context, cascade)
         res_a = torch.empty_like(h)
         res_b = torch.empty_like(h)
         res_in = None
@@ -528,7 +529,8 @@ class LlamaModel:
             if pf:
                 self._pf_layer(w, pf)
             a = ops.decode_attention_fused(qkv, self.cos_sin, kv[w_l, 0], kv[w_l, 1], block_tables, context_lens,
-                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
+                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D,
+                                           cascade=cascade)
             o = ops.linear(a, w.wo)
             self.tp.all_reduce_(o)
             g = ops.linear_norm(o, w.wgu, None if self.norm_folded else w.ln2, c.rms_eps, res_b, res_a,
@@ -543,7 +545,7 @@ class LlamaModel:
         return self._gather(logits)
 
     def _forward_decode_fused_tp(self, h: torch.Tensor, context_lens: torch.Tensor, block_tables: torch.Tensor,
-                                 max_context: int) -> torch.Tensor:
+                                 max_context: int, cascade=None) -> torch.Tensor:
         """TP > 1 decode: the residual add rides on the all-reduce (xGMI kernels add it before their
         single rounding: SURVEY K14 + K2), so the residual stream IS the all-reduce outputs and the
         norm-GEMV prologues read one tensor (no residual read, no residual write)."""
@@ -558,7 +560,8 @@ class LlamaModel:
             if pf:
                 self._pf_layer(w, pf)
             a = ops.decode_attention_fused(qkv, self.cos_sin, kv[l, 0], kv[l, 1], block_tables, context_lens,
-                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D)
+                                           self.scale, self.block_size, max_context, self.nq, self.nkv, self.D,
+                                           cascade=cascade)
             o = self.tp.linear_all_reduce(a, w.wo, residual=x)   # o = x + attention branch (AR in the GEMV)
             g = ops.linear_norm(o, w.wgu, g2(w) if g2 else None, c.rms_eps, None, None, epi=ops.EPI_SWIGLU)
             x = self.tp.linear_all_reduce(g, w.wdown, residual=o)    # x = o + MLP branch

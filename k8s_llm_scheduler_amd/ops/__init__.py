@@ -1184,13 +1184,45 @@ def linear_norm(x: torch.Tensor, w, norm_w: Optional[torch.Tensor], eps: float,
                  folded=norm_w is None)
 
 
+def cascade_groups_max(B: int, nq: int, nkv: int) -> int:
+    """Prefix groups (partials per row and head) of the cascade decode attention at B rows: about 256 workgroups
+    of decode_prefix_kernel over (groups, kv heads, column blocks), 2-32 groups (each group's partial is a row's
+    D + 2 floats per head, so more groups trade prefix-kernel parallelism for partial-sum traffic)."""
+    cb = -(-B // (8 * max(1, 16 // max(1, nq // nkv))))
+    return max(2, min(32, 256 // max(1, nkv * cb)))
+
+
+def cascade_ok(nq: int, nkv: int, block_size: int, D: int) -> bool:
+    """Shapes the cascade (shared-prefix) decode attention takes."""
+    G = nq // nkv if nkv else 0
+    return block_size == 16 and D == 128 and nkv > 0 and nq % nkv == 0 and G in (1, 2, 4, 8, 16)
+
+
 def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                            block_tables: torch.Tensor, context_lens: torch.Tensor, scale: float, block_size: int,
-                           max_context: int, nq: int, nkv: int, D: int, mx: bool = False):
+                           max_context: int, nq: int, nkv: int, D: int, mx: bool = False, cascade=None):
     """RoPE + KV write of the new token + paged GQA attention, one kernel.  Returns [B, nq*D] bf16, or with ``mx``
     an :class:`MxAct` (the fp8 O projection's input: written as MX e4m3 by the one-workgroup kernel and its merge;
-    the other forms quantize their bf16 output)."""
+    the other forms quantize their bf16 output).
+
+    ``cascade`` = (cas, ngm): the batch's shared prefix -- cas a device int32 [2] = (64-token spans every active row
+    shares, a row holding them), written by the engine before the step -- is attended once for all rows by
+    decode_prefix_kernel (ngm partials per row and head) and merged into the per-row attention, whose partitions
+    start after it: ``max_context`` then bounds the tokens PAST the shared prefix (the suffix), not the context.
+    Exact (the same keys, the same softmax); on the CPU the plain per-row attention runs."""
     B = qkv.shape[0]
+    if cascade is not None and _gpu(qkv, k_cache) and cascade_ok(nq, nkv, block_size, D):
+        cas, ngm = cascade
+        if cas.dtype != I32 or cas.numel() < 2 or not cas.is_cuda:
+            raise ValueError("cascade: cas must be a device int32 tensor of 2 values")
+        pre_acc = torch.empty(B * nq * ngm * D, dtype=F32, device=qkv.device)
+        pre_ml = torch.empty(B * nq * ngm * 2, dtype=F32, device=qkv.device)
+        native().decode_prefix(pre_acc.data_ptr(), pre_ml.data_ptr(), _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"),
+                               _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
+                               _chk(block_tables, I32, "block_tables"), _chk(context_lens, I32, "context_lens"),
+                               cas.data_ptr(), float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], ngm, -1)
+        return _decode_attention_onewg(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
+                                       max_context, nq, nkv, D, mx, (cas.data_ptr(), pre_acc, pre_ml, ngm))
     if mx:
         if not _gpu(qkv, k_cache) or block_size != 16 or (B * nkv <= _split_pairs_limit(max_context)
                                                           and max_context <= 64 * SPLIT_PARTITION):
@@ -1209,6 +1241,15 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
     if B * nkv <= _split_pairs_limit(max_context) and max_context <= 64 * SPLIT_PARTITION:
         return _decode_attention_split(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
                                        max_context, nq, nkv, D)
+    return _decode_attention_onewg(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
+                                   max_context, nq, nkv, D, mx, None)
+
+
+def _decode_attention_onewg(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
+                            max_context, nq, nkv, D, mx, cascade):
+    """The one-workgroup-per-(row, kv head, partition) kernel (+ its merge); ``cascade`` = (cas pointer, pre_acc,
+    pre_ml, ngm) of a decode_prefix_kernel launch that ran first."""
+    B = qkv.shape[0]
     part = fused_partition(B * nkv)
     pmax = max(1, math.ceil(max_context / part))
     mxo = MxAct.empty(B, nq * D, qkv.device) if mx else None
@@ -1223,7 +1264,9 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
                                     _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
                                     _chk(block_tables, I32, "block_tables"), _chk(context_lens, I32, "context_lens"),
                                     float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], pmax, part, -1,
-                                    mxo.q.data_ptr() if mx else 0, mxo.e.data_ptr() if mx else 0)
+                                    mxo.q.data_ptr() if mx else 0, mxo.e.data_ptr() if mx else 0,
+                                    *((cascade[0], cascade[1].data_ptr(), cascade[2].data_ptr(), cascade[3])
+                                      if cascade is not None else (0, 0, 0, 0)))
     return mxo if mx else out
 
 

@@ -84,7 +84,7 @@ def _rank_70b(rank, world):
     eng.capture_graphs([1, 64])
     # the transport of every all-reduce the captured graphs replay (TPGroup.ar_log counts host issues: at capture)
     res["capture_transports"] = dict(tp.ar_log)
-    res["graphs"] = sorted({b for b, _, _ in eng.graphs})
+    res["graphs"] = sorted({k[0] for k in eng.graphs})
     res["prefill_graphs"] = sorted(eng.prefill_graphs)
     greedy = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
     tp.ar_log.clear()
