@@ -30,6 +30,7 @@ decoding), ``serving.py`` (background loop, blocking ``generate``); shared types
 
 from __future__ import annotations
 
+import inspect
 import itertools
 import math
 import os
@@ -171,7 +172,8 @@ class LLMEngine(GraphCaptureMixin, RecoveryMixin, SpeculativeMixin, ServingMixin
         # layout) attends it once for every row instead of once per row; K8S_DECODE_CASCADE=0 turns it off
         m = model
         self.cascade = (self.gpu and os.environ.get("K8S_DECODE_CASCADE", "1") != "0" and max_batch >= 2
-                        and ops.cascade_ok(getattr(m, "nq", 0), getattr(m, "nkv", 0), block_size, getattr(m, "D", 0)))
+                        and ops.cascade_ok(getattr(m, "nq", 0), getattr(m, "nkv", 0), block_size, getattr(m, "D", 0))
+                        and "cascade" in inspect.signature(m.forward_decode).parameters)
         self.cascade_min = max(64, int(os.environ.get("K8S_DECODE_CASCADE_MIN", "512")))
         self._cas_key: Optional[tuple] = None
         self._cas_val = (0, 0)
