@@ -64,10 +64,10 @@ int k8s_gemv_norm(void* out, void* partial, const void* x, const void* W, int M,
 int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const void* qkv, const float* cos_sin,
                                void* k_cache, void* v_cache, const int* block_tables, const int* context_lens,
                                float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int pmax, int part,
-                               void* oq, void* oe, const int* cas, const float* pre_acc, const float* pre_ml, int ngm,
+                               void* oq, void* oe, const int* cas, const float* pre, int ngm, int rec_stride,
                                hipStream_t s);
 int k8s_decode_prefix_col_blocks(int B, int nq, int nkv);
-int k8s_decode_prefix(void* pre_acc, void* pre_ml, const void* qkv, const float* cos_sin, const void* k_cache,
+int k8s_decode_prefix(void* pre, int rec_stride, const void* qkv, const float* cos_sin, const void* k_cache,
                       const void* v_cache, const int* block_tables, const int* context_lens, const int* cas, float scale,
                       int B, int nq, int nkv, int D, int block_size, int max_blocks, int ngm, hipStream_t s);
 long long k8s_decode_split_workspace(int B, int nq, int nkv, int pmax);
@@ -253,22 +253,21 @@ PYBIND11_MODULE(K8S_MODULE_NAME, m) {
   m.def("decode_attention_fused", [](uintptr_t out, uintptr_t pacc, uintptr_t pml, uintptr_t qkv, uintptr_t cos_sin,
                                      uintptr_t kc, uintptr_t vc, uintptr_t bt, uintptr_t ctx, float scale, int B, int nq,
                                      int nkv, int D, int bs, int max_blocks, int pmax, int part, int64_t s,
-                                     uintptr_t oq, uintptr_t oe, uintptr_t cas, uintptr_t pre_acc, uintptr_t pre_ml,
-                                     int ngm) {
+                                     uintptr_t oq, uintptr_t oe, uintptr_t cas, uintptr_t pre, int ngm, int rec_stride) {
     check(k8s_decode_attention_fused(P(out), P(pacc), P(pml), P(qkv), P<float>(cos_sin), P(kc), P(vc), P<int>(bt),
                                      P<int>(ctx), scale, B, nq, nkv, D, bs, max_blocks, pmax, part, P(oq), P(oe),
-                                     P<int>(cas), P<float>(pre_acc), P<float>(pre_ml), ngm, S(s)),
+                                     P<int>(cas), P<float>(pre), ngm, rec_stride, S(s)),
           "decode_attention_fused");
   }, py::arg("out"), py::arg("pacc"), py::arg("pml"), py::arg("qkv"), py::arg("cos_sin"), py::arg("kc"),
      py::arg("vc"), py::arg("bt"), py::arg("ctx"), py::arg("scale"), py::arg("B"), py::arg("nq"), py::arg("nkv"),
      py::arg("D"), py::arg("bs"), py::arg("max_blocks"), py::arg("pmax"), py::arg("part"), py::arg("s"),
-     py::arg("oq") = 0, py::arg("oe") = 0, py::arg("cas") = 0, py::arg("pre_acc") = 0, py::arg("pre_ml") = 0,
-     py::arg("ngm") = 0);
+     py::arg("oq") = 0, py::arg("oe") = 0, py::arg("cas") = 0, py::arg("pre") = 0, py::arg("ngm") = 0,
+     py::arg("rec_stride") = 0);
   m.def("decode_prefix_col_blocks", [](int B, int nq, int nkv) { return k8s_decode_prefix_col_blocks(B, nq, nkv); });
-  m.def("decode_prefix", [](uintptr_t pre_acc, uintptr_t pre_ml, uintptr_t qkv, uintptr_t cos_sin, uintptr_t kc,
+  m.def("decode_prefix", [](uintptr_t pre, int rec_stride, uintptr_t qkv, uintptr_t cos_sin, uintptr_t kc,
                             uintptr_t vc, uintptr_t bt, uintptr_t ctx, uintptr_t cas, float scale, int B, int nq, int nkv,
                             int D, int bs, int max_blocks, int ngm, int64_t s) {
-    check(k8s_decode_prefix(P(pre_acc), P(pre_ml), P(qkv), P<float>(cos_sin), P(kc), P(vc), P<int>(bt), P<int>(ctx),
+    check(k8s_decode_prefix(P(pre), rec_stride, P(qkv), P<float>(cos_sin), P(kc), P(vc), P<int>(bt), P<int>(ctx),
                             P<int>(cas), scale, B, nq, nkv, D, bs, max_blocks, ngm, S(s)),
           "decode_prefix");
   });

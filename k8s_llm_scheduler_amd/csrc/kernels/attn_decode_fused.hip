@@ -41,18 +41,21 @@ __device__ __forceinline__ int cascade_groups(int sh, int ngm) {
   const int spg = (sh + ngm - 1) / ngm;
   return (sh + spg - 1) / spg;
 }
-// Fold the npre prefix partials of one (row, head) into (M, num, den) at element d: every load issued up front
+// Prefix partial records share attn_decode_split.hip's layout: per (row, kv head) "pair", rec_stride records of
+// G * D + 2 G floats (the G heads' unnormalised P.V, then their maxima, then their sums); group k is record k.
+// Fold the npre records of one (pair, head g) into (M, num, den) at element d: every load issued up front
 // (unconditional, clamped to the last live group -- a loop of dependent waits would cost one round trip per group).
-__device__ __forceinline__ void cascade_fold(const float* __restrict__ pre_acc, const float* __restrict__ pre_ml,
-                                             size_t pb, int npre, int d, float& M, float& num, float& den) {
+__device__ __forceinline__ void cascade_fold(const float* __restrict__ pre, size_t rec0, int G, int g, int npre, int d,
+                                             float& M, float& num, float& den) {
   constexpr int D = 128;
+  const size_t ps = (size_t)G * D + 2 * G;
   float pm[CASCADE_MAX_GROUPS], pl[CASCADE_MAX_GROUPS], pa[CASCADE_MAX_GROUPS];
 #pragma unroll
   for (int k = 0; k < CASCADE_MAX_GROUPS; ++k) {
-    const size_t kk = pb + (size_t)min(k, npre - 1);
-    pm[k] = pre_ml[kk * 2];
-    pl[k] = pre_ml[kk * 2 + 1];
-    pa[k] = pre_acc[kk * D + d];
+    const float* r = pre + (rec0 + (size_t)min(k, npre - 1)) * ps;
+    pa[k] = r[g * D + d];
+    pm[k] = r[G * D + g];
+    pl[k] = r[G * D + G + g];
   }
   float Mt = M;
 #pragma unroll
@@ -78,7 +81,7 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
     const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ context_lens, float scale, int block_size,
     int max_blocks, int nkv, int pmax, uint8_t* __restrict__ oq, uint8_t* __restrict__ oe,
-    const int* __restrict__ cas, const float* __restrict__ pre_acc, const float* __restrict__ pre_ml, int ngm) {
+    const int* __restrict__ cas, const float* __restrict__ pre, int ngm, int rec_stride) {
   static_assert(D == 128 && G <= 16, "head_dim 128, group <= 16");
   static_assert(PART / NW == 64, "64 tokens per wave");
   constexpr int NT = NW * WAVE;
@@ -369,7 +372,7 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
         float Mw = -INFINITY;
 #pragma unroll
         for (int w = 0; w < NW; ++w) Mw = fmaxf(Mw, wm[w][g]);
-        cascade_fold(pre_acc, pre_ml, ((size_t)b * nq + h) * ngm, npre, d, Mw, num, den);
+        cascade_fold(pre, ((size_t)b * nkv + kvh) * rec_stride, G, g, npre, d, Mw, num, den);
       }
       if (oq != nullptr) {   // MX output: the 32 lanes of (head, d / 32) form one half-wave (NT, D: multiples of 32)
         mx_store_lane(oq, oe, b, h * D + d, nq * D, gridDim.z, bf_round(num / den));
@@ -402,10 +405,11 @@ __global__ void __launch_bounds__(NW * 64) decode_fused_kernel(
 //    convention, so the partials merge with its own (decode_fused_kernel / decode_merge_kernel above);
 //  * q is rotated here (RoPE at each row's own position) from the pre-RoPE QKV rows.
 // cas = {sh, r0}: sh spans shared by every active row (the host's longest common block-table prefix, never reaching a
-// row's new token), read from row r0's block table.  Partials: pre_acc [B, nq, ngm, D], pre_ml [B, nq, ngm, 2].
+// row's new token), read from row r0's block table.  Partials: record k of pair (row, kv head) in the split
+// layout above (cascade_fold), rec_stride records per pair.
 template <int G>
 __global__ void __launch_bounds__(512) decode_prefix_kernel(
-    float* __restrict__ pre_acc, float* __restrict__ pre_ml, const bf16_t* __restrict__ qkv,
+    float* __restrict__ pre, int rec_stride, const bf16_t* __restrict__ qkv,
     const float* __restrict__ cos_sin, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ context_lens, const int* __restrict__ cas,
     float scale, int B, int nkv, int max_blocks, int ngm) {
@@ -584,21 +588,22 @@ __global__ void __launch_bounds__(512) decode_prefix_kernel(
 
   // ---- partials of this group: column c's (max, sum) from lane c, its P.V row from lanes (c / 4 = g4, c % 4 = i)
   const int gi = blockIdx.x;
+  constexpr int PS = G * D + 2 * G;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = 4 * g4 + i;
     const bool ok = __shfl((int)live, c, WAVE) != 0;
     if (ok) {
-      const int b = tile * SPT + c / G, h = kvh * G + c % G;
-      float* dst = pre_acc + (((size_t)b * nq + h) * ngm + gi) * D;
+      const int b = tile * SPT + c / G;
+      float* dst = pre + (((size_t)b * nkv + kvh) * rec_stride + gi) * PS + (c % G) * D;
 #pragma unroll
       for (int nn = 0; nn < D / 16; ++nn) dst[16 * nn + li] = o[nn][i];
     }
   }
   if (g4 == 0 && live) {
-    float* dst = pre_ml + (((size_t)bq * nq + hq) * ngm + gi) * 2;
+    float* dst = pre + (((size_t)bq * nkv + kvh) * rec_stride + gi) * PS + G * D + li % G;
     dst[0] = m_run;
-    dst[1] = l_run;
+    dst[G] = l_run;
   }
 }
 
@@ -607,8 +612,8 @@ __global__ void __launch_bounds__(D) decode_merge_kernel(bf16_t* __restrict__ ou
                                                          const float* __restrict__ part_ml,
                                                          const int* __restrict__ context_lens, int part, int pmax,
                                                          int nq, uint8_t* __restrict__ oq, uint8_t* __restrict__ oe,
-                                                         const int* __restrict__ cas, const float* __restrict__ pre_acc,
-                                                         const float* __restrict__ pre_ml, int ngm) {
+                                                         const int* __restrict__ cas, const float* __restrict__ pre,
+                                                         int ngm, int rec_stride, int G) {
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int sh = cas != nullptr ? max(0, cas[0]) : 0;
   const int ctx = context_lens[b] - 64 * sh;   // (cascade: the partitions start after the shared prefix)
@@ -624,7 +629,7 @@ __global__ void __launch_bounds__(D) decode_merge_kernel(bf16_t* __restrict__ ou
     num += w * part_acc[(base + q) * D + d];
     den += w * part_ml[(base + q) * 2 + 1];
   }
-  if (npre > 0) cascade_fold(pre_acc, pre_ml, ((size_t)b * nq + h) * ngm, npre, d, M, num, den);
+  if (npre > 0) cascade_fold(pre, ((size_t)b * (nq / G) + h / G) * rec_stride, G, h % G, npre, d, M, num, den);
   if (oq != nullptr) mx_store_lane(oq, oe, b, h * D + d, nq * D, gridDim.y, bf_round(num / den));
   else out[((size_t)b * nq + h) * D + d] = f2bf(num / den);
 }
@@ -641,27 +646,28 @@ K8S_CHECK_UNIT(attn_decode_fused)
 // workgroups would run in two rounds).  pmax = ceil(max context / part).
 // oq / oe (optional): the output as MX e4m3 [B][nq * D] + E8M0 scales (common.h mx_scale_off layout) (K16: the fp8 O projection's input
 // quantized by its producer) instead of bf16.
-// cas / pre_acc / pre_ml / ngm (optional, all or none): the cascade inputs -- k8s_decode_prefix ran on the same
-// stream first; the rows' first 64 * cas[0] tokens are skipped here and that kernel's partials merged instead.
+// cas / pre / ngm / rec_stride (optional, all or none): the cascade inputs -- k8s_decode_prefix ran on the same
+// stream first (records of rec_stride per pair); the rows' first 64 * cas[0] tokens are skipped here and that
+// kernel's partials merged instead.
 extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_ml, const void* qkv,
                                           const float* cos_sin, void* k_cache, void* v_cache, const int* block_tables,
                                           const int* context_lens, float scale, int B, int nq, int nkv, int D,
                                           int block_size, int max_blocks, int pmax, int part, void* oq, void* oe,
-                                          const int* cas, const float* pre_acc, const float* pre_ml, int ngm,
+                                          const int* cas, const float* pre, int ngm, int rec_stride,
                                           hipStream_t stream) {
   if (B <= 0) return 0;
   if (D != 128 || nq % nkv != 0) return -1;
   if (block_size != 16) return -4;  // the speculative K loads assume one 16-token block per tile
   if (pmax > 1 && (part_acc == nullptr || part_ml == nullptr)) return -3;
   if (part != 1024 && part != 512) return -5;
-  if (cas != nullptr && (pre_acc == nullptr || pre_ml == nullptr || ngm < 1 || ngm > CASCADE_MAX_GROUPS)) return -6;
+  if (cas != nullptr && (pre == nullptr || ngm < 1 || ngm > CASCADE_MAX_GROUPS || rec_stride < ngm)) return -6;
   const int G = nq / nkv;
   dim3 grid(pmax, nkv, B);
 #define L(GG, PP, WW)                                                                                       \
   decode_fused_kernel<128, GG, PP, WW><<<grid, WW * 64, 0, stream>>>(                                        \
       (bf16_t*)out, (float*)part_acc, (float*)part_ml, (const bf16_t*)qkv, cos_sin, (bf16_t*)k_cache,       \
       (bf16_t*)v_cache, block_tables, context_lens, scale, block_size, max_blocks, nkv, pmax, (uint8_t*)oq,   \
-      (uint8_t*)oe, cas, pre_acc, pre_ml, ngm)
+      (uint8_t*)oe, cas, pre, ngm, rec_stride)
 #define LG(PP, WW)                 \
   switch (G) {                     \
     case 1: L(1, PP, WW); break;   \
@@ -681,7 +687,8 @@ extern "C" int k8s_decode_attention_fused(void* out, void* part_acc, void* part_
   if (pmax > 1)
     decode_merge_kernel<128><<<dim3(nq, B), 128, 0, stream>>>((bf16_t*)out, (const float*)part_acc,
                                                               (const float*)part_ml, context_lens, part, pmax, nq,
-                                                              (uint8_t*)oq, (uint8_t*)oe, cas, pre_acc, pre_ml, ngm);
+                                                              (uint8_t*)oq, (uint8_t*)oe, cas, pre, ngm, rec_stride,
+                                                              G);
   return (int)hipGetLastError();
 }
 
@@ -693,20 +700,21 @@ extern "C" int k8s_decode_prefix_col_blocks(int B, int nq, int nkv) {
 }
 
 // Cascade part 1 (decode_prefix_kernel): the batch's shared prefix (cas = {spans, reference row}, device ints the
-// host writes before the step) attended once for every row; grid (ngm, nkv, column blocks).  The rows' partials go
-// to pre_acc [B, nq, ngm, D] / pre_ml [B, nq, ngm, 2]; k8s_decode_attention_fused with the same cas merges them.
-extern "C" int k8s_decode_prefix(void* pre_acc, void* pre_ml, const void* qkv, const float* cos_sin, const void* k_cache,
+// host writes before the step) attended once for every row; grid (ngm, nkv, column blocks).  Group k's partial of
+// pair (row, kv head) is record k of rec_stride >= ngm records (attn_decode_split.hip's record layout); the per-row
+// kernel given the same cas (k8s_decode_attention_fused / _split) merges them.
+extern "C" int k8s_decode_prefix(void* pre, int rec_stride, const void* qkv, const float* cos_sin, const void* k_cache,
                                  const void* v_cache, const int* block_tables, const int* context_lens, const int* cas,
                                  float scale, int B, int nq, int nkv, int D, int block_size, int max_blocks, int ngm,
                                  hipStream_t stream) {
   if (B <= 0) return 0;
-  if (D != 128 || block_size != 16 || ngm < 1 || ngm > CASCADE_MAX_GROUPS) return -1;
-  if (pre_acc == nullptr || pre_ml == nullptr || cas == nullptr) return -3;
+  if (D != 128 || block_size != 16 || ngm < 1 || ngm > CASCADE_MAX_GROUPS || rec_stride < ngm) return -1;
+  if (pre == nullptr || cas == nullptr) return -3;
   const int cb = k8s_decode_prefix_col_blocks(B, nq, nkv);
   if (cb < 1) return -2;
   const dim3 grid(ngm, nkv, cb);
 #define LP(GG)                                                                                                   \
-  decode_prefix_kernel<GG><<<grid, 512, 0, stream>>>((float*)pre_acc, (float*)pre_ml, (const bf16_t*)qkv, cos_sin, \
+  decode_prefix_kernel<GG><<<grid, 512, 0, stream>>>((float*)pre, rec_stride, (const bf16_t*)qkv, cos_sin,        \
                                                      (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,   \
                                                      context_lens, cas, scale, B, nkv, max_blocks, ngm)
   switch (nq / nkv) {

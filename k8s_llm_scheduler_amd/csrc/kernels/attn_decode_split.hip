@@ -275,7 +275,9 @@ __device__ __forceinline__ void split_body(
 #pragma unroll
   for (int i = 0; i < 4; ++i) lh[i] = __shfl(l, 4 * g4 + i, WAVE);
   TR(4);
-  const int nlive = (ctx + CH - 1) / CH;
+  // (clamped to the launched chunks: a caller whose max_context is below a row's context gets a wrong row, never a
+  // ticket left armed for the next launch)
+  const int nlive = min(pmax, (ctx + CH - 1) / CH);
   if (nlive == 1) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

@@ -1215,14 +1215,17 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
         cas, ngm = cascade
         if cas.dtype != I32 or cas.numel() < 2 or not cas.is_cuda:
             raise ValueError("cascade: cas must be a device int32 tensor of 2 values")
-        pre_acc = torch.empty(B * nq * ngm * D, dtype=F32, device=qkv.device)
-        pre_ml = torch.empty(B * nq * ngm * 2, dtype=F32, device=qkv.device)
-        native().decode_prefix(pre_acc.data_ptr(), pre_ml.data_ptr(), _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"),
+        G = nq // nkv
+        ps = G * D + 2 * G                      # floats per partial record (attn_decode_split.hip's layout)
+        part = torch.empty(B * nkv * ngm * ps, dtype=F32, device=qkv.device)
+        native().decode_prefix(part.data_ptr(), ngm, _chk(qkv, BF16, "qkv"), _chk(cos_sin, F32, "cos_sin"),
                                _chk(k_cache, BF16, "k_cache"), _chk(v_cache, BF16, "v_cache"),
                                _chk(block_tables, I32, "block_tables"), _chk(context_lens, I32, "context_lens"),
                                cas.data_ptr(), float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], ngm, -1)
+        # (the suffix on the one-wave-per-chunk split kernel, its last arriver merging the prefix records as well,
+        # measured 1.7-3.6x slower: one wave folds every record of a pair -- profiles/cascade_kbench_r6.txt)
         return _decode_attention_onewg(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
-                                       max_context, nq, nkv, D, mx, (cas.data_ptr(), pre_acc, pre_ml, ngm))
+                                       max_context, nq, nkv, D, mx, (cas.data_ptr(), part, ngm, ngm))
     if mx:
         if not _gpu(qkv, k_cache) or block_size != 16 or (B * nkv <= _split_pairs_limit(max_context)
                                                           and max_context <= 64 * SPLIT_PARTITION):
@@ -1247,8 +1250,8 @@ def decode_attention_fused(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: to
 
 def _decode_attention_onewg(qkv, cos_sin, k_cache, v_cache, block_tables, context_lens, scale, block_size,
                             max_context, nq, nkv, D, mx, cascade):
-    """The one-workgroup-per-(row, kv head, partition) kernel (+ its merge); ``cascade`` = (cas pointer, pre_acc,
-    pre_ml, ngm) of a decode_prefix_kernel launch that ran first."""
+    """The one-workgroup-per-(row, kv head, partition) kernel (+ its merge); ``cascade`` = (cas pointer, prefix
+    records, ngm, records per pair) of a decode_prefix_kernel launch that ran first."""
     B = qkv.shape[0]
     part = fused_partition(B * nkv)
     pmax = max(1, math.ceil(max_context / part))
@@ -1265,7 +1268,7 @@ def _decode_attention_onewg(qkv, cos_sin, k_cache, v_cache, block_tables, contex
                                     _chk(block_tables, I32, "block_tables"), _chk(context_lens, I32, "context_lens"),
                                     float(scale), B, nq, nkv, D, block_size, block_tables.shape[1], pmax, part, -1,
                                     mxo.q.data_ptr() if mx else 0, mxo.e.data_ptr() if mx else 0,
-                                    *((cascade[0], cascade[1].data_ptr(), cascade[2].data_ptr(), cascade[3])
+                                    *((cascade[0], cascade[1].data_ptr(), cascade[2], cascade[3])
                                       if cascade is not None else (0, 0, 0, 0)))
     return mxo if mx else out
 

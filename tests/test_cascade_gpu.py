@@ -107,12 +107,15 @@ def test_cascade_mx_output_is_the_quantized_bf16_output(mc):
     assert torch.equal(mx.q, want.q) and torch.equal(mx.e, want.e)
 
 
-def test_cascade_graph_replay_follows_the_shared_length():
-    """The shared length is device state the engine writes before a replay: one graph serves every length."""
-    nq, nkv, B, mc = 64, 8, 16, 4096
+@pytest.mark.parametrize("mc", [1024, 4096])
+def test_cascade_graph_replay_follows_the_shared_length(mc):
+    """The shared length is device state the engine writes before a replay: one graph serves every length (mc 1024:
+    one partition past the prefix, 4096: several and the merge kernel)."""
+    nq, nkv, B = 64, 8, 16
     prefix = 1536
     qkv, cs, kc, vc, bt, ctx = _batch(B, nq, nkv, prefix, [3 + 50 * b for b in range(B)], seed=7)
-    assert int(ctx.max()) <= mc
+    shs = (prefix // 64, 7, 0, 1, prefix // 64) if mc > 1024 else (prefix // 64, 20, 22, prefix // 64)
+    assert int(ctx.max()) - 64 * min(shs) <= mc            # every row's suffix fits max_context
     cas = torch.tensor([prefix // 64, 0], dtype=torch.int32, device=DEV)
     ngm = ops.cascade_groups_max(B, nq, nkv)
     s = torch.cuda.Stream()
@@ -123,8 +126,8 @@ def test_cascade_graph_replay_follows_the_shared_length():
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         out = _run(qkv, cs, kc, vc, bt, ctx, mc, nq, nkv, cascade=(cas, ngm))
-    base = _run(qkv, cs, kc.clone(), vc.clone(), bt, ctx, mc, nq, nkv)
-    for sh in (prefix // 64, 7, 0, 1, prefix // 64):
+    base = _run(qkv, cs, kc.clone(), vc.clone(), bt, ctx, 4096, nq, nkv)
+    for sh in shs:
         cas[0] = sh
         g.replay()
         torch.cuda.synchronize()
