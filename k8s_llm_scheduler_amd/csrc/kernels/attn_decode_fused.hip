@@ -422,9 +422,7 @@ __global__ void __launch_bounds__(512) decode_prefix_kernel(
   const int spg = (sh + ngm - 1) / ngm;
   const int s0 = blockIdx.x * spg, s1 = min(s0 + spg, sh);
   if (s0 >= s1) return;
-  int r0 = cas[1];
-  K8S_CHECK_RANGE(r0, 0, K8S_CHK_SLOT, 0);   // (a host value; checked builds clamp it like any index)
-  r0 = min(max(r0, 0), B - 1);
+  const int r0 = min(max(cas[1], 0), B - 1);   // (a host value, clamped to the launch's rows)
   const int kvh = blockIdx.y, nq = nkv * G;
   const size_t kvs = (size_t)nkv * D;
   const int* bt0 = block_tables + (size_t)r0 * max_blocks;
