@@ -12,15 +12,18 @@
 //  * fp8 (OCP e4m3 x and W, per-token / per-row scales in the epilogue): the same tile and LDS image with
 //    128-value k-tiles on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales), which runs at
 //    twice the bf16 rate -- the non-scaled 16x16x32 fp8 MFMA is only as fast as bf16.
-//  * k-tiles of 128 bytes per row (64 bf16 / 128 e4m3) in two LDS stages of (BP + BQ) x 128 B, each split into
-//    four regions: QB0 / QB1 (the first / second FQ fragments of every wave column) and PA0 / PA1 (the first /
-//    second FP fragments of every wave row).  One k-tile is four phases, each one MFMA quadrant:
+//  * k-tiles of 128 bytes per row (64 bf16 / 128 e4m3), split into four regions: QB0 / QB1 (the first / second FQ
+//    fragments of every wave column) and PA0 / PA1 (the first / second FP fragments of every wave row).  The x
+//    regions live in a two-stage LDS ring, the weight regions in a WS-stage ring (WS = 2, or 3-4 where the 160 KiB
+//    hold it: more weight bytes in flight per CU for the weight-streaming row counts).  One k-tile is four
+//    phases, each one MFMA quadrant:
 //        phase 0: read QB0 + PA0, MFMA (a0, b0)        phase 2: read PA1, MFMA (a1, b1)
 //        phase 1: read QB1,        MFMA (a0, b1)        phase 3: (registers only) MFMA (a1, b0)
-//    and every phase refills ONE region with LDS-DMA (global_load_lds_dwordx4), the phase after its last
-//    reader: PA1 of k-tile t+1 in phase 0, QB0 / PA0 / QB1 of k-tile t+2 in phases 1 / 2 / 3.  Five regions
-//    (~80 KB at 256 x 256) stay in flight across the raw s_barriers; each wait is a counted `s_waitcnt vmcnt`
-//    one phase before the first reader (never vmcnt(0) in the steady state).
+//    and every phase refills ONE region with LDS-DMA (global_load_lds_dwordx4), at least one phase after its
+//    last reader: PA1 of k-tile t+WS-1 in phase 0, QB0 of t+2 in phase 1, PA0 of t+WS in phase 2, QB1 of t+2 in
+//    phase 3.  Five regions (~80 KB at 256 x 256, WS = 2) to nine (WS = 3) stay in flight across the raw
+//    s_barriers; each wait is a counted `s_waitcnt vmcnt` one phase before the first reader (never vmcnt(0) in
+//    the steady state; pg_window counts the sequence).
 //  * waves 4-7 run one barrier behind waves 0-3 (two barriers per phase): on every SIMD one wave is in its
 //    MFMA section while its partner reads LDS and issues the next DMA (8-wave ping-pong).  Every LDS read is
 //    retired (lgkmcnt(0)) before the phase's first barrier, which is what makes the one-phase refill legal for
@@ -61,25 +64,18 @@ template <int N>
 __device__ __forceinline__ void pg_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-// wave-uniform count -> immediate (the tail k-tiles; the steady state uses constants)
-__device__ __forceinline__ void pg_vm_wait(int n) {
-  switch (n) {
-    case 1: pg_vmcnt<1>(); break;
-    case 2: pg_vmcnt<2>(); break;
-    case 3: pg_vmcnt<3>(); break;
-    case 4: pg_vmcnt<4>(); break;
-    case 5: pg_vmcnt<5>(); break;
-    case 6: pg_vmcnt<6>(); break;
-    case 7: pg_vmcnt<7>(); break;
-    case 8: pg_vmcnt<8>(); break;
-    case 9: pg_vmcnt<9>(); break;
-    case 10: pg_vmcnt<10>(); break;
-    case 11: pg_vmcnt<11>(); break;
-    case 12: pg_vmcnt<12>(); break;
-    case 13: pg_vmcnt<13>(); break;
-    default: pg_vmcnt<0>(); break;
+// wave-uniform count -> immediate (the tail k-tiles; the steady state uses constants).  A count above the largest
+// case waits for more than needed, which is always safe.
+template <int N>
+__device__ __forceinline__ void pg_vm_wait_chain(int n) {
+  if constexpr (N == 0) {
+    pg_vmcnt<0>();
+  } else {
+    if (n >= N) pg_vmcnt<N>();
+    else pg_vm_wait_chain<N - 1>(n);
   }
 }
+__device__ __forceinline__ void pg_vm_wait(int n) { pg_vm_wait_chain<40>(n); }
 // retire this wave's LDS reads, then the raw workgroup barrier (LDS-DMA stays in flight across it)
 __device__ __forceinline__ void pg_sync_reads() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -93,23 +89,49 @@ __device__ __forceinline__ void pg_barrier() {
 }
 __device__ __forceinline__ float pg_silu(float g) { return g / (1.f + __expf(-g)); }
 
-// LDS-DMA instructions issued after region (u0, y0) up to and including region (u1, y1) in issue order
-// (k-tile major; region types y = 0 QB0 (+ GS scale loads), 1 PA0, 2 QB1, 3 PA1), counting only k-tiles < n.
-template <int GP, int GQ, int GS = 0>
-__device__ __forceinline__ int pg_after(int u0, int y0, int u1, int y1, int n) {
+// LDS-DMA issue sequence.  Position s = 4 base + j (j = s mod 4) issues region j of one k-tile:
+//     j = 0: PA1 of k-tile base + WS - 1      j = 2: PA0 of k-tile base + WS
+//     j = 1: QB0 of k-tile base + 2            j = 3: QB1 of k-tile base + 2
+// and phase j of local k-tile t issues position 4 t + j (positions < 0: the prologue).  x regions (QB0 / QB1) live
+// in a two-stage ring (stage u & 1), weight regions (PA0 / PA1) in a WS-stage ring (stage u % WS): WS = 2 is the
+// original schedule, WS = 3 / 4 keep one / two more k-tiles of weights in flight per CU.
+__host__ __device__ constexpr int pg_floor4(int s) { return s >= 0 ? s / 4 : -((-s + 3) / 4); }
+template <int WS>
+__host__ __device__ constexpr int pg_seq_tile(int s) {
+  const int base = pg_floor4(s), j = s - 4 * base;
+  return base + (j == 0 ? WS - 1 : j == 2 ? WS : 2);
+}
+// positions of the regions of k-tile u
+template <int WS> __host__ __device__ constexpr int pg_pos_qb0(int u) { return 4 * (u - 2) + 1; }
+template <int WS> __host__ __device__ constexpr int pg_pos_pa0(int u) { return 4 * (u - WS) + 2; }
+template <int WS> __host__ __device__ constexpr int pg_pos_qb1(int u) { return 4 * (u - 2) + 3; }
+template <int WS> __host__ __device__ constexpr int pg_pos_pa1(int u) { return 4 * (u - WS + 1); }
+// DMA instructions per wave issued at positions (s0, s1] whose k-tile is in [0, n)
+template <int GP, int GQ, int GS, int WS>
+__host__ __device__ constexpr int pg_window(int s0, int s1, int n) {
   int c = 0;
-  int u = u0, y = y0 + 1;
-  while (u < u1 || (u == u1 && y <= y1)) {
-    if (y == 4) {
-      y = 0;
-      ++u;
-      continue;
-    }
-    if (u < n) c += (y & 1) ? GP : y == 0 ? GQ + GS : GQ;
-    ++y;
+  for (int s = s0 + 1; s <= s1; ++s) {
+    const int u = pg_seq_tile<WS>(s), j = s - 4 * pg_floor4(s);
+    if (u >= 0 && u < n) c += (j == 0 || j == 2) ? GP : j == 1 ? GQ + GS : GQ;
   }
   return c;
 }
+// the region phase j + 1 reads is the target of phase j's wait (phase 3 reads nothing, so phase 2 does not wait;
+// phase 3 waits for QB0 and PA0 of k-tile t + 1, read in phase 0): its position for local k-tile t
+template <int WS>
+__host__ __device__ constexpr int pg_wait_target(int j, int t) {
+  return j == 0 ? pg_pos_qb1<WS>(t)
+       : j == 1 ? pg_pos_pa1<WS>(t)
+                : (pg_pos_qb0<WS>(t + 1) > pg_pos_pa0<WS>(t + 1) ? pg_pos_qb0<WS>(t + 1) : pg_pos_pa0<WS>(t + 1));
+}
+template <int GP, int GQ, int GS, int WS>
+__host__ __device__ constexpr int pg_steady(int j) {   // every position of the window exists (t = 16 stands for any)
+  return pg_window<GP, GQ, GS, WS>(pg_wait_target<WS>(j, 16), 4 * 16 + j, 1 << 30);
+}
+__host__ __device__ constexpr int pg_lds_ring(int bp, int bq, int ws, bool mx) {
+  return 2 * (bq * 128 + (mx ? bq * 4 : 0)) + ws * bp * 128;
+}
+constexpr int PG_LDS_MAX = 163840;
 }  // namespace
 
 struct PgArgs {
@@ -134,29 +156,35 @@ struct PgArgs {
                          // sums [splits][M]) and k8s_pgemm_reduce (all CUs) combines them -- no last-arriver tail
 };
 
-template <int FP, int FQ, int EPI, bool FP8, bool RMS, bool MX = false, bool MXO = false>
+template <int FP, int FQ, int EPI, bool FP8, bool RMS, bool MX = false, bool MXO = false, int WS = 2>
 __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   constexpr int BP = 64 * FP, BQ = 128 * FQ;         // weight rows, tokens per tile
   constexpr int RP = BP / 2, RQ = BQ / 2;            // rows per PA / QB region
   constexpr int GP = RP / 64, GQ = RQ / 64;          // 16-byte DMA instructions per thread per region
   constexpr int GS = MX ? 1 : 0;                     // MX: one 4-byte scale LDS-DMA per wave with QB0
   constexpr int SCH = BQ / 8;                        // MX: scale dwords (token rows) per wave
-  constexpr int OFF_SC = (BP + BQ) * 128;            // MX: the stage's [BQ] scale dwords
-  constexpr int STAGE = (BP + BQ) * 128 + (MX ? BQ * 4 : 0);
-  constexpr int OFF_QB0 = 0, OFF_PA0 = RQ * 128, OFF_QB1 = (RQ + RP) * 128, OFF_PA1 = (2 * RQ + RP) * 128;
+  // LDS: x ring [2][QB0 | QB1 | MX scales], then the weight ring [WS][PA0 | PA1]
+  constexpr int XSTAGE = BQ * 128 + (MX ? BQ * 4 : 0), WSTAGE = BP * 128, WOFF = 2 * XSTAGE;
+  constexpr int OFF_QB0 = 0, OFF_QB1 = RQ * 128, OFF_SC = BQ * 128, OFF_PA0 = 0, OFF_PA1 = RP * 128;
+  constexpr int RING = pg_lds_ring(BP, BQ, WS, MX);
   constexpr int NA = 2 * FP, NB = 2 * FQ;            // fragments per wave along P / Q
   constexpr int SLAB = BP * BQ + BQ;
-  // counted waits (see phase()): j = 0 waits for QB1(t), j = 1 for PA1(t), j = 3 for PA0(t + 1)
-  constexpr int STEADY0 = 3 * GP + 2 * GQ + GS, STEADY1 = 2 * GP + 3 * GQ + 2 * GS, STEADY3 = 2 * GP + 3 * GQ + GS;
-  static_assert(GP >= 1 && GQ >= 1 && STEADY0 <= 13 && STEADY1 <= 13, "tile shape");
+  // counted waits (see phase()): j = 0 waits for QB1(t), j = 1 for PA1(t), j = 3 for QB0 / PA0(t + 1)
+  constexpr int STEADY0 = pg_steady<GP, GQ, GS, WS>(0), STEADY1 = pg_steady<GP, GQ, GS, WS>(1),
+                STEADY3 = pg_steady<GP, GQ, GS, WS>(3);
+  static_assert(WS != 2 || (STEADY0 == 3 * GP + 2 * GQ + GS && STEADY1 == 2 * GP + 3 * GQ + 2 * GS &&
+                            STEADY3 == 2 * GP + 3 * GQ + GS), "two-stage schedule");
+  static_assert(GP >= 1 && GQ >= 1 && WS >= 2 && WS <= 4 && STEADY1 <= 40, "tile shape");
+  static_assert(RING <= PG_LDS_MAX && 64 + BQ * 4 <= RING, "LDS");
   static_assert(!(FP8 && RMS), "fp8 activations are quantized before the GEMM");
   static_assert(!MX || FP8, "MX: e4m3 activations");
   static_assert(!MXO || (EPI == PG_SWIGLU && FP8 && FP % 2 == 0), "MX output: SwiGLU fragment pairs");
   static_assert(SCH <= 64, "scale dwords per wave");
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the launch stub
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + 64 + BQ * 4];
-  unsigned* flag = reinterpret_cast<unsigned*>(lds + 2 * STAGE);
-  float* rss = reinterpret_cast<float*>(lds + 2 * STAGE + 64);   // [BQ] row sums of squares
+  __shared__ __attribute__((aligned(16))) char lds[RING];
+  // after the main loop only (the ring is dead then: every wave has passed the re-aligning barrier)
+  unsigned* flag = reinterpret_cast<unsigned*>(lds);
+  float* rss = reinterpret_cast<float*>(lds + 64);   // [BQ] row sums of squares
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
@@ -215,10 +243,12 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
       __builtin_amdgcn_global_load_lds(src + off[i], (__attribute__((address_space(3))) void*)(dst + i * 8192), 16,
                                        0, 0);
   };
-  // issue region y of local k-tile u into stage u & 1
+  auto xstage = [&](int u) { return lds + (u & 1) * XSTAGE; };
+  auto wstage = [&](int u) { return lds + WOFF + (WS == 2 ? (u & 1) : (int)((unsigned)u % (unsigned)WS)) * WSTAGE; };
+  // issue region y of local k-tile u: x regions into x stage u & 1, weight regions into weight stage u % WS
   auto issue = [&](auto Y, int u) {
     constexpr int y = decltype(Y)::value;
-    char* dst = lds + (u & 1) * STAGE + wid * 1024 +
+    char* dst = ((y & 1) ? wstage(u) : xstage(u)) + wid * 1024 +
                 (y == 0 ? OFF_QB0 : y == 1 ? OFF_PA0 : y == 2 ? OFF_QB1 : OFF_PA1);
     const uint32_t kb = (uint32_t)u * 128u;
     if constexpr (y == 0) {
@@ -226,7 +256,7 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
       if constexpr (MX) {
         if (lane < SCH)
           __builtin_amdgcn_global_load_lds(a.xe + (osc + (uint32_t)u * (uint32_t)a.M * 4u),   // saddr + 32-bit voffset
-                                           (__attribute__((address_space(3))) void*)(lds + (u & 1) * STAGE + OFF_SC +
+                                           (__attribute__((address_space(3))) void*)(xstage(u) + OFF_SC +
                                                                                      wid * SCH * 4),
                                            4, 0, 0);
       }
@@ -325,10 +355,11 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   // one phase of local k-tile t; J = phase index 0..3
   auto phase = [&](auto J, int t) {
     constexpr int j = decltype(J)::value;
-    const char* sb = lds + (t & 1) * STAGE;
+    const char* sb = xstage(t);
+    const char* wb = wstage(t);
     if constexpr (j == 0) {
       read_frags(sb + OFF_QB0 + qbase, B0r[0], B0r[FP8 ? 0 : 1], NFQ{});
-      read_frags(sb + OFF_PA0 + pbase, Ar[0], Ar[FP8 ? 0 : 1], NFP{});
+      read_frags(wb + OFF_PA0 + pbase, Ar[0], Ar[FP8 ? 0 : 1], NFP{});
       if constexpr (MX) {   // both halves' scales now: the region is refilled in phase 1
         const int* scl = reinterpret_cast<const int*>(sb + OFF_SC);
 #pragma unroll
@@ -339,25 +370,22 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
             scp = (int)(((uint32_t)scp & ~(0xffu << (8 * (h * FQ + f)))) | (byte << (8 * (h * FQ + f))));
           }
       }
-      if (t + 1 < n) issue(Y3{}, t + 1);
+      if (t + WS - 1 < n) issue(Y3{}, t + WS - 1);
     } else if constexpr (j == 1) {
       read_frags(sb + OFF_QB1 + qbase, B1r[0], B1r[FP8 ? 0 : 1], NFQ{});
       if (t + 2 < n) issue(Y0{}, t + 2);
     } else if constexpr (j == 2) {
-      read_frags(sb + OFF_PA1 + pbase, Ar[0], Ar[FP8 ? 0 : 1], NFP{});
-      if (t + 2 < n) issue(Y1{}, t + 2);
+      read_frags(wb + OFF_PA1 + pbase, Ar[0], Ar[FP8 ? 0 : 1], NFP{});
+      if (t + WS < n) issue(Y1{}, t + WS);
     } else {
       if (t + 2 < n) issue(Y2{}, t + 2);
     }
     // the regions the next phase reads are complete for this wave (counted: the newer DMA stays in flight)
     if constexpr (j != 2) {
-      if (t + 2 < n) {
+      if (t >= 2 && t + WS < n) {
         pg_vmcnt<j == 0 ? STEADY0 : j == 1 ? STEADY1 : STEADY3>();
       } else {
-        const int c = j == 0 ? pg_after<GP, GQ, GS>(t, 2, t + 1, 3, n)
-                    : j == 1 ? pg_after<GP, GQ, GS>(t, 3, t + 2, 0, n)
-                             : pg_after<GP, GQ, GS>(t + 1, 1, t + 2, 2, n);
-        pg_vm_wait(c);
+        pg_vm_wait(pg_window<GP, GQ, GS, WS>(pg_wait_target<WS>(j, t), 4 * t + j, n));
       }
     }
     pg_sync_reads();
@@ -379,17 +407,18 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     pg_barrier();
   };
 
-  // ---- prologue: k-tile 0 whole and k-tile 1 except PA1 (issued in k-tile 0's phase 0)
-  issue(Y0{}, 0);
-  issue(Y1{}, 0);
-  issue(Y2{}, 0);
-  issue(Y3{}, 0);
-  if (n > 1) {
-    issue(Y0{}, 1);
-    issue(Y1{}, 1);
-    issue(Y2{}, 1);
+  // ---- prologue: the sequence positions before k-tile 0's phase 0 (WS = 2: k-tile 0 whole and k-tile 1 except
+  // PA1, which k-tile 0's phase 0 issues), in sequence order
+#pragma unroll
+  for (int s = -4 * WS - 4; s < 0; ++s) {
+    const int u = pg_seq_tile<WS>(s), j = s - 4 * pg_floor4(s);
+    if (u < 0 || u >= n) continue;
+    if (j == 0) issue(Y3{}, u);
+    else if (j == 1) issue(Y0{}, u);
+    else if (j == 2) issue(Y1{}, u);
+    else issue(Y2{}, u);
   }
-  pg_vm_wait(pg_after<GP, GQ, GS>(0, 1, 1, 2, n));
+  pg_vm_wait(pg_window<GP, GQ, GS, WS>(pg_wait_target<WS>(3, -1), -1, n));
   pg_barrier();
   if (late) __builtin_amdgcn_s_barrier();   // stagger waves 4-7 by one barrier (wave-uniform branch)
   if (a.prio == 1 && late) __builtin_amdgcn_s_setprio(1);
@@ -591,21 +620,28 @@ using namespace k8sllm;
 
 namespace {
 struct PgCfg {
-  int fp, fq;
+  int fp, fq, ws;
 };
-// tile configurations: BP = 64 FP weight rows x BQ = 128 FQ tokens
+// tile configurations: BP = 64 FP weight rows x BQ = 128 FQ tokens, WS weight-ring stages
 constexpr PgCfg kPgCfgs[] = {
-    {4, 2},   // 0: 256 x 256
-    {2, 2},   // 1: 128 x 256
-    {4, 1},   // 2: 256 x 128
-    {2, 1},   // 3: 128 x 128
+    {4, 2, 2},   // 0: 256 x 256
+    {2, 2, 2},   // 1: 128 x 256
+    {4, 1, 2},   // 2: 256 x 128
+    {2, 1, 2},   // 3: 128 x 128
+    {4, 2, 3},   // 4: 256 x 256, three weight stages (all 160 KiB of LDS; MX activations: two).  The same tiles at
+                 // 128 x 256 / 256 x 128 / 128 x 128 with 3-4 weight stages lost to configs 0-3 on all 30 TP=1
+                 // shapes (256-8192 rows) and were dropped (profiles/pgemm_weight_ring_r6.txt)
 };
+// the weight-ring depth a config runs with: its own where the LDS holds it, else two
+constexpr int pg_ws(const PgCfg& c, bool mx) {
+  return pg_lds_ring(64 * c.fp, 128 * c.fq, c.ws, mx) <= PG_LDS_MAX ? c.ws : 2;
+}
 constexpr int kPgNumCfgs = sizeof(kPgCfgs) / sizeof(kPgCfgs[0]);
 
 template <int C, int EPI, bool FP8, bool RMS, bool MX = false, bool MXO = false>
 int pg_launch(const PgArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((pgemm_kernel<kPgCfgs[C].fp, kPgCfgs[C].fq, EPI, FP8, RMS, MX, MXO>), dim3(a.nwg), dim3(512), 0,
-                     s, a);
+  hipLaunchKernelGGL((pgemm_kernel<kPgCfgs[C].fp, kPgCfgs[C].fq, EPI, FP8, RMS, MX, MXO, pg_ws(kPgCfgs[C], MX)>),
+                     dim3(a.nwg), dim3(512), 0, s, a);
   return (int)hipGetLastError();
 }
 
@@ -699,7 +735,7 @@ extern "C" int k8s_pgemm_config(int cfg, int* bp, int* bq, int* lds_bytes) {
   if (cfg < 0 || cfg >= kPgNumCfgs) return -1;
   *bp = 64 * kPgCfgs[cfg].fp;
   *bq = 128 * kPgCfgs[cfg].fq;
-  *lds_bytes = 2 * (*bp + *bq) * 128 + 64 + *bq * 4;
+  *lds_bytes = pg_lds_ring(*bp, *bq, kPgCfgs[cfg].ws, false);
   return 0;
 }
 

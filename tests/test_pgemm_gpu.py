@@ -60,6 +60,24 @@ def test_exact_small_integers_every_config():
             assert torch.equal(y, exp), f"cfg {cfg} splits {splits}: {(y - exp).abs().max().item()}"
 
 
+def test_exact_short_k_every_ring_depth():
+    """1-5 k-tiles per slice: fewer k-tiles than weight-ring stages (configs 4-7 keep 3-4 weight stages), so the
+    prologue, the tail waits and the ring slots all run their short-loop paths; exact integer data."""
+    for cfg, (bp, bq, _lds) in enumerate(ops.pgemm_configs()):
+        M, N = bq + 8, bp + 20
+        for K in (64, 192, 320):
+            x = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+            w = (torch.arange(N * K, device=DEV).view(N, K) % 5 - 2).to(torch.bfloat16)
+            w[:, 3] += torch.arange(N, device=DEV).to(torch.bfloat16) % 3
+            exp = x.float() @ w.float().t()
+            for splits in (1, 2):
+                if splits > K * 2 // 128:
+                    continue
+                y = ops.pgemm(x, w, ops.EPI_F32, cfg=cfg, splits=splits)
+                torch.cuda.synchronize()
+                assert torch.equal(y, exp), f"cfg {cfg} K {K} splits {splits}: {(y - exp).abs().max().item()}"
+
+
 @pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("epi", [ops.EPI_BF16, ops.EPI_F32, ops.EPI_SWIGLU])
 def test_every_config(epi, fp8):

@@ -71,7 +71,21 @@ def main() -> int:
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--model", choices=["70b", "8b"], default="70b", help="projection shapes of Llama-3.3-70B / 3-8B")
+    ap.add_argument("--merge-json", default=None, help="merge the plans of an earlier --json-out run into the table "
+                                                        "(no GPU needed) and exit")
     a = ap.parse_args()
+    if a.merge_json:
+        with open(a.merge_json) as f:
+            rows = json.load(f)
+        plans = {}
+        for r in rows:
+            key = f"{r['M']},{r['N']},{r['K']},{r['epi']},{int(r['fp8'])}"
+            if r["mgemm_us"] == r["mgemm_us"] and r["mgemm_us"] < r["pgemm_us"]:   # (NaN: mgemm not timed)
+                plans[key] = ["mgemm", 0, 0, 0, r["mgemm_us"], r["lib_us"]]
+            else:
+                plans[key] = [r["kernel"], r["cfg"], r["splits"], r["group_m"], r["pgemm_us"], r["lib_us"]]
+        _write_plans(plans)
+        return 0
     dims = {} if a.model == "70b" else dict(hidden=4096, inter=14336, nq=32, nkv=8)
 
     torch.manual_seed(0)
@@ -133,16 +147,20 @@ def main() -> int:
         with open(a.json_out, "w") as f:
             json.dump(rows, f, indent=1)
     if a.write:
-        path = ops.PG_TABLE_PATH
-        table = {"arch": "gfx950", "plans": {}}
-        if os.path.isfile(path):
-            with open(path) as f:
-                table = json.load(f)
-        table["plans"].update(plans)
-        with open(path, "w") as f:
-            json.dump(table, f, indent=0, sort_keys=True)
-        print(f"# wrote {len(plans)} plans to {path}")
+        _write_plans(plans)
     return 0
+
+
+def _write_plans(plans: dict) -> None:
+    path = ops.PG_TABLE_PATH
+    table = {"arch": "gfx950", "plans": {}}
+    if os.path.isfile(path):
+        with open(path) as f:
+            table = json.load(f)
+    table["plans"].update(plans)
+    with open(path, "w") as f:
+        json.dump(table, f, indent=0, sort_keys=True)
+    print(f"# wrote {len(plans)} plans to {path}")
 
 
 if __name__ == "__main__":
