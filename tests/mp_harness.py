@@ -21,9 +21,11 @@ def free_port() -> int:
 
 
 def _entry(fn, rank, world, port, env, q, dump_after=None):
-    if dump_after:
-        import faulthandler
+    import faulthandler
+    import signal
 
+    faulthandler.register(signal.SIGUSR1, all_threads=True)   # the parent asks still-running ranks where they wait
+    if dump_after:
         faulthandler.dump_traceback_later(dump_after, exit=False)   # a hung rank shows where it waits
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -61,6 +63,20 @@ def run_ranks(fn, world: int, env=None, timeout_s: float = 600.0) -> dict:
                 if any(p.exitcode not in (None, 0) for p in procs):
                     break
     finally:
+        if len(got) < world:
+            # a rank failed or the run timed out: every rank still running prints its Python stack (all threads) to
+            # stderr before it is stopped -- the peer a failed collective waited for shows where it was
+            import signal
+
+            for r, p in enumerate(procs):
+                if r not in got and p.is_alive():
+                    print(f"[mp_harness] {fn.__name__}: rank {r} still running; its stack:", file=sys.__stderr__,
+                          flush=True)
+                    try:
+                        os.kill(p.pid, signal.SIGUSR1)
+                    except OSError:
+                        pass
+                    time.sleep(1.0)
         for p in procs:
             p.join(60 if len(got) == world else 5)
             if p.is_alive():
