@@ -14,16 +14,15 @@
 //    twice the bf16 rate -- the non-scaled 16x16x32 fp8 MFMA is only as fast as bf16.
 //  * k-tiles of 128 bytes per row (64 bf16 / 128 e4m3), split into four regions: QB0 / QB1 (the first / second FQ
 //    fragments of every wave column) and PA0 / PA1 (the first / second FP fragments of every wave row).  The x
-//    regions live in a two-stage LDS ring, the weight regions in a WS-stage ring (WS = 2, or 3-4 where the 160 KiB
-//    hold it: more weight bytes in flight per CU for the weight-streaming row counts).  One k-tile is four
-//    phases, each one MFMA quadrant:
-//        phase 0: read QB0 + PA0, MFMA (a0, b0)        phase 2: read PA1, MFMA (a1, b1)
-//        phase 1: read QB1,        MFMA (a0, b1)        phase 3: (registers only) MFMA (a1, b0)
-//    and every phase refills ONE region with LDS-DMA (global_load_lds_dwordx4), at least one phase after its
-//    last reader: PA1 of k-tile t+WS-1 in phase 0, QB0 of t+2 in phase 1, PA0 of t+WS in phase 2, QB1 of t+2 in
-//    phase 3.  Five regions (~80 KB at 256 x 256, WS = 2) to nine (WS = 3) stay in flight across the raw
-//    s_barriers; each wait is a counted `s_waitcnt vmcnt` one phase before the first reader (never vmcnt(0) in
-//    the steady state; pg_window counts the sequence).
+//    regions live in a two-stage LDS ring, the weight regions in a WS-stage ring (WS = 2, or 3 where the 160 KiB
+//    hold it).  One k-tile is two phases, each two MFMA quadrants:
+//        phase 0: read QB0 + QB1 + PA0, MFMA (a0, b0) (a0, b1)      phase 1: read PA1, MFMA (a1, b1) (a1, b0)
+//    and each phase refills two regions with LDS-DMA (global_load_lds_dwordx4) at least one phase after their last
+//    reader: PA0 + PA1 of k-tile t+WS-1 in phase 0, QB0 + QB1 of t+2 in phase 1.  Each wait is a counted
+//    `s_waitcnt vmcnt` one phase before the first reader (never vmcnt(0) in the steady state; pg_window counts
+//    the issue sequence).  The four-phase form (one quadrant per phase, one region per phase) ran 1.02-1.19x
+//    slower on all 40 TP=1 / TP=8 70B shapes at 256-8192 rows: twice the barriers, and a quarter-k-tile MFMA
+//    section too short to hide the partner group's reads (profiles/pgemm_two_phase_r6.txt).
 //  * waves 4-7 run one barrier behind waves 0-3 (two barriers per phase): on every SIMD one wave is in its
 //    MFMA section while its partner reads LDS and issues the next DMA (8-wave ping-pong).  Every LDS read is
 //    retired (lgkmcnt(0)) before the phase's first barrier, which is what makes the one-phase refill legal for
@@ -89,44 +88,42 @@ __device__ __forceinline__ void pg_barrier() {
 }
 __device__ __forceinline__ float pg_silu(float g) { return g / (1.f + __expf(-g)); }
 
-// LDS-DMA issue sequence.  Position s = 4 base + j (j = s mod 4) issues region j of one k-tile:
-//     j = 0: PA1 of k-tile base + WS - 1      j = 2: PA0 of k-tile base + WS
-//     j = 1: QB0 of k-tile base + 2            j = 3: QB1 of k-tile base + 2
-// and phase j of local k-tile t issues position 4 t + j (positions < 0: the prologue).  x regions (QB0 / QB1) live
-// in a two-stage ring (stage u & 1), weight regions (PA0 / PA1) in a WS-stage ring (stage u % WS): WS = 2 is the
-// original schedule, WS = 3 / 4 keep one / two more k-tiles of weights in flight per CU.
+// LDS-DMA issue sequence.  Position s = 4 base + k issues region k: 0 PA0 / 1 PA1 of k-tile base + WS - 1 (both in
+// phase 0 of local k-tile base), 2 QB0 / 3 QB1 of k-tile base + 2 (both in phase 1); positions < 0 are the
+// prologue.  x regions (QB0 / QB1) live in a two-stage ring (stage u & 1), weight regions (PA0 / PA1) in a
+// WS-stage ring (stage u % WS).
 __host__ __device__ constexpr int pg_floor4(int s) { return s >= 0 ? s / 4 : -((-s + 3) / 4); }
 template <int WS>
 __host__ __device__ constexpr int pg_seq_tile(int s) {
-  const int base = pg_floor4(s), j = s - 4 * base;
-  return base + (j == 0 ? WS - 1 : j == 2 ? WS : 2);
+  const int base = pg_floor4(s), k = s - 4 * base;
+  return base + (k < 2 ? WS - 1 : 2);
 }
-// positions of the regions of k-tile u
-template <int WS> __host__ __device__ constexpr int pg_pos_qb0(int u) { return 4 * (u - 2) + 1; }
-template <int WS> __host__ __device__ constexpr int pg_pos_pa0(int u) { return 4 * (u - WS) + 2; }
-template <int WS> __host__ __device__ constexpr int pg_pos_qb1(int u) { return 4 * (u - 2) + 3; }
-template <int WS> __host__ __device__ constexpr int pg_pos_pa1(int u) { return 4 * (u - WS + 1); }
+template <int WS> __host__ __device__ constexpr int pg_pos_pa0(int u) { return 4 * (u - WS + 1); }
+template <int WS> __host__ __device__ constexpr int pg_pos_pa1(int u) { return 4 * (u - WS + 1) + 1; }
+__host__ __device__ constexpr int pg_pos_qb0(int u) { return 4 * (u - 2) + 2; }
+__host__ __device__ constexpr int pg_pos_qb1(int u) { return 4 * (u - 2) + 3; }
+// the last position phase j of local k-tile t issues
+__host__ __device__ constexpr int pg_issue_end(int j, int t) { return 4 * t + (j == 0 ? 1 : 3); }
 // DMA instructions per wave issued at positions (s0, s1] whose k-tile is in [0, n)
 template <int GP, int GQ, int GS, int WS>
 __host__ __device__ constexpr int pg_window(int s0, int s1, int n) {
   int c = 0;
   for (int s = s0 + 1; s <= s1; ++s) {
-    const int u = pg_seq_tile<WS>(s), j = s - 4 * pg_floor4(s);
-    if (u >= 0 && u < n) c += (j == 0 || j == 2) ? GP : j == 1 ? GQ + GS : GQ;
+    const int u = pg_seq_tile<WS>(s), k = s - 4 * pg_floor4(s);
+    if (u >= 0 && u < n) c += k < 2 ? GP : k == 2 ? GQ + GS : GQ;
   }
   return c;
 }
-// the region phase j + 1 reads is the target of phase j's wait (phase 3 reads nothing, so phase 2 does not wait;
-// phase 3 waits for QB0 and PA0 of k-tile t + 1, read in phase 0): its position for local k-tile t
+__host__ __device__ constexpr int pg_max(int a, int b) { return a > b ? a : b; }
+// phase j's wait covers what the next phase reads: phase 0 waits for PA1(t), phase 1 for QB0 / QB1 / PA0 of
+// k-tile t + 1 (the latest of their positions)
 template <int WS>
 __host__ __device__ constexpr int pg_wait_target(int j, int t) {
-  return j == 0 ? pg_pos_qb1<WS>(t)
-       : j == 1 ? pg_pos_pa1<WS>(t)
-                : (pg_pos_qb0<WS>(t + 1) > pg_pos_pa0<WS>(t + 1) ? pg_pos_qb0<WS>(t + 1) : pg_pos_pa0<WS>(t + 1));
+  return j == 0 ? pg_pos_pa1<WS>(t) : pg_max(pg_pos_qb1(t + 1), pg_pos_pa0<WS>(t + 1));
 }
 template <int GP, int GQ, int GS, int WS>
 __host__ __device__ constexpr int pg_steady(int j) {   // every position of the window exists (t = 16 stands for any)
-  return pg_window<GP, GQ, GS, WS>(pg_wait_target<WS>(j, 16), 4 * 16 + j, 1 << 30);
+  return pg_window<GP, GQ, GS, WS>(pg_wait_target<WS>(j, 16), pg_issue_end(j, 16), 1 << 30);
 }
 __host__ __device__ constexpr int pg_lds_ring(int bp, int bq, int ws, bool mx) {
   return 2 * (bq * 128 + (mx ? bq * 4 : 0)) + ws * bp * 128;
@@ -169,12 +166,9 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   constexpr int RING = pg_lds_ring(BP, BQ, WS, MX);
   constexpr int NA = 2 * FP, NB = 2 * FQ;            // fragments per wave along P / Q
   constexpr int SLAB = BP * BQ + BQ;
-  // counted waits (see phase()): j = 0 waits for QB1(t), j = 1 for PA1(t), j = 3 for QB0 / PA0(t + 1)
-  constexpr int STEADY0 = pg_steady<GP, GQ, GS, WS>(0), STEADY1 = pg_steady<GP, GQ, GS, WS>(1),
-                STEADY3 = pg_steady<GP, GQ, GS, WS>(3);
-  static_assert(WS != 2 || (STEADY0 == 3 * GP + 2 * GQ + GS && STEADY1 == 2 * GP + 3 * GQ + 2 * GS &&
-                            STEADY3 == 2 * GP + 3 * GQ + GS), "two-stage schedule");
-  static_assert(GP >= 1 && GQ >= 1 && WS >= 2 && WS <= 4 && STEADY1 <= 40, "tile shape");
+  // counted waits (see phase()): j = 0 waits for PA1(t), j = 1 for QB0 / QB1 / PA0 of k-tile t + 1
+  constexpr int STEADY0 = pg_steady<GP, GQ, GS, WS>(0), STEADY1 = pg_steady<GP, GQ, GS, WS>(1);
+  static_assert(GP >= 1 && GQ >= 1 && WS >= 2 && WS <= 4 && STEADY0 <= 40 && STEADY1 <= 40, "tile shape");
   static_assert(RING <= PG_LDS_MAX && 64 + BQ * 4 <= RING, "LDS");
   static_assert(!(FP8 && RMS), "fp8 activations are quantized before the GEMM");
   static_assert(!MX || FP8, "MX: e4m3 activations");
@@ -352,13 +346,15 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
     }
   };
 
-  // one phase of local k-tile t; J = phase index 0..3
+  // one phase of local k-tile t (J = 0 / 1): phase 0 reads QB0 + QB1 + PA0 and runs quadrants (a0, b0), (a0, b1);
+  // phase 1 reads PA1 and runs (a1, b1), (a1, b0)
   auto phase = [&](auto J, int t) {
     constexpr int j = decltype(J)::value;
     const char* sb = xstage(t);
     const char* wb = wstage(t);
     if constexpr (j == 0) {
       read_frags(sb + OFF_QB0 + qbase, B0r[0], B0r[FP8 ? 0 : 1], NFQ{});
+      read_frags(sb + OFF_QB1 + qbase, B1r[0], B1r[FP8 ? 0 : 1], NFQ{});
       read_frags(wb + OFF_PA0 + pbase, Ar[0], Ar[FP8 ? 0 : 1], NFP{});
       if constexpr (MX) {   // both halves' scales now: the region is refilled in phase 1
         const int* scl = reinterpret_cast<const int*>(sb + OFF_SC);
@@ -370,37 +366,33 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
             scp = (int)(((uint32_t)scp & ~(0xffu << (8 * (h * FQ + f)))) | (byte << (8 * (h * FQ + f))));
           }
       }
-      if (t + WS - 1 < n) issue(Y3{}, t + WS - 1);
-    } else if constexpr (j == 1) {
-      read_frags(sb + OFF_QB1 + qbase, B1r[0], B1r[FP8 ? 0 : 1], NFQ{});
-      if (t + 2 < n) issue(Y0{}, t + 2);
-    } else if constexpr (j == 2) {
-      read_frags(wb + OFF_PA1 + pbase, Ar[0], Ar[FP8 ? 0 : 1], NFP{});
-      if (t + WS < n) issue(Y1{}, t + WS);
-    } else {
-      if (t + 2 < n) issue(Y2{}, t + 2);
-    }
-    // the regions the next phase reads are complete for this wave (counted: the newer DMA stays in flight)
-    if constexpr (j != 2) {
-      if (t >= 2 && t + WS < n) {
-        pg_vmcnt<j == 0 ? STEADY0 : j == 1 ? STEADY1 : STEADY3>();
-      } else {
-        pg_vm_wait(pg_window<GP, GQ, GS, WS>(pg_wait_target<WS>(j, t), 4 * t + j, n));
+      if (t + WS - 1 < n) {
+        issue(Y1{}, t + WS - 1);
+        issue(Y3{}, t + WS - 1);
       }
+    } else {
+      read_frags(wb + OFF_PA1 + pbase, Ar[0], Ar[FP8 ? 0 : 1], NFP{});
+      if (t + 2 < n) {
+        issue(Y0{}, t + 2);
+        issue(Y2{}, t + 2);
+      }
+    }
+    if (t >= 2 && t + WS < n) {
+      pg_vmcnt<j == 0 ? STEADY0 : STEADY1>();
+    } else {
+      pg_vm_wait(pg_window<GP, GQ, GS, WS>(pg_wait_target<WS>(j, t), pg_issue_end(j, t), n));
     }
     pg_sync_reads();
     __builtin_amdgcn_sched_barrier(0);
     if (a.prio == 0) __builtin_amdgcn_s_setprio(1);
     if constexpr (j == 0) {
       mma(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-      if (wr == 0) squares(std::integral_constant<int, 0>{});
-    } else if constexpr (j == 1) {
       mma(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-      if (wr == 1) squares(std::integral_constant<int, 1>{});
-    } else if constexpr (j == 2) {
-      mma(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+      if (wr == 0) squares(std::integral_constant<int, 0>{});
     } else {
+      mma(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
       mma(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+      if (wr == 1) squares(std::integral_constant<int, 1>{});
     }
     if (a.prio == 0) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
@@ -411,14 +403,14 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   // PA1, which k-tile 0's phase 0 issues), in sequence order
 #pragma unroll
   for (int s = -4 * WS - 4; s < 0; ++s) {
-    const int u = pg_seq_tile<WS>(s), j = s - 4 * pg_floor4(s);
+    const int u = pg_seq_tile<WS>(s), k = s - 4 * pg_floor4(s);
     if (u < 0 || u >= n) continue;
-    if (j == 0) issue(Y3{}, u);
-    else if (j == 1) issue(Y0{}, u);
-    else if (j == 2) issue(Y1{}, u);
+    if (k == 0) issue(Y1{}, u);
+    else if (k == 1) issue(Y3{}, u);
+    else if (k == 2) issue(Y0{}, u);
     else issue(Y2{}, u);
   }
-  pg_vm_wait(pg_window<GP, GQ, GS, WS>(pg_wait_target<WS>(3, -1), -1, n));
+  pg_vm_wait(pg_window<GP, GQ, GS, WS>(pg_wait_target<WS>(1, -1), -1, n));
   pg_barrier();
   if (late) __builtin_amdgcn_s_barrier();   // stagger waves 4-7 by one barrier (wave-uniform branch)
   if (a.prio == 1 && late) __builtin_amdgcn_s_setprio(1);
@@ -426,8 +418,6 @@ __global__ void __launch_bounds__(512) pgemm_kernel(PgArgs a) {
   for (int t = 0; t < n; ++t) {
     phase(std::integral_constant<int, 0>{}, t);
     phase(std::integral_constant<int, 1>{}, t);
-    phase(std::integral_constant<int, 2>{}, t);
-    phase(std::integral_constant<int, 3>{}, t);
   }
   if (!late) __builtin_amdgcn_s_barrier();  // re-align the two wave groups
   if (a.prio == 1) __builtin_amdgcn_s_setprio(0);
@@ -622,15 +612,14 @@ namespace {
 struct PgCfg {
   int fp, fq, ws;
 };
-// tile configurations: BP = 64 FP weight rows x BQ = 128 FQ tokens, WS weight-ring stages
+// tile configurations: BP = 64 FP weight rows x BQ = 128 FQ tokens, WS weight-ring stages.  (3-4-stage rings at the
+// smaller tiles never beat configs 0-3: profiles/pgemm_weight_ring_r6.txt)
 constexpr PgCfg kPgCfgs[] = {
     {4, 2, 2},   // 0: 256 x 256
     {2, 2, 2},   // 1: 128 x 256
     {4, 1, 2},   // 2: 256 x 128
     {2, 1, 2},   // 3: 128 x 128
-    {4, 2, 3},   // 4: 256 x 256, three weight stages (all 160 KiB of LDS; MX activations: two).  The same tiles at
-                 // 128 x 256 / 256 x 128 / 128 x 128 with 3-4 weight stages lost to configs 0-3 on all 30 TP=1
-                 // shapes (256-8192 rows) and were dropped (profiles/pgemm_weight_ring_r6.txt)
+    {4, 2, 3},   // 4: 256 x 256, three weight stages (all 160 KiB of LDS; MX activations: two)
 };
 // the weight-ring depth a config runs with: its own where the LDS holds it, else two
 constexpr int pg_ws(const PgCfg& c, bool mx) {
