@@ -123,12 +123,17 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
   const int lo = li * 64 + ((g ^ (li >> 2)) << 4);
   const int pb = (wr * (BP / 2)) * 64 + lo, qb = (BP + wc * (BQ / 2)) * 64 + lo;
   bf16x8 A0[FP], B0[FQ], A1[FP], B1[FQ];
+  // The fragment reads are inline asm as well: a compiler-visible LDS read ahead of the (opaque) asm MFMAs made the
+  // compiler drain lgkmcnt(0) before the first MFMA, exposing the whole read latency every k-step.  Nothing reads
+  // An / Bn before the next k-step's p4_sync, whose lgkmcnt(0) retires these reads.
   auto rd = [&](int u, bf16x8* A, bf16x8* B) {
     const char* sb = lds + (u & (NSLOT - 1)) * SUB;
+    const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)(sb + pb));
+    const uint32_t lb = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)(sb + qb));
 #pragma unroll
-    for (int f = 0; f < FP; ++f) A[f] = *reinterpret_cast<const bf16x8*>(sb + pb + f * 1024);
+    for (int f = 0; f < FP; ++f) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A[f]) : "v"(la), "i"(f * 1024));
 #pragma unroll
-    for (int f = 0; f < FQ; ++f) B[f] = *reinterpret_cast<const bf16x8*>(sb + qb + f * 1024);
+    for (int f = 0; f < FQ; ++f) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(B[f]) : "v"(lb), "i"(f * 1024));
   };
 
   f32x4 acc[FP][FQ];
@@ -147,7 +152,9 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
       if (i >= i0 && i < i1)
 #pragma unroll
         for (int j = 0; j < FQ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
+          // in place, in inline asm: the AGPR tile stays put (with the builtin the register allocator rotated the
+          // accumulators through AGPR <-> VGPR copies, 2.2-3.7 per MFMA in every configuration; 11-13 % slower)
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(A[i]), "v"(B[j]));
   };
   auto squares = [&](const bf16x8* B, bool sq) {
     if constexpr (RMS) {
@@ -164,13 +171,40 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
   };
   // One k-step s: make s+1 visible (counted vmcnt + barrier), refill the slot of s-1 with s+3 (LDS-DMA), read
   // s+1 into the other register set, then the 64 MFMAs on s (registers read one k-step earlier).
+  // One k-step s: make s+1 visible (counted vmcnt + barrier), then the 64 MFMAs on s (registers read one k-step
+  // earlier) with the LDS-DMA refill of s-1's slot by s+3 and the fragment reads of s+1 spread between them: one wave
+  // per SIMD, so nothing else would hide a DMA issue or an LDS read (all three are volatile asm or side-effecting
+  // builtins, so this program order is the issue order).
   auto step_full = [&](int s, bf16x8* Ac, bf16x8* Bc, bf16x8* An, bf16x8* Bn) {
     p4_vmcnt<G>();
     p4_sync();
     __builtin_amdgcn_sched_barrier(0);
-    issue(s + 3);
-    rd(s + 1, An, Bn);
-    mma(Ac, Bc, 0, FP);
+    constexpr int MF = FP * FQ, DR = FP + FQ;
+    char* dst = lds + ((s + 3) & (NSLOT - 1)) * SUB + wid * 1024;
+    const uint32_t kb = (uint32_t)(s + 3) * 64u;
+    const char* sb = lds + ((s + 1) & (NSLOT - 1)) * SUB;
+    const uint32_t la = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)(sb + pb));
+    const uint32_t lb = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)(sb + qb));
+#pragma unroll
+    for (int i = 0; i < FP; ++i)
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) {
+      const int k = i * FQ + j;
+#pragma unroll
+      for (int d = 0; d < G; ++d)
+        if (k == d * MF / G)
+          __builtin_amdgcn_global_load_lds((d < GW ? a.W : a.x) + (off[d] + kb),
+                                           (__attribute__((address_space(3))) void*)(dst + d * 4096), 16, 0, 0);
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(Ac[i]), "v"(Bc[j]));
+#pragma unroll
+      for (int r = 0; r < DR; ++r)
+        if (k == r * MF / DR + MF / (2 * DR)) {
+          if (r < FP)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(An[r]) : "v"(la), "i"(r * 1024));
+          else
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Bn[r - FP]) : "v"(lb), "i"((r - FP) * 1024));
+        }
+    }
     squares(Bc, (s & 1) == wr);
   };
   auto step_tail = [&](int s, bf16x8* Ac, bf16x8* Bc, bf16x8* An, bf16x8* Bn) {
@@ -185,6 +219,14 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
   };
 
   // n is even (the host splits K in 64-deep units): the loop body is two k-steps with fixed register sets
+  {   // the inline-asm MFMAs are opaque to the hazard recognizer: every zeroed accumulator passes through an asm
+    // tied to it after its write, all before the first MFMA (volatile asm keeps its order)
+    asm volatile("s_nop 1" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < FP; ++i)
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) asm volatile("s_nop 0" : "+a"(acc[i][j]));
+  }
   issue(0);
   issue(1);
   if (n > 2) issue(2);
@@ -204,6 +246,14 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
   step_tail(s, A0, B0, A1, B1);
   step_tail(s + 1, A1, B1, A0, B0);
   p4_vmcnt<0>();
+  {   // ... and the last MFMAs' results wait out the MFMA latency before the epilogue reads them:
+    // the padding, then one tied empty asm per accumulator (so no read is hoisted above the padding)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < FP; ++i)
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) asm volatile("" : "+a"(acc[i][j]));
+  }
 
   if constexpr (RMS) {
 #pragma unroll
@@ -379,8 +429,8 @@ constexpr int kP4NumCfgs = sizeof(kP4Cfgs) / sizeof(kP4Cfgs[0]);
 
 template <int C, int EPI, bool RMS>
 int p4_launch(const P4Args& a, hipStream_t s) {
-  hipLaunchKernelGGL((pgemm4_kernel<kP4Cfgs[C].fp, kP4Cfgs[C].fq, EPI, RMS>), dim3(a.nwg), dim3(256), 0,
-                     s, a);
+  hipLaunchKernelGGL((pgemm4_kernel<kP4Cfgs[C].fp, kP4Cfgs[C].fq, EPI, RMS>), dim3(a.nwg),
+                     dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 template <int C>
