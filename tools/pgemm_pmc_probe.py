@@ -19,12 +19,16 @@ def main():
     ap.add_argument("--m", type=int, default=8192)
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--plan", default=None, help="kernel,cfg,splits,group_m instead of the tuned plan (e.g. pgemm4,0,1,8)")
     a = ap.parse_args()
     name, N, K, epi = next(s for s in shapes(a.tp) if s[0] == a.proj)
     rows = 2 * N if epi == ops.EPI_SWIGLU else N
     w = torch.empty(rows, K, dtype=torch.bfloat16, device="cuda").uniform_(-0.05, 0.05)
     x = torch.empty(a.m, K, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1)
     plan, _ = ops.pgemm_plan_for(a.m, N, K, epi, False)
+    if a.plan:
+        k_, c_, s_, g_ = a.plan.split(",")
+        plan = (k_, int(c_), int(s_), int(g_))
     kern, cfg, sp, gm = plan
     print(f"{name} M={a.m} N={N} K={K} plan {plan}", flush=True)
     for _ in range(a.reps):
