@@ -57,7 +57,7 @@ struct P4Args {
   float eps;
 };
 
-template <int FP, int FQ, int EPI, bool RMS>
+template <int FP, int FQ, int EPI, bool RMS, bool K64 = false>
 __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
   constexpr int BP = 32 * FP, BQ = 32 * FQ;          // weight rows, tokens per tile (2 x 2 waves)
   constexpr int ROWS = BP + BQ;
@@ -65,9 +65,12 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
   constexpr int G = ROWS / 64;                       // 16-byte DMA instructions per thread per k-step
   constexpr int NSLOT = 4;
   static_assert(ROWS % 64 == 0 && G >= 1, "tile shape");
+  // K64: 64-deep LDS stages of 128-byte rows, two of them (the same 4 x 32-deep bytes): every LDS-DMA instruction
+  // moves 8 whole 128-byte rows instead of 16 half rows, and one barrier covers 2 x FP x FQ MFMAs
+  constexpr int RING = K64 ? 2 * ROWS * 128 : NSLOT * SUB;
 #if defined(__HIP_DEVICE_COMPILE__)
-  __shared__ __attribute__((aligned(16))) char lds[NSLOT * SUB + BQ * 8];
-  float* rss = reinterpret_cast<float*>(lds + NSLOT * SUB);   // [2][BQ] row sums of squares (wave rows)
+  __shared__ __attribute__((aligned(16))) char lds[RING + BQ * 8];
+  float* rss = reinterpret_cast<float*>(lds + RING);   // [2][BQ] row sums of squares (wave rows)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -218,7 +221,6 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
     squares(Bc, (s & 1) == wr);
   };
 
-  // n is even (the host splits K in 64-deep units): the loop body is two k-steps with fixed register sets
   {   // the inline-asm MFMAs are opaque to the hazard recognizer: every zeroed accumulator passes through an asm
     // tied to it after its write, all before the first MFMA (volatile asm keeps its order)
     asm volatile("s_nop 1" ::: "memory");
@@ -227,6 +229,109 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
 #pragma unroll
       for (int j = 0; j < FQ; ++j) asm volatile("s_nop 0" : "+a"(acc[i][j]));
   }
+  if constexpr (K64) {
+    // ---- 64-deep stages: stage u in slot u & 1, row r at r * 128 bytes, 16-byte chunk c of row r at slot
+    // c ^ ((r >> 1) & 7) (the swizzle is applied on the per-lane global source, the DMA image is lane-linear).
+    // Sub-step h (k 32 h .. 32 h + 31) of a fragment row li = chunks 4 h + g.  Register sets: R0 = (A0, B0) holds
+    // sub-step 0, R1 = (A1, B1) sub-step 1.  Per stage s after the barrier: phase A = the MFMAs of (s - 1, 1) on R1
+    // with the reads of (s, 0) into R0 and the LDS-DMA of stage s + 1 (into the slot of s - 1, whose reads every
+    // wave retired before the barrier) spread between them; phase P = the MFMAs of (s, 0) on R0 with the reads of
+    // (s, 1) into R1.
+    constexpr int SUB2 = ROWS * 128, G2 = ROWS / 32, GW2 = BP / 32;
+    const int n2 = n / 2;
+    uint32_t off2[G2];
+#pragma unroll
+    for (int j = 0; j < G2; ++j) {
+      const int p = j * 256 + tid, r = p >> 3, c = (p & 7) ^ ((r >> 1) & 7);
+      const uint32_t col = (uint32_t)(c * 16 + ks0 * 64);
+      if (j < GW2) {
+        const int w = r / (BP / 2), q = r % (BP / 2);
+        int row;
+        if constexpr (EPI == P4_SWIGLU) {
+          const int f = min(nt * (BP / 2) + w * (BP / 4) + (q % (BP / 4)), a.N_out - 1);
+          row = q < BP / 4 ? f : a.half_rows + f;
+        } else {
+          row = min(nt * BP + r, a.N_out - 1);
+        }
+        off2[j] = (uint32_t)row * a.kbytes + col;
+      } else {
+        off2[j] = (uint32_t)min(mt * BQ + (r - BP), a.M - 1) * a.kbytes + col;
+      }
+    }
+    auto dma2 = [&](int u, int d) {   // instruction d of stage u
+      __builtin_amdgcn_global_load_lds((d < GW2 ? a.W : a.x) + (off2[d] + (uint32_t)u * 128u),
+                                       (__attribute__((address_space(3))) void*)(lds + (u & 1) * SUB2 + wid * 1024 +
+                                                                                 d * 4096),
+                                       16, 0, 0);
+    };
+    const int lo0 = li * 128 + ((g ^ (li >> 1)) << 4), lo1 = li * 128 + (((4 + g) ^ (li >> 1)) << 4);
+    const int pb2 = wr * (BP / 2) * 128, qb2 = (BP + wc * (BQ / 2)) * 128;
+    auto laddr = [&](int u, int off) {
+      return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)(lds + (u & 1) * SUB2 + off));
+    };
+    auto rd2 = [&](int u, int h, bf16x8* A, bf16x8* B) {   // whole sub-step, not interleaved (prologue / tail)
+      const uint32_t la = laddr(u, pb2 + (h ? lo1 : lo0)), lb = laddr(u, qb2 + (h ? lo1 : lo0));
+#pragma unroll
+      for (int f = 0; f < FP; ++f) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A[f]) : "v"(la), "i"(f * 2048));
+#pragma unroll
+      for (int f = 0; f < FQ; ++f) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(B[f]) : "v"(lb), "i"(f * 2048));
+    };
+    // 64 MFMAs on (Ac, Bc) with the reads of sub-step h of stage u into (An, Bn) and (dma) the G2 instructions of
+    // stage u + 1 spread between them
+    auto phase = [&](const bf16x8* Ac, const bf16x8* Bc, int u, int h, bf16x8* An, bf16x8* Bn, bool rd, bool dma) {
+      constexpr int MF = FP * FQ, DR = FP + FQ;
+      const uint32_t la = laddr(u, pb2 + (h ? lo1 : lo0)), lb = laddr(u, qb2 + (h ? lo1 : lo0));
+#pragma unroll
+      for (int i = 0; i < FP; ++i)
+#pragma unroll
+        for (int j = 0; j < FQ; ++j) {
+          const int k = i * FQ + j;
+#pragma unroll
+          for (int d = 0; d < G2; ++d)
+            if (k == d * MF / G2 && dma) dma2(u + 1, d);
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(Ac[i]), "v"(Bc[j]));
+#pragma unroll
+          for (int r = 0; r < DR; ++r)
+            if (k == 4 + r * (MF - 8) / DR && rd) {   // the first read 4 MFMAs in: the previous phase's
+                                                       // MFMAs on these registers are long issued
+              if (r < FP)
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(An[r]) : "v"(la), "i"(r * 2048));
+              else
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Bn[r - FP]) : "v"(lb), "i"((r - FP) * 2048));
+            }
+        }
+    };
+    // prologue: stages 0 (and 1) in flight, stage 0 visible, (0, 0) read
+#pragma unroll
+    for (int d = 0; d < G2; ++d) dma2(0, d);
+    p4_vmcnt<0>();
+    p4_sync();
+    rd2(0, 0, A0, B0);
+    if (n2 > 1) {
+#pragma unroll
+      for (int d = 0; d < G2; ++d) dma2(1, d);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    phase(A0, B0, 0, 1, A1, B1, true, false);           // P_0: (0, 0) on R0, read (0, 1)
+    squares(B0, wr == 0);
+    for (int s2 = 1; s2 < n2; ++s2) {
+      p4_vmcnt<0>();                                     // stage s2 landed (this wave's DMA)
+      p4_sync();                                         // ... for every wave; (s2 - 1, 1) reads retired
+      __builtin_amdgcn_sched_barrier(0);
+      phase(A1, B1, s2, 0, A0, B0, true, s2 + 1 < n2);   // A: (s2 - 1, 1) on R1, read (s2, 0), DMA stage s2 + 1
+      squares(B1, wr == 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      phase(A0, B0, s2, 1, A1, B1, true, false);         // P: (s2, 0) on R0, read (s2, 1)
+      squares(B0, wr == 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    phase(A1, B1, 0, 0, A0, B0, false, false);           // the last sub-step, (n2 - 1, 1), on R1
+    squares(B1, wr == 1);
+  } else {
+  // n is even (the host splits K in 64-deep units): the loop body is two k-steps with fixed register sets
   issue(0);
   issue(1);
   if (n > 2) issue(2);
@@ -245,6 +350,7 @@ __global__ void __launch_bounds__(256, 1) pgemm4_kernel(P4Args a) {
   }
   step_tail(s, A0, B0, A1, B1);
   step_tail(s + 1, A1, B1, A0, B0);
+  }
   p4_vmcnt<0>();
   {   // ... and the last MFMAs' results wait out the MFMA latency before the epilogue reads them:
     // the padding, then one tied empty asm per accumulator (so no read is hoisted above the padding)
@@ -417,6 +523,7 @@ using namespace k8sllm;
 namespace {
 struct P4Cfg {
   int fp, fq;
+  bool k64 = false;
 };
 // tile configurations: BP = 32 FP weight rows x BQ = 32 FQ tokens, 4 waves of (BP / 2) x (BQ / 2)
 constexpr P4Cfg kP4Cfgs[] = {
@@ -424,12 +531,15 @@ constexpr P4Cfg kP4Cfgs[] = {
     {8, 4},   // 1: 256 x 128
     {4, 8},   // 2: 128 x 256
     {4, 4},   // 3: 128 x 128
+    {8, 8, true},   // 4: 256 x 256, 64-deep LDS stages (128-byte rows): 1.01-1.10x of config 0 on 29 of 30 70B
+                    // TP=1 / TP=8 shapes; the 64-deep forms of configs 1 and 2 were within 2 % of them and were dropped
+                    // (profiles/pgemm4_asm_r6.txt)
 };
 constexpr int kP4NumCfgs = sizeof(kP4Cfgs) / sizeof(kP4Cfgs[0]);
 
 template <int C, int EPI, bool RMS>
 int p4_launch(const P4Args& a, hipStream_t s) {
-  hipLaunchKernelGGL((pgemm4_kernel<kP4Cfgs[C].fp, kP4Cfgs[C].fq, EPI, RMS>), dim3(a.nwg),
+  hipLaunchKernelGGL((pgemm4_kernel<kP4Cfgs[C].fp, kP4Cfgs[C].fq, EPI, RMS, kP4Cfgs[C].k64>), dim3(a.nwg),
                      dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
