@@ -403,7 +403,13 @@ def _vocab_parallel_rank(rank, world):
 def test_vocab_parallel_sampling_equals_gathered_rehearsal(world):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    res = run_ranks(_vocab_parallel_rank, world, env={"K8S_TP_BACKEND": "gloo", "K8S_TP_COMM": "xgmi"}, timeout_s=300)
+    # K8S_FUSED_AR=0: this test is about sampling; the fused GEMV + all-reduce (tested on its own above and in
+    # test_multigpu_70b.py) launches full grids whose workgroups wait for the peers' partials, and with every rank on
+    # ONE device those grids of the ranks that arrived first can hold the CUs the last rank's kernel needs -- the
+    # flake this test showed in 3 of 6 full-suite runs of round 6 (the harness's stack dump: the last rank waiting on
+    # its own GPU event while the others timed out in the collective).  One process per GPU has no such contention.
+    res = run_ranks(_vocab_parallel_rank, world, env={"K8S_TP_BACKEND": "gloo", "K8S_TP_COMM": "xgmi",
+                                                      "K8S_FUSED_AR": "0"}, timeout_s=300)
     r0 = res[0]
     assert r0["1"]["replays"] > 0 and r0["1"]["mixed_steps"] >= 1, r0["1"]
     assert (r0["1"]["tokens"], r0["1"]["mixed"]) == (r0["0"]["tokens"], r0["0"]["mixed"]), r0
