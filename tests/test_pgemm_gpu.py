@@ -212,6 +212,24 @@ def test_pgemm4_exact_small_integers_every_config():
             assert torch.equal(y, exp), f"cfg {cfg} splits {splits}: {(y - exp).abs().max().item()}"
 
 
+def test_pgemm4_exact_short_k_every_config():
+    """1-4 k-steps of 64 per slice: the 64-deep-stage configuration's prologue-only, one-loop-iteration and tail paths
+    (and the 32-deep ones' short loops); exact integer data."""
+    for cfg, (bp, bq, _lds) in enumerate(ops.pgemm4_configs()):
+        M, N = bq + 8, bp + 20
+        for K in (64, 128, 256):
+            x = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+            w = (torch.arange(N * K, device=DEV).view(N, K) % 5 - 2).to(torch.bfloat16)
+            w[:, 3] += torch.arange(N, device=DEV).to(torch.bfloat16) % 3
+            exp = x.float() @ w.float().t()
+            for splits in (1, 2):
+                if splits > K // 64:
+                    continue
+                y = ops.pgemm4(x, w, ops.EPI_F32, cfg=cfg, splits=splits)
+                torch.cuda.synchronize()
+                assert torch.equal(y, exp), f"cfg {cfg} K {K} splits {splits}: {(y - exp).abs().max().item()}"
+
+
 @pytest.mark.parametrize("epi", [ops.EPI_BF16, ops.EPI_F32, ops.EPI_SWIGLU])
 def test_pgemm4_every_config(epi):
     torch.manual_seed(0)
